@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""Headline benchmark: batched Metropolis-Hastings on the C2 workload of BASELINE.json.
+
+  python bench.py [--gpus N --steps K --warmup W]     (N > 1: launched by torch.distributed.run)
+
+Workload (BASELINE.json configs[1]): D=32 diagonal-Gaussian log-target, isotropic Gaussian
+proposal s = 2.38/sqrt(D) * median(sigma), flat box prior [-10, 10]^32, 65,536 independent chains
+per GPU (weak scaling), starts drawn from the target.  One bench "step" = one fused kernel launch
+of --sweeps MH sweeps over every chain (default 100), so the default --warmup 10 --steps 100 is
+the C2 job: nbin = 1,000 burn-in sweeps, then 10,000 recorded sweeps whose samples are folded on
+the device into Welford moments and harmonic-mean partials.  The timed region covers the K steps
+plus the end-of-run reduction (tile kernel, RCCL all-gather of tile partials, host combine).
+
+Prints ONE JSON line (rank 0).  `value` = whole-job MH steps/s over all GPUs.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(ROOT, "mcmc-ocaml_amd"), os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+METRIC = "MH steps/s (whole node) + |Δlog-evidence|, D=32 Gaussian, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def c2_target(D, seed=42):
+    rng = np.random.default_rng(seed)
+    mu = rng.uniform(-1.0, 1.0, D)
+    sg = rng.uniform(0.5, 2.0, D)
+    s = 2.38 / math.sqrt(D) * float(np.median(sg))
+    return mu, sg, s
+
+
+def analytic_log_z(mu, sg, lo=-10.0, hi=10.0):
+    """log Z = -D log(hi-lo) + sum_d log(Phi((hi-mu)/s) - Phi((lo-mu)/s))."""
+    phi = lambda z: 0.5 * math.erfc(-z / math.sqrt(2.0))
+    return sum(math.log(phi((hi - m) / s) - phi((lo - m) / s)) - math.log(hi - lo)
+               for m, s in zip(mu, sg))
+
+
+def cpu_baseline(args, mu, sg, s):
+    """Oracle (C restatement, -O2) on a bounded sample of the same workload, all granted cores."""
+    import oracle as O
+    D = args.ndim
+    threads = int(os.environ.get("MCG_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    m = O.Model(D, 1, np.concatenate([mu, sg]), 1,
+                np.concatenate([-10 * np.ones(D), 10 * np.ones(D), [-D * math.log(20.0)]]),
+                1, [s])
+    rng = np.random.default_rng(7)
+
+    def run(nch, nsteps):
+        x0 = rng.normal(mu[:, None], sg[:, None], size=(D, nch))
+        ll = np.array([m.loglik(x0[:, i]) for i in range(nch)])
+        lp = np.full(nch, m.logprior(x0[:, 0]))
+        t = time.perf_counter()
+        O.mh_run(m, 1, x0, ll, lp, nbin=nsteps, nskip=1, n_rec=1, record_x=False, record_llp=False,
+                 record_accept=False, accumulate=False, nthreads=threads)
+        return time.perf_counter() - t
+
+    nch = 64 * threads * 4
+    dt = run(nch, 20)
+    rate = nch * 20 / dt
+    nsteps = max(20, int(args.cpu_seconds * rate / nch))
+    dt = run(nch, nsteps)
+    return dict(value=nch * nsteps / dt, unit="MH steps/s", cores=threads, kind="port",
+                sample="%d chains x %d steps of the C2 target (oracle/oracle.c, -O2, %d threads)"
+                       % (nch, nsteps, threads))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--sweeps", type=int, default=100, help="MH sweeps per bench step (one launch)")
+    ap.add_argument("--chains", type=int, default=65536, help="chains per GPU")
+    ap.add_argument("--ndim", type=int, default=32)
+    ap.add_argument("--lanes", type=int, default=0, help="lanes per chain (0 = auto)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=1.5,
+                    help="wall seconds of the CPU baseline sample (x threads = CPU work)")
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+
+    from mcmc_amd import Context, targets as T
+    from mcmc_amd.context import combine_tiles
+
+    D, N, S = args.ndim, args.chains, args.sweeps
+    mu, sg, s = c2_target(D)
+    lik, pri, prop = T.diag_gauss(mu, sg), T.box(-10 * np.ones(D), 10 * np.ones(D)), T.gauss(s)
+    ctx = Context(seed=1, device=local, chain_offset=rank * N, lanes_per_chain=args.lanes)
+    ctx.set_model(lik, pri, prop)
+    x0 = np.random.default_rng(1000 + rank).normal(mu[:, None], sg[:, None], size=(D, N))
+    ctx.init(x0)
+
+    def barrier():
+        ctx.sync()
+        torch.cuda.synchronize(dev)
+        if dist:
+            tdist.barrier()
+            torch.cuda.synchronize(dev)
+
+    # warmup = burn-in (nbin = W*S sweeps); record 0 = post-burn-in state (mcmc.ml:66)
+    ctx.run(nbin=args.warmup * S, nskip=1, n_rec=1, record_x=False, record_llp=False,
+            record_accept=False, accumulate=True)
+    ctx.set_timing(True)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.run(nbin=0, nskip=1, n_rec=S, record_x=False, record_llp=False, record_accept=False,
+                accumulate=True, append=True)
+    # end-of-run reduction: tile kernel -> RCCL all-gather of tile partials -> host combine
+    tiles = ctx.tile_stats()
+    if dist:
+        t = torch.from_numpy(tiles).to(dev)
+        out = [torch.empty_like(t) for _ in range(world)]
+        tdist.all_gather(out, t)
+        tiles = torch.cat(out).cpu().numpy()
+    mean, sd, log_z_hm = combine_tiles(D, tiles)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    timing = ctx.kernel_timing("mh")
+    acc, rej = ctx.counters()
+
+    steps_total = float(N) * world * S * args.steps
+    value = steps_total / elapsed
+    bytes_per_step = 8.0 * (D + 2)                     # chain-state read
+    per_launch = timing["total_ms"] / max(timing["launches"], 1)
+    launch_steps = float(N) * S                        # one launch = S sweeps of this rank
+    achieved = launch_steps * bytes_per_step / (per_launch * 1e-3) / 1e9
+    lz_true = analytic_log_z(mu, sg)
+    if rank != 0:
+        if dist:
+            tdist.barrier()
+            tdist.destroy_process_group()
+        return
+    cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(args, mu, sg, s)
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "MH steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (C2 target: mu~U[-1,1], sigma~U[0.5,2], seed 42; starts ~ target)",
+        "config": {"workload": "C2 D=%d diagonal-Gaussian, %d chains/GPU, isotropic Gaussian "
+                               "proposal, box prior [-10,10]^D, %d MH sweeps per step (one fused launch), "
+                               "on-device Welford moments + harmonic-mean evidence, RCCL all-gather"
+                               % (D, N, S),
+                   "ndim": D, "chains_per_gpu": N, "sweeps_per_step": S,
+                   "lanes_per_chain": ctx_lanes(ctx), "parallelism": "chains sharded, dp%d" % world},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "mcg::mh_kernel<32,P,DIAG_GAUSS,GAUSS>",
+                     "bytes_per_step": bytes_per_step, "avg_launch_ms": per_launch,
+                     "launches": timing["launches"]},
+        "cpu_baseline": cpu,
+        "accept_frac": acc / max(acc + rej, 1),
+        "log_evidence": {"harmonic_mean": log_z_hm, "analytic": lz_true,
+                         "abs_delta": abs(log_z_hm - lz_true),
+                         "note": "harmonic-mean estimator (evidence.ml:101-107); high variance at D=32"},
+        "posterior_check": {"max_abs_mean_err": float(np.max(np.abs(mean - mu))),
+                            "max_rel_sd_err": float(np.max(np.abs(sd / sg - 1)))},
+    }
+    print(json.dumps(line), flush=True)
+    if dist:
+        tdist.barrier()
+        tdist.destroy_process_group()
+
+
+def ctx_lanes(ctx):
+    import os as _os
+    return int(_os.environ.get("MCG_LANES_PER_CHAIN", "0")) or "auto"
+
+
+if __name__ == "__main__":
+    main()

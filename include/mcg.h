@@ -1,0 +1,214 @@
+/*
+ * mcg.h -- C-ABI of the MI355X-native batched sampler (libmcg.so).
+ *
+ * Drop-in boundary for farr/mcmc-ocaml's hot path.  Every entry point replaces a reference
+ * interface (cited file:line, paths relative to the reference root); an OCaml host binds these
+ * through ctypes / C stubs, the Python mirror in mcmc-ocaml_amd/mcmc_amd does the
+ * same through ctypes.  Plain pointers and sizes only; no torch / HIP types cross this boundary.
+ *
+ * Conventions
+ *   - Caller owns every host buffer; the context owns every device buffer.
+ *   - Chain / point coordinates cross the boundary structure-of-arrays: x[d*N + i] ([D][N], C
+ *     order) -- maps 1:1 to an OCaml Bigarray.Array2 c_layout or a numpy (D, N) array.
+ *   - Return 0 on success, a negative MCG_E* code on error (the OCaml stub raises
+ *     Invalid_argument for MCG_EINVAL, Failure for MCG_EFAIL, as the reference does at
+ *     kd_tree.ml:70,97 / nested.ml:71).  mcg_last_error() gives the message.
+ *   - No globals: the reference's global accept/reject counters (mcmc.ml:27-28) and global
+ *     Random state become per-context state, so contexts are reentrant (one per host thread).
+ *   - The reference's OCaml closures (log_likelihood, log_prior, jump_proposal, log_jump_prob;
+ *     mcmc.mli:58-60) become data descriptors (kind + parameter vector) that a GPU kernel can run.
+ */
+#ifndef MCG_H
+#define MCG_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MCG_ABI_VERSION 1
+
+/* ---- status codes ---- */
+enum {
+  MCG_OK = 0,
+  MCG_EINVAL = -1,    /* Invalid_argument */
+  MCG_EFAIL = -2,     /* Failure (e.g. nested.ml:70-72 constraint violation) */
+  MCG_EDEVICE = -3,   /* HIP runtime error / no device / extension not loaded */
+  MCG_ENOMEM = -4,
+  MCG_ESTATE = -5     /* call out of order (e.g. mcg_run before mcg_init) */
+};
+
+/* ---- likelihood kinds (replace the log_likelihood closure, mcmc.mli:58) ----
+   parameter layouts (doubles):
+   DIAG_GAUSS    : mu[D], sigma[D]        Stats.log_multi_gaussian (stats.ml:103-108)
+   FULLCOV_GAUSS : mu[D], U[D*D]          U = upper Cholesky factor of the precision, row major;
+                                          ll = -D/2 log 2pi + sum log U_ii - 1/2 |U (x-mu)|^2
+   GAUSS_SHELL   : c[D], r, w             ll = -log(sqrt(2 pi) w) - (|x-c| - r)^2 / (2 w^2)
+   GAUSS_DATA    : nd, data[nsamp*nd]     D = 2 nd, x = (mu[nd], sigma[nd]); sum over data of
+                                          Stats.log_gaussian (bin/gaussian_cauchy.ml:149-164)
+   CAUCHY_DATA   : nd, data[nsamp*nd]     same with Stats.log_cauchy
+   FLAT          : (none)                 ll = 0
+*/
+enum {
+  MCG_LIK_FLAT = 0,
+  MCG_LIK_DIAG_GAUSS = 1,
+  MCG_LIK_FULLCOV_GAUSS = 2,
+  MCG_LIK_GAUSS_SHELL = 3,
+  MCG_LIK_GAUSS_DATA = 4,
+  MCG_LIK_CAUCHY_DATA = 5
+};
+
+/* ---- prior kinds (replace the log_prior closure) ----
+   FLAT     : (none)              lp = 0
+   BOX      : lo[D], hi[D], lp_in lp = lp_in if lo <= x <= hi for all d (inclusive) else -inf
+   OPEN_BOX : lo[D], hi[D], lp_in same with strict inequalities (test/nested_test.ml:23-28)
+   For nested sampling the prior must be a box: draw_prior = uniform in [lo, hi]. */
+enum { MCG_PRIOR_FLAT = 0, MCG_PRIOR_BOX = 1, MCG_PRIOR_OPEN_BOX = 2 };
+
+/* ---- proposal kinds (replace jump_proposal / log_jump_prob, mcmc.mli:58-60) ----
+   GAUSS        : s[1] or s[D]        y = x + s*z, z ~ N(0,1) per dim (symmetric)
+   WRAP_UNIFORM : lo[D], hi[D], dx[D] Mcmc.uniform_wrapping per dim (mcmc.ml:187-196), symmetric
+   KD_INTERP    : set with mcg_set_kd_proposal; independence proposal Interpolate_pdf.draw with
+                  log_jump_prob _ y = log (jump_prob y)  (interpolate_pdf.ml:114-142)
+   DE           : used by nested sampling (mcmc.ml:198-218) */
+enum { MCG_PROP_GAUSS = 1, MCG_PROP_WRAP_UNIFORM = 2, MCG_PROP_KD_INTERP = 3, MCG_PROP_DE = 4 };
+
+/* ---- context ---- */
+enum {
+  MCG_FLAG_NESTED_FIXED_STOP = 1u << 0  /* use log(1/n) instead of the nested.ml:140 quirk */
+};
+
+typedef struct {
+  int32_t device;          /* HIP device ordinal */
+  uint32_t flags;          /* MCG_FLAG_* */
+  uint64_t seed;           /* Philox key (replaces Random.init / self_init) */
+  uint64_t chain_offset;   /* global id of this context's chain 0 (multi-GPU sharding) */
+  int32_t lanes_per_chain; /* 0 = auto (1, 2, 4 or 8 lanes share one chain's dimensions) */
+  int32_t steps_per_launch;/* 0 = auto (MH steps fused into one kernel launch) */
+} mcg_opts;
+
+typedef struct mcg_ctx mcg_ctx;
+
+int mcg_ctx_create(mcg_ctx** out, const mcg_opts* opts);
+void mcg_ctx_destroy(mcg_ctx* ctx);
+const char* mcg_last_error(const mcg_ctx* ctx);
+int mcg_abi_version(void);
+/* name of the compiled device target ("gfx950") */
+const char* mcg_device_arch(void);
+
+/* ---- model descriptors ---- */
+int mcg_set_likelihood(mcg_ctx* ctx, int32_t kind, int32_t ndim, const double* params, size_t n);
+int mcg_set_prior(mcg_ctx* ctx, int32_t kind, const double* params, size_t n);
+int mcg_set_proposal(mcg_ctx* ctx, int32_t kind, const double* params, size_t n);
+/* Interpolate_pdf.make pts low high (interpolate_pdf.ml:111-112): kD tree built on the host
+   with Kd_tree.tree_of_objects semantics (kd_tree.ml:155-175), flattened into HBM. */
+int mcg_set_kd_proposal(mcg_ctx* ctx, const double* pts /*[M][D] row-major*/, int64_t M,
+                        const double* low, const double* high);
+
+/* flattened tree of the last mcg_set_kd_proposal (pre-order; left child = node + 1):
+   node_dim (-1 = leaf), node_split, node_right, node_leaf (-1 = internal), leaf_count,
+   leaf_box [nleaves][2][D] (low then high), leaf_logq = log jump_prob inside the leaf */
+int mcg_kd_info(mcg_ctx* ctx, int64_t* nnodes, int64_t* nleaves);
+int mcg_kd_export(mcg_ctx* ctx, int32_t* node_dim, double* node_split, int32_t* node_right,
+                  int32_t* node_leaf, int32_t* leaf_count, double* leaf_box, double* leaf_logq);
+
+/* ---- chain state (like_prior / mcmc_sample records, mcmc.ml:17-25) ----
+   x_soa [D][N]; ll, lp may be NULL -> evaluated on the device (mcmc.ml:59-61). */
+int mcg_init(mcg_ctx* ctx, int64_t nchains, const double* x_soa, const double* ll,
+             const double* lp);
+int mcg_get_state(mcg_ctx* ctx, double* x_soa, double* ll, double* lp);
+
+/* ---- Mcmc.mcmc_array (mcmc.ml:58-72) over every chain ----
+   nbin burn-in steps, record 0 = post-burn-in state, then (n_rec-1)*nskip steps recording
+   every nskip-th.  Records stay in device memory (read with mcg_get_records); with
+   accumulate != 0 every recorded sample is folded into per-chain running statistics (Welford
+   moments + log-space harmonic-mean partials) that mcg_stats reduces. */
+typedef struct {
+  int64_t nbin;
+  int64_t nskip;
+  int64_t n_rec;
+  int32_t record_x;        /* keep x of recorded samples */
+  int32_t record_llp;      /* keep ll, lp of recorded samples */
+  int32_t record_accept;   /* keep the accept/reject bitmap of every step */
+  int32_t accumulate;      /* fold recorded samples into running statistics */
+  int32_t append;          /* continue the previous run's records/statistics: n_rec*nskip
+                              steps, recording after every nskip-th (no initial record) */
+} mcg_run_opts;
+
+int mcg_run(mcg_ctx* ctx, const mcg_run_opts* opts);
+/* rec_x [n_rec][D][N], rec_ll / rec_lp [n_rec][N], accept_bits [nsteps][ceil(N/64)] (bit c of
+   row t = chain c accepted at step t of the last run).  Any pointer may be NULL. */
+int mcg_get_records(mcg_ctx* ctx, double* rec_x, double* rec_ll, double* rec_lp,
+                    uint64_t* accept_bits);
+int64_t mcg_last_run_steps(const mcg_ctx* ctx);
+
+/* ---- counters (mcmc.ml:27-35) ---- */
+int mcg_get_counters(mcg_ctx* ctx, uint64_t* naccept, uint64_t* nreject);
+int mcg_reset_counters(mcg_ctx* ctx);
+
+/* ---- reductions over the recorded samples of the last run ----
+   Tile partials: 256-chain tiles reduced on the device by a fixed pairwise tree (layout per
+   tile: n, mean[D], m2[D], hm_max, hm_sum; 2D+3 doubles).  Tiles are independent of the GPU
+   count, so an all-gather of every rank's tiles followed by mcg_combine_tiles gives
+   bit-identical results on 1/2/4/8 GPUs. */
+int64_t mcg_num_tiles(const mcg_ctx* ctx);
+int mcg_tile_stats(mcg_ctx* ctx, double* tiles /*[ntiles][2D+3]*/);
+/* device pointer of the tile partials (for a device-side all-gather, e.g. RCCL) */
+int mcg_tile_stats_device(mcg_ctx* ctx, void** dev_ptr, int64_t* ntiles);
+/* Stats.multi_mean / multi_std (stats.ml:58-87, std with n-1) and the harmonic-mean evidence
+   (evidence.ml:101-107) in log space: log Z = log n - logsumexp(-ll). */
+int mcg_combine_tiles(int32_t ndim, int64_t ntiles, const double* tiles, double* mean, double* sd,
+                      double* log_z_hm);
+/* single-context convenience: tiles + combine */
+int mcg_stats(mcg_ctx* ctx, double* mean, double* sd, double* log_z_hm);
+
+/* ---- Nested.nested_evidence (nested.ml:122-146) ----
+   Uses the context's likelihood and (box) prior; the DE proposal (mcmc.ml:198-218) runs inside.
+   k = live points retired per generation (k = 1 is the reference algorithm; k > 1 runs k
+   constrained walkers in parallel and shrinks the volume with live counts n, n-1, ..., n-k+1). */
+typedef struct {
+  int64_t nlive;          /* default 1000 */
+  int64_t nmcmc;          /* default 1000 */
+  int64_t k;              /* default 1 */
+  double epsrel;          /* default 0.01 */
+  double mode_hop;        /* default 0.1 */
+  int64_t max_dead;       /* safety cap (0 = 1000 * nlive) */
+} mcg_nested_opts;
+
+typedef struct {
+  double log_ev;
+  double log_dev;
+  int64_t n_dead;
+  int64_t n_total;        /* n_dead + nlive */
+  int64_t n_gen;
+} mcg_nested_result;
+
+/* observer: called after each batch of generations with the newly retired points (batch form
+   of the per-point ?observer of nested.ml:136); may be NULL. */
+typedef void (*mcg_observer_fn)(void* user, const double* pts /*[n][D]*/, const double* ll,
+                                const double* lp, int64_t n);
+
+int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res,
+               mcg_observer_fn observer, void* user);
+/* all points of the last nested run (dead in retirement order, then live ascending in ll):
+   pts [n_total][D] row-major, ll, lp, log_wts [n_total] (nested_output, nested.ml:20) */
+int mcg_nested_get(mcg_ctx* ctx, double* pts, double* ll, double* lp, double* log_wts);
+/* Nested.log_total_error_estimate (nested.ml:148-150) */
+double mcg_log_total_error_estimate(double log_ev, double log_dev, int64_t nlive);
+
+/* ---- device timing of the dominant kernel (HIP events on the launch stream) ---- */
+typedef struct {
+  int64_t launches;
+  double total_ms;
+  double last_ms;
+} mcg_kernel_timing;
+int mcg_get_kernel_timing(mcg_ctx* ctx, const char* kernel, mcg_kernel_timing* out);
+int mcg_set_timing(mcg_ctx* ctx, int32_t enabled);
+/* synchronize the context's stream */
+int mcg_sync(mcg_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,533 @@
+// mcg_mh_kernel.h -- the batched Metropolis-Hastings kernel.
+//
+// Restates Mcmc.make_mcmc_sampler (mcmc.ml:37-56) driven by Mcmc.mcmc_array (mcmc.ml:58-72)
+// for N independent chains.  Layout and execution (DESIGN.md §MH kernel):
+//   * P lanes per chain (P in {1,2,4,8}); lane `sub` owns the dims of Philox calls
+//     c = sub, sub+P, ... (4 dims per call); chain state stays in VGPRs for the whole launch;
+//   * SoA state x[d][chain] in HBM is read once and written once per launch (coalesced);
+//   * one Philox4x32-10 call gives 4 proposal normals (two Box-Muller pairs) per lane;
+//   * the log-target is a canonical 8-accumulator sum (reduction tree fixed, P-independent);
+//   * the accept test `log u < ratio` (mcmc.ml:49) is packed per step into a 64-lane
+//     wavefront ballot -> accept bitmap row;
+//   * recorded samples optionally fold into per-chain Welford moments and log-space
+//     harmonic-mean partials (Evidence.evidence_harmonic_mean, evidence.ml:101-107).
+#pragma once
+#include "mcg_device.h"
+#include "mcg_math.h"
+#include "mcg.h"
+
+namespace mcg {
+
+template <int D, int P>
+struct Layout {
+  static_assert(P == 1 || P == 2 || P == 4 || P == 8, "P must divide 8");
+  static constexpr int NC = (D + 3) / 4;                 // Philox calls per step
+  static constexpr int NCL = (NC + P - 1) / P;           // calls owned by one lane
+  static constexpr int NL = NCL * 4;                     // local dims
+  static constexpr int NA = 8 / P;                       // local accumulators
+  static_assert(P == 1 || D % (4 * P) == 0, "P > 1 needs D % 4P == 0");
+  __device__ static __forceinline__ int dim(int sub, int i, int q) { return 4 * (sub + P * i) + q; }
+  __device__ static __forceinline__ bool valid(int sub, int i, int q) {
+    return P > 1 || (4 * i + q) < D;
+  }
+};
+
+// reduce the lane-local accumulators of the canonical tree across the P lanes of a chain
+template <int P>
+__device__ __forceinline__ double reduce_canon(const double* a) {
+  if constexpr (P == 1) {
+    return canon8(a);
+  } else if constexpr (P == 2) {
+    double c = (a[0] + a[2]) + (a[1] + a[3]);
+    return c + shfl_xor_d(c, 1);
+  } else if constexpr (P == 4) {
+    double b = a[0] + a[1];
+    double c = b + shfl_xor_d(b, 2);
+    return c + shfl_xor_d(c, 1);
+  } else {
+    double b = a[0] + shfl_xor_d(a[0], 4);
+    double c = b + shfl_xor_d(b, 2);
+    return c + shfl_xor_d(c, 1);
+  }
+}
+
+template <int P>
+__device__ __forceinline__ int and_lanes(int v) {
+  if constexpr (P >= 8) v &= __shfl_xor(v, 4, 64);
+  if constexpr (P >= 4) v &= __shfl_xor(v, 2, 64);
+  if constexpr (P >= 2) v &= __shfl_xor(v, 1, 64);
+  return v;
+}
+
+// gather bit (c*P) of a 64-lane ballot for c in [0, 64/P)
+template <int P>
+__device__ __forceinline__ uint64_t compress_ballot(uint64_t m) {
+  if constexpr (P == 1) {
+    return m;
+  } else if constexpr (P == 2) {
+    m &= 0x5555555555555555ull;
+    m = (m | (m >> 1)) & 0x3333333333333333ull;
+    m = (m | (m >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+    m = (m | (m >> 4)) & 0x00FF00FF00FF00FFull;
+    m = (m | (m >> 8)) & 0x0000FFFF0000FFFFull;
+    m = (m | (m >> 16)) & 0x00000000FFFFFFFFull;
+    return m;
+  } else if constexpr (P == 4) {
+    m &= 0x1111111111111111ull;
+    m = (m | (m >> 3)) & 0x0303030303030303ull;
+    m = (m | (m >> 6)) & 0x000F000F000F000Full;
+    m = (m | (m >> 12)) & 0x000000FF000000FFull;
+    m = (m | (m >> 24)) & 0x000000000000FFFFull;
+    return m;
+  } else {
+    m &= 0x0101010101010101ull;
+    m = (m | (m >> 7)) & 0x0003000300030003ull;
+    m = (m | (m >> 14)) & 0x0000000F0000000Full;
+    m = (m | (m >> 28)) & 0x00000000000000FFull;
+    return m;
+  }
+}
+
+// kD descent (Interpolate_pdf.find_cell, interpolate_pdf.ml:101-109): go left iff the point
+// is in the left child's inclusive box; boxes nest, so outside the root box -> always right.
+template <int D>
+__device__ __forceinline__ int kd_find_leaf(const KdNode* __restrict__ nodes,
+                                            const double* __restrict__ root, const double* v) {
+  bool inside = true;
+#pragma unroll
+  for (int d = 0; d < D; ++d) inside = inside && (v[d] >= root[d]) && (v[d] <= root[D + d]);
+  int node = 0;
+  for (int guard = 0; guard < 4096; ++guard) {
+    KdNode nd = nodes[node];
+    if (nd.dim < 0) return -1 - nd.dim;
+    double c = v[0];
+#pragma unroll
+    for (int d = 1; d < D; ++d) c = (nd.dim == d) ? v[d] : c;
+    bool left = inside && (c <= nd.split);
+    node = left ? node + 1 : nd.right;
+  }
+  return 0;
+}
+
+__device__ __forceinline__ double wrap_uniform(double xmin, double xmax, double dx, double x,
+                                               double u) {
+  double nx = x + (u - 0.5) * dx;                        // mcmc.ml:187-196
+  for (int it = 0; it < 64; ++it) {
+    if (nx < xmin) nx = xmin + (xmin - nx);
+    else if (nx >= xmax) nx = xmax - (nx - xmax);
+    else break;
+  }
+  return nx;
+}
+
+template <int D, int P, int LIK>
+__device__ __forceinline__ double eval_lik(const double* y, int sub, const MhArgs& a,
+                                           const double* __restrict__ q) {
+  using L = Layout<D, P>;
+  if constexpr (LIK == MCG_LIK_FLAT) {
+    return 0.0;
+  } else if constexpr (LIK == MCG_LIK_DIAG_GAUSS || LIK == MCG_LIK_GAUSS_SHELL) {
+    // DIAG: q = mu[D], isig[D], C        SHELL: q = c[D], R, iw, C
+    double A[L::NA];
+#pragma unroll
+    for (int j = 0; j < L::NA; ++j) A[j] = 0.0;
+#pragma unroll
+    for (int i = 0; i < L::NCL; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (!L::valid(sub, i, k)) continue;
+        int d = L::dim(sub, i, k);
+        double e = y[4 * i + k] - q[d];
+        if constexpr (LIK == MCG_LIK_DIAG_GAUSS) e = e * q[D + d];
+        A[i % L::NA] = fma(e, e, A[i % L::NA]);
+      }
+    double S = reduce_canon<P>(A);
+    if constexpr (LIK == MCG_LIK_DIAG_GAUSS) {
+      return q[2 * D] - 0.5 * S;
+    } else {
+      double r = psqrt(S);
+      double qq = (r - q[D]) * q[D + 1];
+      return q[D + 2] - 0.5 * qq * qq;
+    }
+  } else if constexpr (LIK == MCG_LIK_FULLCOV_GAUSS) {
+    static_assert(P == 1, "FULLCOV: one lane per chain");
+    // q = mu[D], C, U[D*D]
+    double r[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) r[d] = y[d] - q[d];
+    double A[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) A[j] = 0.0;
+    const double* __restrict__ U = q + D + 1;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      double t = 0.0;
+#pragma unroll
+      for (int j = i; j < D; ++j) t = fma(U[i * D + j], r[j], t);
+      A[(i >> 2) & 7] = fma(t, t, A[(i >> 2) & 7]);
+    }
+    return q[D] - 0.5 * canon8(A);
+  } else {
+    // GAUSS_DATA / CAUCHY_DATA (bin/gaussian_cauchy.ml:149-164), D = 2 nd, y = (mu, sigma)
+    static_assert(P == 1, "DATA: one lane per chain");
+    constexpr int ND = D / 2;
+    const double PI = 3.14159265358979323846;
+    double lterm[ND];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) lterm[j] = a.is_cauchy ? plog(PI * y[ND + j]) : plog(y[ND + j]);
+    double acc = 0.0;
+    for (int64_t i = 0; i < a.data_n; ++i) {
+#pragma unroll
+      for (int j = 0; j < ND; ++j) {
+        double dx = (q[i * ND + j] - y[j]) / y[ND + j];
+        double term;
+        if (a.is_cauchy) term = (0.0 - lterm[j]) - plog(1.0 + dx * dx);
+        else term = (-0.91893853320467274178 - lterm[j]) - 0.5 * dx * dx;
+        acc = acc + term;
+      }
+    }
+    return acc + 0.0;
+  }
+}
+
+template <int D, int P>
+__device__ __forceinline__ double eval_prior(const double* y, int sub, const MhArgs& a,
+                                             const double* __restrict__ q) {
+  using L = Layout<D, P>;
+  if (a.prior_kind == MCG_PRIOR_FLAT) return 0.0;
+  int inb = 1;
+  bool open = a.prior_kind == MCG_PRIOR_OPEN_BOX;
+#pragma unroll
+  for (int i = 0; i < L::NCL; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (!L::valid(sub, i, k)) continue;
+      int d = L::dim(sub, i, k);
+      double v = y[4 * i + k];
+      const int okc = (int)(v >= q[d]) & (int)(v <= q[D + d]);
+      const int oko = (int)(v > q[d]) & (int)(v < q[D + d]);
+      inb &= open ? oko : okc;
+    }
+  inb = and_lanes<P>(inb);
+  return inb ? q[2 * D] : -__builtin_inf();
+}
+
+template <int D, int P>
+struct AccumCfg {
+  // Welford accumulators live in LDS ([NL][256] doubles each, conflict-free) when they fit in
+  // 64 KiB per block, else they are read-modified-written in HBM at each record.
+  static constexpr bool kLds = Layout<D, P>::NL <= 16;
+  static constexpr int kLdsBytes = kLds ? 2 * Layout<D, P>::NL * 256 * 8 : 0;
+};
+
+template <int D, int P, int LIK, int PROP>
+__global__ void __launch_bounds__(256) mh_kernel(const MhArgs a) {
+  using L = Layout<D, P>;
+  constexpr bool kSeparable = (LIK == MCG_LIK_DIAG_GAUSS || LIK == MCG_LIK_GAUSS_SHELL ||
+                               LIK == MCG_LIK_FLAT) && PROP == MCG_PROP_GAUSS;
+  extern __shared__ double lds_acc[];
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int sub = (int)(tid & (P - 1));
+  const int64_t chain = tid / P;
+  const bool active = chain < a.N;
+  const int64_t c = active ? chain : 0;
+  const int64_t N = a.N;
+  const Rng rng{a.k0, a.k1};
+  const uint32_t gid = a.chain_offset + (uint32_t)c;
+  const int lane = threadIdx.x & 63;
+
+  double x[L::NL], y[L::NL];
+#pragma unroll
+  for (int i = 0; i < L::NCL; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      x[4 * i + k] = L::valid(sub, i, k) ? a.x[(int64_t)L::dim(sub, i, k) * N + c] : 0.0;
+  double ll = a.ll[c], lp = a.lp[c];
+  double lq = 0.0;
+  if constexpr (PROP == MCG_PROP_KD_INTERP) lq = a.kd_logq[kd_find_leaf<D>(a.kd_nodes, a.kd_root, x)];
+  unsigned long long na = 0;
+
+  const bool accum = (a.flags & RUNF_ACCUMULATE) != 0;
+  double hm_m = 0.0, hm_s = 0.0;
+  // accumulator slot j of this lane: LDS [j][threadIdx] or HBM [dim][chain]
+  auto acc_mean = [&](int i, int k) -> double& {
+    if constexpr (AccumCfg<D, P>::kLds) return lds_acc[(4 * i + k) * 256 + threadIdx.x];
+    else return a.mean[(int64_t)L::dim(sub, i, k) * N + c];
+  };
+  auto acc_m2 = [&](int i, int k) -> double& {
+    if constexpr (AccumCfg<D, P>::kLds) return lds_acc[(L::NL + 4 * i + k) * 256 + threadIdx.x];
+    else return a.m2[(int64_t)L::dim(sub, i, k) * N + c];
+  };
+  if (accum) {
+    if constexpr (AccumCfg<D, P>::kLds) {
+#pragma unroll
+      for (int i = 0; i < L::NCL; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          int64_t o = (int64_t)L::dim(sub, i, k) * N + c;
+          acc_mean(i, k) = L::valid(sub, i, k) ? a.mean[o] : 0.0;
+          acc_m2(i, k) = L::valid(sub, i, k) ? a.m2[o] : 0.0;
+        }
+    }
+    hm_m = a.hm_m[c];
+    hm_s = a.hm_s[c];
+  }
+
+  int64_t next_rec = a.next_rec, r = a.next_r;
+  auto record = [&](int64_t R) {
+    int64_t s = R - a.rec_base;
+    if ((a.flags & RUNF_RECORD_X) && active) {
+#pragma unroll
+      for (int i = 0; i < L::NCL; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (L::valid(sub, i, k)) a.rec_x[(s * D + L::dim(sub, i, k)) * N + c] = x[4 * i + k];
+    }
+    if ((a.flags & RUNF_RECORD_LLP) && active && sub == 0) {
+      a.rec_ll[s * N + c] = ll;
+      a.rec_lp[s * N + c] = lp;
+    }
+    if (accum) {
+      const double inv = 1.0 / (double)(R + 1);
+#pragma unroll
+      for (int i = 0; i < L::NCL; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (!L::valid(sub, i, k)) continue;
+          if constexpr (!AccumCfg<D, P>::kLds) { if (!active) continue; }
+          double& mu = acc_mean(i, k);
+          double& m2 = acc_m2(i, k);
+          const double xv = x[4 * i + k];
+          const double delta = xv - mu;
+          const double mnew = fma(delta, inv, mu);
+          m2 = fma(delta, xv - mnew, m2);
+          mu = mnew;
+        }
+      const double v = -ll;
+      if (R == 0) {
+        hm_m = v;
+        hm_s = 1.0;
+      } else {
+        const double e = (v == hm_m) ? 1.0 : pexp(-fabs(v - hm_m));
+        if (v > hm_m) {
+          hm_s = hm_s * e + 1.0;
+          hm_m = v;
+        } else {
+          hm_s = hm_s + e;
+        }
+      }
+    }
+  };
+
+  if (a.flags & RUNF_RECORD_INITIAL) {
+    record(r);
+    ++r;
+  }
+
+  for (int64_t t = 0; t < a.nsteps; ++t) {
+    const uint64_t T = a.step_base + (uint64_t)t;
+    const uint32_t tlo = (uint32_t)T, thi = (uint32_t)(T >> 32);
+    double lf = 0.0, lb = 0.0, lqy = 0.0;
+    // Re-read the (tiny, cache-resident) model constants every step: opaque pointers stop the
+    // compiler from hoisting D*5 doubles into registers, which would cap occupancy.
+    const double* qlik = a.lik;
+    const double* qpri = a.pri;
+    const double* qprop = a.prop;
+    asm volatile("" : "+s"(qlik), "+s"(qpri), "+s"(qprop));
+    double lly, lpy;
+    if constexpr (kSeparable) {
+      // fused: per Philox call -> 4 normals -> 4 proposed coordinates -> their terms of the
+      // canonical sum and of the box test.  Keeps only x, y and 8/P accumulators live.
+      double A[L::NA];
+#pragma unroll
+      for (int j = 0; j < L::NA; ++j) A[j] = 0.0;
+      int inb = 1;
+      const bool box = a.prior_kind != MCG_PRIOR_FLAT;
+      const bool open = a.prior_kind == MCG_PRIOR_OPEN_BOX;
+#pragma unroll
+      for (int i = 0; i < L::NCL; ++i) {
+        if (P == 1 && 4 * i >= D) continue;
+        asm volatile("" ::: "memory");
+        const int cc = sub + P * i;
+        const u32x4 w = rng(gid, tlo, (uint32_t)cc, TAG_MH, thi);
+        double z[4];
+        normal_pair(w.x, w.y, z[0], z[1]);
+        normal_pair(w.z, w.w, z[2], z[3]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (!L::valid(sub, i, k)) continue;
+          const int d = 4 * cc + k;
+          const double yv = x[4 * i + k] + qprop[d] * z[k];
+          y[4 * i + k] = yv;
+          if constexpr (LIK == MCG_LIK_DIAG_GAUSS) {
+            const double e = (yv - qlik[d]) * qlik[D + d];
+            A[i % L::NA] = fma(e, e, A[i % L::NA]);
+          } else if constexpr (LIK == MCG_LIK_GAUSS_SHELL) {
+            const double e = yv - qlik[d];
+            A[i % L::NA] = fma(e, e, A[i % L::NA]);
+          }
+          {
+            // branch-free box test; the host pads FLAT priors with a valid (unused) box
+            const double lo = qpri[d], hi = qpri[D + d];
+            const int okc = (int)(yv >= lo) & (int)(yv <= hi);
+            const int oko = (int)(yv > lo) & (int)(yv < hi);
+            inb &= open ? oko : okc;
+          }
+        }
+      }
+      if constexpr (LIK == MCG_LIK_FLAT) {
+        lly = 0.0;
+      } else {
+        const double S = reduce_canon<P>(A);
+        if constexpr (LIK == MCG_LIK_DIAG_GAUSS) {
+          lly = qlik[2 * D] - 0.5 * S;
+        } else {
+          const double rr = psqrt(S);
+          const double qq = (rr - qlik[D]) * qlik[D + 1];
+          lly = qlik[D + 2] - 0.5 * qq * qq;
+        }
+      }
+      inb = and_lanes<P>(inb);
+      lpy = !box ? 0.0 : (inb ? qpri[2 * D] : -__builtin_inf());
+    } else {
+      // ---- proposal (jump_proposal, mcmc.ml:41) ----
+      if constexpr (PROP == MCG_PROP_GAUSS) {
+#pragma unroll
+        for (int i = 0; i < L::NCL; ++i) {
+          const int cc = sub + P * i;
+          if (P == 1 && 4 * i >= D) continue;
+          const u32x4 w = rng(gid, tlo, (uint32_t)cc, TAG_MH, thi);
+          double z[4];
+          normal_pair(w.x, w.y, z[0], z[1]);
+          normal_pair(w.z, w.w, z[2], z[3]);
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (L::valid(sub, i, k)) y[4 * i + k] = x[4 * i + k] + qprop[L::dim(sub, i, k)] * z[k];
+        }
+      } else if constexpr (PROP == MCG_PROP_WRAP_UNIFORM) {
+        static_assert(P == 1, "WRAP: one lane per chain");
+#pragma unroll
+        for (int d = 0; d < D; d += 2) {
+          const u32x4 w = rng(gid, tlo, (uint32_t)(d >> 1), TAG_MH, thi);
+          y[d] = wrap_uniform(qprop[d], qprop[D + d], qprop[2 * D + d], x[d], u53(w.x, w.y));
+          if (d + 1 < D)
+            y[d + 1] = wrap_uniform(qprop[d + 1], qprop[D + d + 1], qprop[2 * D + d + 1], x[d + 1],
+                                    u53(w.z, w.w));
+        }
+      } else if constexpr (PROP == MCG_PROP_KD_INTERP) {
+        static_assert(P == 1, "KD: one lane per chain");
+        // Interpolate_pdf.draw (interpolate_pdf.ml:114-119)
+        const u32x4 w = rng(gid, tlo, CALL_KD_PICK, TAG_MH, thi);
+        const uint32_t pick = randint(w.x, w.y, (uint32_t)a.kd_M);
+        double pt[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) pt[d] = a.kd_pts[(int64_t)pick * D + d];
+        const int leaf = kd_find_leaf<D>(a.kd_nodes, a.kd_root, pt);
+        const double* __restrict__ bx = a.kd_box + (int64_t)leaf * 2 * D;
+#pragma unroll
+        for (int d = 0; d < D; d += 2) {
+          const u32x4 v = rng(gid, tlo, (uint32_t)(d >> 1), TAG_MH, thi);
+          y[d] = bx[d] + (bx[D + d] - bx[d]) * u53(v.x, v.y);
+          if (d + 1 < D) y[d + 1] = bx[d + 1] + (bx[D + d + 1] - bx[d + 1]) * u53(v.z, v.w);
+        }
+        lqy = a.kd_logq[kd_find_leaf<D>(a.kd_nodes, a.kd_root, y)];
+        lf = lqy;   // log_jump_prob start proposed = log q(proposed)
+        lb = lq;    // log_jump_prob proposed start = log q(start)
+      }
+      lly = eval_lik<D, P, LIK>(y, sub, a, qlik);
+      lpy = eval_prior<D, P>(y, sub, a, qpri);
+    }
+    // ---- Hastings ratio and accept test (mcmc.ml:42-56) ----
+    const double post_y = lly + lpy;
+    const double post_x = ll + lp;
+    const double ratio = ((post_y - post_x) + lb) - lf;
+    const u32x4 wa = rng(gid, tlo, CALL_ACCEPT, TAG_MH, thi);
+    const double lu = plog(u53(wa.x, wa.y));
+    const bool acc = lu < ratio;
+    if (acc) {
+#pragma unroll
+      for (int j = 0; j < L::NL; ++j) x[j] = y[j];
+      ll = lly;
+      lp = lpy;
+      lq = lqy;
+      ++na;
+    }
+    if (a.flags & RUNF_RECORD_ACCEPT) {
+      const uint64_t m = compress_ballot<P>((uint64_t)__ballot(acc && active));
+      const int64_t wave = tid >> 6;
+      if (lane == 0 && wave * (64 / P) < N) {
+        uint8_t* row = a.bits + (a.t0 + t) * a.bits_row_bytes;
+        const int64_t byte = wave * (8 / P);
+        if constexpr (P == 1) *(uint64_t*)(row + byte) = m;
+        else if constexpr (P == 2) *(uint32_t*)(row + byte) = (uint32_t)m;
+        else if constexpr (P == 4) *(uint16_t*)(row + byte) = (uint16_t)m;
+        else row[byte] = (uint8_t)m;
+      }
+    }
+    const int64_t tt1 = a.t0 + t + 1;
+    if (tt1 == next_rec && r < a.rec_end) {
+      record(r);
+      ++r;
+      next_rec += a.nskip;
+    }
+  }
+
+  if (!active) return;
+#pragma unroll
+  for (int i = 0; i < L::NCL; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (L::valid(sub, i, k)) a.x[(int64_t)L::dim(sub, i, k) * N + c] = x[4 * i + k];
+  if (sub == 0) {
+    a.ll[c] = ll;
+    a.lp[c] = lp;
+    a.nacc[c] += na;
+  }
+  if (accum) {
+    if constexpr (AccumCfg<D, P>::kLds) {
+#pragma unroll
+      for (int i = 0; i < L::NCL; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (L::valid(sub, i, k)) {
+            int64_t o = (int64_t)L::dim(sub, i, k) * N + c;
+            a.mean[o] = acc_mean(i, k);
+            a.m2[o] = acc_m2(i, k);
+          }
+    }
+    if (sub == 0) {
+      a.hm_m[c] = hm_m;
+      a.hm_s[c] = hm_s;
+    }
+  }
+}
+
+// evaluate ll, lp of the initial states (mcmc.ml:59-61)
+template <int D, int LIK>
+__global__ void __launch_bounds__(256) eval_kernel(const MhArgs a) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.N) return;
+  double x[Layout<D, 1>::NL];
+#pragma unroll
+  for (int d = 0; d < Layout<D, 1>::NL; ++d) x[d] = d < D ? a.x[(int64_t)d * a.N + c] : 0.0;
+  a.ll[c] = eval_lik<D, 1, LIK>(x, 0, a, a.lik);
+  a.lp[c] = eval_prior<D, 1>(x, 0, a, a.pri);
+}
+
+template <int D, int LIK>
+hipError_t launch_eval(const MhArgs& a, hipStream_t s) {
+  const int64_t grid = (a.N + 255) / 256;
+  hipLaunchKernelGGL((eval_kernel<D, LIK>), dim3((unsigned)grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int D, int P, int LIK, int PROP>
+hipError_t launch_mh(const MhArgs& a, int64_t nthreads, hipStream_t s) {
+  const int block = 256;
+  const int64_t grid = (nthreads + block - 1) / block;
+  constexpr int lds = AccumCfg<D, P>::kLdsBytes;
+  hipLaunchKernelGGL((mh_kernel<D, P, LIK, PROP>), dim3((unsigned)grid), dim3(block), lds, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace mcg

@@ -1,0 +1,678 @@
+// mcg_runtime.cpp -- host runtime behind the C-ABI (include/mcg.h).
+//
+// Owns the HIP device buffers of a sampling context, turns the reference's closure arguments
+// (mcmc.mli:58-60) into device constant blocks, slices Mcmc.mcmc_array (mcmc.ml:58-72) into
+// fused multi-step kernel launches, and finishes the tile reductions.  Nested sampling lives in
+// mcg_nested.cpp, the kD tree build in mcg_kdtree.cpp.
+#include "mcg_runtime.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+using namespace mcg;
+
+namespace mcg {
+
+int set_error(mcg_ctx* ctx, int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (ctx) ctx->err = buf;
+  return code;
+}
+
+int hip_check(mcg_ctx* ctx, hipError_t e, const char* what) {
+  if (e == hipSuccess) return MCG_OK;
+  return set_error(ctx, e == hipErrorOutOfMemory ? MCG_ENOMEM : MCG_EDEVICE, "%s: %s", what,
+                   hipGetErrorString(e));
+}
+
+DevBuf::~DevBuf() { release(); }
+void DevBuf::release() {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  bytes = 0;
+}
+hipError_t DevBuf::ensure(size_t n) {
+  if (n <= bytes && p) return hipSuccess;
+  release();
+  if (n == 0) n = 8;
+  hipError_t e = hipMalloc(&p, n);
+  if (e != hipSuccess) {
+    p = nullptr;
+    return e;
+  }
+  bytes = n;
+  return hipSuccess;
+}
+
+// portable exp for x <= 0 (same operation sequence as the device pexp)
+double host_pexp(double x) {
+  if (!(x > -708.0)) return 0.0;
+  const double inv_ln2 = 0x1.71547652b82fep+0;
+  const double ln2_hi = 0x1.62e42fee00000p-1, ln2_lo = 0x1.a39ef35793c76p-33;
+  double kd = std::floor(std::fma(x, inv_ln2, 0.5));
+  double r = std::fma(-kd, ln2_hi, x);
+  r = std::fma(-kd, ln2_lo, r);
+  static const double c[] = {0x1.ae64567f544e4p-26, 0x1.27e4fb7789f5cp-22, 0x1.71de3a556c734p-19,
+                             0x1.a01a01a01a01ap-16, 0x1.a01a01a01a01ap-13, 0x1.6c16c16c16c17p-10,
+                             0x1.1111111111111p-7,  0x1.5555555555555p-5,  0x1.5555555555555p-3,
+                             0.5, 1.0, 1.0};
+  double p = 0x1.1eed8eff8d898p-29;
+  for (double ci : c) p = std::fma(p, r, ci);
+  uint64_t sc = (uint64_t)((int)kd + 1023) << 52;
+  double scale;
+  std::memcpy(&scale, &sc, 8);
+  return p * scale;
+}
+
+void timing_begin(mcg_ctx* ctx, hipEvent_t* a, hipEvent_t* b) {
+  for (hipEvent_t* e : {a, b}) {
+    if (!ctx->ev_free.empty()) {
+      *e = ctx->ev_free.back();
+      ctx->ev_free.pop_back();
+    } else if (hipEventCreate(e) != hipSuccess) {
+      *e = nullptr;
+    }
+  }
+  if (*a) (void)hipEventRecord(*a, ctx->stream);
+}
+
+void timing_end(mcg_ctx* ctx, hipEvent_t a, hipEvent_t b, int kind) {
+  if (!a || !b) return;
+  (void)hipEventRecord(b, ctx->stream);
+  ctx->ev_pending.push_back(mcg_ctx::Pending{a, b, kind});
+}
+
+void timing_harvest(mcg_ctx* ctx) {
+  for (auto& p : ctx->ev_pending) {
+    (void)hipEventSynchronize(p.b);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, p.a, p.b);
+    mcg_kernel_timing& t = p.kind == 0 ? ctx->t_mh : ctx->t_walk;
+    t.launches += 1;
+    t.total_ms += ms;
+    t.last_ms = ms;
+    ctx->ev_free.push_back(p.a);
+    ctx->ev_free.push_back(p.b);
+  }
+  ctx->ev_pending.clear();
+}
+
+}  // namespace mcg
+
+static const double kNegHalfLog2Pi = -0.91893853320467274178;
+
+extern "C" {
+
+int mcg_abi_version(void) { return MCG_ABI_VERSION; }
+const char* mcg_device_arch(void) { return "gfx950"; }
+
+const char* mcg_last_error(const mcg_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int mcg_ctx_create(mcg_ctx** out, const mcg_opts* opts) {
+  if (!out) return MCG_EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev <= 0) return MCG_EDEVICE;
+  mcg_opts o{};
+  if (opts) o = *opts;
+  if (o.device < 0 || o.device >= ndev) return MCG_EINVAL;
+  if (o.lanes_per_chain != 0 && o.lanes_per_chain != 1 && o.lanes_per_chain != 2 &&
+      o.lanes_per_chain != 4 && o.lanes_per_chain != 8)
+    return MCG_EINVAL;
+  mcg_ctx* ctx = new mcg_ctx();
+  ctx->opts = o;
+  if (hipSetDevice(o.device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) {
+    delete ctx;
+    return MCG_EDEVICE;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, o.device) == hipSuccess) {
+    ctx->arch = prop.gcnArchName;
+    ctx->num_cus = prop.multiProcessorCount;
+  }
+  *out = ctx;
+  return MCG_OK;
+}
+
+void mcg_ctx_destroy(mcg_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->opts.device);
+  (void)hipStreamSynchronize(ctx->stream);
+  timing_harvest(ctx);
+  for (hipEvent_t e : ctx->ev_free) (void)hipEventDestroy(e);
+  (void)hipEventDestroy(ctx->ev0);
+  (void)hipEventDestroy(ctx->ev1);
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+int mcg_set_likelihood(mcg_ctx* ctx, int32_t kind, int32_t ndim, const double* params, size_t n) {
+  if (!ctx) return MCG_EINVAL;
+  std::vector<double> dev;
+  int D = ndim;
+  int32_t is_cauchy = 0;
+  int64_t data_n = 0;
+  switch (kind) {
+    case MCG_LIK_FLAT:
+      if (D < 1) return set_error(ctx, MCG_EINVAL, "FLAT: ndim >= 1");
+      dev.push_back(0.0);
+      break;
+    case MCG_LIK_DIAG_GAUSS: {
+      if (D < 1 || n != (size_t)(2 * D) || !params)
+        return set_error(ctx, MCG_EINVAL, "DIAG_GAUSS: params = mu[D], sigma[D]");
+      // [mu[D], 1/sigma[D], C = sum_d (-1/2 log 2pi - log sigma_d)]   (stats.ml:98-108)
+      double C = 0.0;
+      dev.resize(2 * D + 1);
+      for (int d = 0; d < D; ++d) {
+        if (!(params[D + d] > 0.0)) return set_error(ctx, MCG_EINVAL, "DIAG_GAUSS: sigma > 0");
+        dev[d] = params[d];
+        dev[D + d] = 1.0 / params[D + d];
+        C = C + (kNegHalfLog2Pi - std::log(params[D + d]));
+      }
+      dev[2 * D] = C;
+      break;
+    }
+    case MCG_LIK_GAUSS_SHELL: {
+      if (D < 1 || n != (size_t)(D + 2) || !params || !(params[D + 1] > 0.0))
+        return set_error(ctx, MCG_EINVAL, "GAUSS_SHELL: params = c[D], r, w (w > 0)");
+      dev.assign(params, params + D);
+      dev.push_back(params[D]);
+      dev.push_back(1.0 / params[D + 1]);
+      dev.push_back(kNegHalfLog2Pi - std::log(params[D + 1]));
+      break;
+    }
+    case MCG_LIK_FULLCOV_GAUSS: {
+      if (D < 1 || n != (size_t)(D + D * D) || !params)
+        return set_error(ctx, MCG_EINVAL, "FULLCOV_GAUSS: params = mu[D], U[D*D]");
+      const double* U = params + D;
+      double C = 0.0;
+      for (int i = 0; i < D; ++i) {
+        if (!(U[i * D + i] > 0.0)) return set_error(ctx, MCG_EINVAL, "FULLCOV_GAUSS: U_ii > 0");
+        C = C + (std::log(U[i * D + i]) + kNegHalfLog2Pi);
+      }
+      dev.assign(params, params + D);
+      dev.push_back(C);
+      dev.insert(dev.end(), U, U + (size_t)D * D);
+      break;
+    }
+    case MCG_LIK_GAUSS_DATA:
+    case MCG_LIK_CAUCHY_DATA: {
+      if (!params || n < 2) return set_error(ctx, MCG_EINVAL, "DATA: params = nd, data[nsamp*nd]");
+      int nd = (int)params[0];
+      if (nd < 1 || D != 2 * nd || (n - 1) % (size_t)nd != 0)
+        return set_error(ctx, MCG_EINVAL, "DATA: ndim must be 2*nd and data a multiple of nd");
+      data_n = (int64_t)((n - 1) / nd);
+      dev.assign(params + 1, params + n);
+      is_cauchy = kind == MCG_LIK_CAUCHY_DATA;
+      break;
+    }
+    default:
+      return set_error(ctx, MCG_EINVAL, "unknown likelihood kind %d", kind);
+  }
+  if (ctx->D != 0 && ctx->D != D && ctx->N > 0)
+    return set_error(ctx, MCG_ESTATE, "ndim changed after mcg_init");
+  ctx->D = D;
+  ctx->lik_kind = kind;
+  ctx->is_cauchy = is_cauchy;
+  ctx->data_n = data_n;
+  ctx->lik_host = dev;
+  int rc = hip_check(ctx, ctx->d_lik.ensure(dev.size() * 8), "alloc likelihood");
+  if (rc) return rc;
+  rc = hip_check(ctx, hipMemcpy(ctx->d_lik.p, dev.data(), dev.size() * 8, hipMemcpyHostToDevice), "copy likelihood");
+  if (rc) return rc;
+  // keep a padded flat prior / default proposal consistent with D
+  if (ctx->pri_host.size() != (size_t)(2 * D + 1)) {
+    double z = 0.0;
+    rc = mcg_set_prior(ctx, MCG_PRIOR_FLAT, &z, 0);
+    if (rc) return rc;
+  }
+  return MCG_OK;
+}
+
+int mcg_set_prior(mcg_ctx* ctx, int32_t kind, const double* params, size_t n) {
+  if (!ctx) return MCG_EINVAL;
+  int D = ctx->D;
+  if (D < 1) return set_error(ctx, MCG_ESTATE, "set the likelihood (ndim) first");
+  std::vector<double> dev(2 * D + 1);
+  if (kind == MCG_PRIOR_FLAT) {
+    for (int d = 0; d < D; ++d) {
+      dev[d] = -HUGE_VAL;
+      dev[D + d] = HUGE_VAL;
+    }
+    dev[2 * D] = 0.0;
+  } else if (kind == MCG_PRIOR_BOX || kind == MCG_PRIOR_OPEN_BOX) {
+    if (!params || n != (size_t)(2 * D + 1))
+      return set_error(ctx, MCG_EINVAL, "BOX: params = lo[D], hi[D], lp_in");
+    dev.assign(params, params + n);
+  } else {
+    return set_error(ctx, MCG_EINVAL, "unknown prior kind %d", kind);
+  }
+  ctx->prior_kind = kind;
+  ctx->pri_host = dev;
+  int rc = hip_check(ctx, ctx->d_pri.ensure(dev.size() * 8), "alloc prior");
+  if (rc) return rc;
+  return hip_check(ctx, hipMemcpy(ctx->d_pri.p, dev.data(), dev.size() * 8, hipMemcpyHostToDevice), "copy prior");
+}
+
+int mcg_set_proposal(mcg_ctx* ctx, int32_t kind, const double* params, size_t n) {
+  if (!ctx) return MCG_EINVAL;
+  int D = ctx->D;
+  if (D < 1) return set_error(ctx, MCG_ESTATE, "set the likelihood (ndim) first");
+  std::vector<double> dev;
+  if (kind == MCG_PROP_GAUSS) {
+    if (!params || (n != 1 && n != (size_t)D)) return set_error(ctx, MCG_EINVAL, "GAUSS: s[1] or s[D]");
+    dev.resize(D);
+    for (int d = 0; d < D; ++d) dev[d] = params[n == 1 ? 0 : d];
+  } else if (kind == MCG_PROP_WRAP_UNIFORM) {
+    if (!params || n != (size_t)(3 * D)) return set_error(ctx, MCG_EINVAL, "WRAP_UNIFORM: lo[D], hi[D], dx[D]");
+    dev.assign(params, params + n);
+  } else if (kind == MCG_PROP_KD_INTERP) {
+    if (!ctx->kd.built) return set_error(ctx, MCG_ESTATE, "call mcg_set_kd_proposal first");
+    dev.push_back(0.0);
+  } else {
+    return set_error(ctx, MCG_EINVAL, "unsupported proposal kind %d for MH", kind);
+  }
+  ctx->prop_kind = kind;
+  ctx->prop_host = dev;
+  int rc = hip_check(ctx, ctx->d_prop.ensure(dev.size() * 8), "alloc proposal");
+  if (rc) return rc;
+  return hip_check(ctx, hipMemcpy(ctx->d_prop.p, dev.data(), dev.size() * 8, hipMemcpyHostToDevice), "copy proposal");
+}
+
+int mcg_set_kd_proposal(mcg_ctx* ctx, const double* pts, int64_t M, const double* low,
+                        const double* high) {
+  if (!ctx || !pts || !low || !high) return MCG_EINVAL;
+  int D = ctx->D;
+  if (D < 1) return set_error(ctx, MCG_ESTATE, "set the likelihood (ndim) first");
+  if (M < 1) return set_error(ctx, MCG_EINVAL, "Interpolate_pdf.make: no points");
+  int rc = kd_build(ctx, pts, M, D, low, high);
+  if (rc) return rc;
+  double z = 0.0;
+  return mcg_set_proposal(ctx, MCG_PROP_KD_INTERP, &z, 1);
+}
+
+int mcg_init(mcg_ctx* ctx, int64_t nchains, const double* x_soa, const double* ll,
+             const double* lp) {
+  if (!ctx || nchains < 1 || !x_soa) return MCG_EINVAL;
+  if (ctx->D < 1) return set_error(ctx, MCG_ESTATE, "set the likelihood first");
+  if (nchains > (int64_t)0x7FFFFFFF) return set_error(ctx, MCG_EINVAL, "too many chains");
+  (void)hipSetDevice(ctx->opts.device);
+  const int D = ctx->D;
+  const size_t N = (size_t)nchains;
+  int rc;
+  if ((rc = hip_check(ctx, ctx->d_x.ensure(N * D * 8), "alloc x"))) return rc;
+  if ((rc = hip_check(ctx, ctx->d_ll.ensure(N * 8), "alloc ll"))) return rc;
+  if ((rc = hip_check(ctx, ctx->d_lp.ensure(N * 8), "alloc lp"))) return rc;
+  if ((rc = hip_check(ctx, ctx->d_nacc.ensure(N * 8), "alloc counters"))) return rc;
+  if ((rc = hip_check(ctx, hipMemcpy(ctx->d_x.p, x_soa, N * D * 8, hipMemcpyHostToDevice), "copy x"))) return rc;
+  if ((rc = hip_check(ctx, hipMemset(ctx->d_nacc.p, 0, N * 8), "zero counters"))) return rc;
+  ctx->N = nchains;
+  ctx->steps_done = 0;
+  ctx->nsteps_total = 0;
+  ctx->last_nsteps = 0;
+  ctx->nrec_total = 0;
+  ctx->rec_stored = 0;
+  if (ll && lp) {
+    if ((rc = hip_check(ctx, hipMemcpy(ctx->d_ll.p, ll, N * 8, hipMemcpyHostToDevice), "copy ll"))) return rc;
+    if ((rc = hip_check(ctx, hipMemcpy(ctx->d_lp.p, lp, N * 8, hipMemcpyHostToDevice), "copy lp"))) return rc;
+    return MCG_OK;
+  }
+  eval_launch_fn fn = find_eval_kernel(D, ctx->lik_kind);
+  if (!fn) return set_error(ctx, MCG_EINVAL, "no compiled kernel for likelihood %d at D=%d", ctx->lik_kind, D);
+  MhArgs a = base_args(ctx);
+  if ((rc = hip_check(ctx, fn(a, ctx->stream), "eval launch"))) return rc;
+  return hip_check(ctx, hipStreamSynchronize(ctx->stream), "eval sync");
+}
+
+int mcg_get_state(mcg_ctx* ctx, double* x_soa, double* ll, double* lp) {
+  if (!ctx) return MCG_EINVAL;
+  if (ctx->N < 1) return set_error(ctx, MCG_ESTATE, "no chains");
+  const size_t N = (size_t)ctx->N;
+  int rc;
+  if ((rc = hip_check(ctx, hipStreamSynchronize(ctx->stream), "sync"))) return rc;
+  if (x_soa && (rc = hip_check(ctx, hipMemcpy(x_soa, ctx->d_x.p, N * ctx->D * 8, hipMemcpyDeviceToHost), "copy x"))) return rc;
+  if (ll && (rc = hip_check(ctx, hipMemcpy(ll, ctx->d_ll.p, N * 8, hipMemcpyDeviceToHost), "copy ll"))) return rc;
+  if (lp && (rc = hip_check(ctx, hipMemcpy(lp, ctx->d_lp.p, N * 8, hipMemcpyDeviceToHost), "copy lp"))) return rc;
+  return MCG_OK;
+}
+
+}  // extern "C"
+
+namespace mcg {
+
+MhArgs base_args(mcg_ctx* ctx) {
+  MhArgs a{};
+  a.x = (double*)ctx->d_x.p;
+  a.ll = (double*)ctx->d_ll.p;
+  a.lp = (double*)ctx->d_lp.p;
+  a.nacc = (unsigned long long*)ctx->d_nacc.p;
+  a.lik = (const double*)ctx->d_lik.p;
+  a.pri = (const double*)ctx->d_pri.p;
+  a.prop = (const double*)ctx->d_prop.p;
+  a.N = ctx->N;
+  a.k0 = (uint32_t)ctx->opts.seed;
+  a.k1 = (uint32_t)(ctx->opts.seed >> 32);
+  a.chain_offset = (uint32_t)ctx->opts.chain_offset;
+  a.prior_kind = ctx->prior_kind;
+  a.data_n = ctx->data_n;
+  a.is_cauchy = ctx->is_cauchy;
+  a.kd_nodes = (const KdNode*)ctx->kd.d_nodes.p;
+  a.kd_logq = (const double*)ctx->kd.d_logq.p;
+  a.kd_box = (const double*)ctx->kd.d_box.p;
+  a.kd_pts = (const double*)ctx->kd.d_pts.p;
+  a.kd_root = (const double*)ctx->kd.d_root.p;
+  a.kd_M = ctx->kd.M;
+  return a;
+}
+
+// lanes per chain: enough lanes to put >= 4 waves on every SIMD, as long as the dimensions split
+// evenly into 4-dim Philox blocks (separable likelihoods with a Gaussian proposal only).
+int choose_lanes(mcg_ctx* ctx) {
+  const int D = ctx->D;
+  const bool separable = (ctx->lik_kind == MCG_LIK_DIAG_GAUSS || ctx->lik_kind == MCG_LIK_GAUSS_SHELL ||
+                          ctx->lik_kind == MCG_LIK_FLAT) && ctx->prop_kind == MCG_PROP_GAUSS;
+  const char* env = std::getenv("MCG_LANES_PER_CHAIN");
+  int want = ctx->opts.lanes_per_chain;
+  if (env && *env) want = std::atoi(env);
+  if (want > 0) {
+    if (want == 1) return 1;
+    if (separable && D % (4 * want) == 0 && find_mh_kernel(D, want, ctx->lik_kind, ctx->prop_kind)) return want;
+    return 1;
+  }
+  if (!separable) return 1;
+  const int64_t lanes_target = (int64_t)std::max(ctx->num_cus, 1) * 4 * 4 * 64;  // 4 waves/SIMD
+  int best = 1;
+  for (int P : {2, 4}) {
+    if (ctx->N * best >= lanes_target) break;
+    if (D % (4 * P) == 0 && find_mh_kernel(D, P, ctx->lik_kind, ctx->prop_kind)) best = P;
+  }
+  return best;
+}
+
+}  // namespace mcg
+
+extern "C" {
+
+int mcg_run(mcg_ctx* ctx, const mcg_run_opts* o) {
+  if (!ctx || !o) return MCG_EINVAL;
+  if (ctx->N < 1) return set_error(ctx, MCG_ESTATE, "mcg_run before mcg_init");
+  if (o->nskip < 1 || o->n_rec < 0 || o->nbin < 0) return set_error(ctx, MCG_EINVAL, "nbin >= 0, nskip >= 1, n_rec >= 0");
+  if (o->append && ctx->nrec_total == 0 && o->accumulate)
+    return set_error(ctx, MCG_ESTATE, "append needs a previous run with records");
+  (void)hipSetDevice(ctx->opts.device);
+  const int D = ctx->D;
+  const int64_t N = ctx->N;
+  const int P = choose_lanes(ctx);
+  mh_launch_fn fn = find_mh_kernel(D, P, ctx->lik_kind, ctx->prop_kind);
+  if (!fn) return set_error(ctx, MCG_EINVAL, "no compiled MH kernel for D=%d likelihood=%d proposal=%d", D, ctx->lik_kind, ctx->prop_kind);
+  ctx->lanes = P;
+  // mcmc_array schedule: records at run-local step counts s_r = nbin + r*nskip (r < n_rec);
+  // append mode records at nskip, 2 nskip, ... (no initial record).
+  const bool append = o->append != 0;
+  const int64_t nbin_eff = append ? o->nskip : o->nbin;
+  const int64_t n_rec = o->n_rec;
+  const int64_t nsteps = n_rec > 0 ? nbin_eff + (n_rec - 1) * o->nskip : o->nbin;
+  const int64_t rec_base = append ? ctx->nrec_total : 0;
+  int rc;
+  // buffers
+  const size_t Nz = (size_t)N;
+  if (o->record_x && n_rec > 0) {
+    if ((rc = hip_check(ctx, ctx->d_rec_x.ensure((size_t)n_rec * D * Nz * 8), "alloc rec_x"))) return rc;
+  }
+  if (o->record_llp && n_rec > 0) {
+    if ((rc = hip_check(ctx, ctx->d_rec_ll.ensure((size_t)n_rec * Nz * 8), "alloc rec_ll"))) return rc;
+    if ((rc = hip_check(ctx, ctx->d_rec_lp.ensure((size_t)n_rec * Nz * 8), "alloc rec_lp"))) return rc;
+  }
+  const int64_t row_bytes = ((N + 63) / 64) * 8;
+  if (o->record_accept && nsteps > 0) {
+    if ((rc = hip_check(ctx, ctx->d_bits.ensure((size_t)nsteps * row_bytes), "alloc accept bits"))) return rc;
+    if ((rc = hip_check(ctx, hipMemsetAsync(ctx->d_bits.p, 0, (size_t)nsteps * row_bytes, ctx->stream), "zero bits"))) return rc;
+  }
+  if (o->accumulate) {
+    if ((rc = hip_check(ctx, ctx->d_mean.ensure(Nz * D * 8), "alloc mean"))) return rc;
+    if ((rc = hip_check(ctx, ctx->d_m2.ensure(Nz * D * 8), "alloc m2"))) return rc;
+    if ((rc = hip_check(ctx, ctx->d_hm_m.ensure(Nz * 8), "alloc hm"))) return rc;
+    if ((rc = hip_check(ctx, ctx->d_hm_s.ensure(Nz * 8), "alloc hm"))) return rc;
+    if (!append) {
+      if ((rc = hip_check(ctx, hipMemsetAsync(ctx->d_mean.p, 0, Nz * D * 8, ctx->stream), "zero"))) return rc;
+      if ((rc = hip_check(ctx, hipMemsetAsync(ctx->d_m2.p, 0, Nz * D * 8, ctx->stream), "zero"))) return rc;
+    }
+  }
+  MhArgs a = base_args(ctx);
+  a.mean = (double*)ctx->d_mean.p;
+  a.m2 = (double*)ctx->d_m2.p;
+  a.hm_m = (double*)ctx->d_hm_m.p;
+  a.hm_s = (double*)ctx->d_hm_s.p;
+  a.rec_x = (double*)ctx->d_rec_x.p;
+  a.rec_ll = (double*)ctx->d_rec_ll.p;
+  a.rec_lp = (double*)ctx->d_rec_lp.p;
+  a.bits = (uint8_t*)ctx->d_bits.p;
+  a.bits_row_bytes = row_bytes;
+  a.nskip = o->nskip;
+  a.rec_base = rec_base;
+  a.rec_end = rec_base + n_rec;
+  int64_t spl = ctx->opts.steps_per_launch;
+  if (const char* env = std::getenv("MCG_STEPS_PER_LAUNCH")) spl = std::atoll(env);
+  if (spl <= 0) spl = std::max<int64_t>(1, std::min<int64_t>(4096, ((int64_t)1 << 26) / N));
+  const int64_t nthreads = N * P;
+  int64_t t0 = 0;
+  bool first = true;
+  do {
+    const int64_t n = std::min<int64_t>(spl, nsteps - t0);
+    a.t0 = t0;
+    a.nsteps = n;
+    a.step_base = ctx->steps_done + (uint64_t)t0;
+    a.flags = (o->record_x ? RUNF_RECORD_X : 0) | (o->record_llp ? RUNF_RECORD_LLP : 0) |
+              (o->record_accept ? RUNF_RECORD_ACCEPT : 0) | (o->accumulate ? RUNF_ACCUMULATE : 0);
+    // first record strictly after step count t0 (the initial state is record 0 when nbin = 0)
+    int64_t r_first;
+    if (!append && first && nbin_eff == 0 && n_rec > 0) {
+      a.flags |= RUNF_RECORD_INITIAL;
+      r_first = 0;
+    } else {
+      r_first = (t0 < nbin_eff) ? 0 : (t0 - nbin_eff) / o->nskip + 1;
+    }
+    a.next_r = rec_base + r_first;
+    a.next_rec = nbin_eff + r_first * o->nskip;
+    if (a.flags & RUNF_RECORD_INITIAL) a.next_rec = nbin_eff + (r_first + 1) * o->nskip;
+    if (n_rec == 0 || !(o->record_x || o->record_llp || o->accumulate)) a.rec_end = a.next_r;  // nothing to record
+    if (n > 0 || (a.flags & RUNF_RECORD_INITIAL)) {
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      if (ctx->timing) timing_begin(ctx, &e0, &e1);
+      if ((rc = hip_check(ctx, fn(a, nthreads, ctx->stream), "MH launch"))) return rc;
+      if (ctx->timing) timing_end(ctx, e0, e1, 0);
+    }
+    t0 += n;
+    first = false;
+  } while (t0 < nsteps);
+  ctx->steps_done += (uint64_t)nsteps;
+  ctx->nsteps_total += nsteps;
+  ctx->last_nsteps = nsteps;
+  ctx->last_record_accept = o->record_accept != 0;
+  if (o->accumulate) ctx->nrec_total = rec_base + n_rec;
+  ctx->rec_stored = n_rec;
+  ctx->rec_x_valid = o->record_x != 0;
+  ctx->rec_llp_valid = o->record_llp != 0;
+  return MCG_OK;
+}
+
+int64_t mcg_last_run_steps(const mcg_ctx* ctx) { return ctx ? ctx->last_nsteps : -1; }
+
+int mcg_get_records(mcg_ctx* ctx, double* rec_x, double* rec_ll, double* rec_lp,
+                    uint64_t* accept_bits) {
+  if (!ctx) return MCG_EINVAL;
+  int rc;
+  if ((rc = hip_check(ctx, hipStreamSynchronize(ctx->stream), "sync"))) return rc;
+  const size_t N = (size_t)ctx->N, R = (size_t)ctx->rec_stored;
+  if (rec_x) {
+    if (!ctx->rec_x_valid) return set_error(ctx, MCG_ESTATE, "last run did not record x");
+    if ((rc = hip_check(ctx, hipMemcpy(rec_x, ctx->d_rec_x.p, R * ctx->D * N * 8, hipMemcpyDeviceToHost), "copy rec_x"))) return rc;
+  }
+  if (rec_ll || rec_lp) {
+    if (!ctx->rec_llp_valid) return set_error(ctx, MCG_ESTATE, "last run did not record ll/lp");
+    if (rec_ll && (rc = hip_check(ctx, hipMemcpy(rec_ll, ctx->d_rec_ll.p, R * N * 8, hipMemcpyDeviceToHost), "copy rec_ll"))) return rc;
+    if (rec_lp && (rc = hip_check(ctx, hipMemcpy(rec_lp, ctx->d_rec_lp.p, R * N * 8, hipMemcpyDeviceToHost), "copy rec_lp"))) return rc;
+  }
+  if (accept_bits) {
+    if (!ctx->last_record_accept) return set_error(ctx, MCG_ESTATE, "last run did not record the accept bitmap");
+    const size_t bytes = (size_t)ctx->last_nsteps * ((N + 63) / 64) * 8;
+    if (bytes && (rc = hip_check(ctx, hipMemcpy(accept_bits, ctx->d_bits.p, bytes, hipMemcpyDeviceToHost), "copy bits"))) return rc;
+  }
+  return MCG_OK;
+}
+
+int mcg_get_counters(mcg_ctx* ctx, uint64_t* naccept, uint64_t* nreject) {
+  if (!ctx) return MCG_EINVAL;
+  if (ctx->N < 1) {
+    if (naccept) *naccept = 0;
+    if (nreject) *nreject = 0;
+    return MCG_OK;
+  }
+  std::vector<uint64_t> h((size_t)ctx->N);
+  int rc;
+  if ((rc = hip_check(ctx, hipStreamSynchronize(ctx->stream), "sync"))) return rc;
+  if ((rc = hip_check(ctx, hipMemcpy(h.data(), ctx->d_nacc.p, h.size() * 8, hipMemcpyDeviceToHost), "copy counters"))) return rc;
+  uint64_t s = 0;
+  for (uint64_t v : h) s += v;
+  const uint64_t total = (uint64_t)ctx->nsteps_total * (uint64_t)ctx->N;
+  if (naccept) *naccept = s;
+  if (nreject) *nreject = total - s;
+  return MCG_OK;
+}
+
+int mcg_reset_counters(mcg_ctx* ctx) {
+  if (!ctx) return MCG_EINVAL;
+  ctx->nsteps_total = 0;
+  if (ctx->N < 1) return MCG_OK;
+  return hip_check(ctx, hipMemsetAsync(ctx->d_nacc.p, 0, (size_t)ctx->N * 8, ctx->stream), "reset counters");
+}
+
+int64_t mcg_num_tiles(const mcg_ctx* ctx) { return ctx ? (ctx->N + 255) / 256 : -1; }
+
+int mcg_tile_stats_device(mcg_ctx* ctx, void** dev_ptr, int64_t* ntiles) {
+  if (!ctx) return MCG_EINVAL;
+  if (ctx->nrec_total < 1) return set_error(ctx, MCG_ESTATE, "no accumulated records");
+  const int D = ctx->D;
+  const int64_t nt = (ctx->N + 255) / 256;
+  int rc;
+  if ((rc = hip_check(ctx, ctx->d_tiles.ensure((size_t)nt * (2 * D + 3) * 8), "alloc tiles"))) return rc;
+  TileArgs t{};
+  t.mean = (const double*)ctx->d_mean.p;
+  t.m2 = (const double*)ctx->d_m2.p;
+  t.hm_m = (const double*)ctx->d_hm_m.p;
+  t.hm_s = (const double*)ctx->d_hm_s.p;
+  t.tiles = (double*)ctx->d_tiles.p;
+  t.N = ctx->N;
+  t.nrec = ctx->nrec_total;
+  t.D = D;
+  if ((rc = hip_check(ctx, launch_tile_stats(t, ctx->stream), "tile launch"))) return rc;
+  if (dev_ptr) *dev_ptr = ctx->d_tiles.p;
+  if (ntiles) *ntiles = nt;
+  return MCG_OK;
+}
+
+int mcg_tile_stats(mcg_ctx* ctx, double* tiles) {
+  if (!ctx || !tiles) return MCG_EINVAL;
+  int64_t nt = 0;
+  int rc = mcg_tile_stats_device(ctx, nullptr, &nt);
+  if (rc) return rc;
+  if ((rc = hip_check(ctx, hipStreamSynchronize(ctx->stream), "tile sync"))) return rc;
+  return hip_check(ctx, hipMemcpy(tiles, ctx->d_tiles.p, (size_t)nt * (2 * ctx->D + 3) * 8, hipMemcpyDeviceToHost), "copy tiles");
+}
+
+// Fold tiles in global order (the same Chan / log-space combine as the device tree), then
+// Stats.multi_mean / multi_std (stats.ml:58-87) and log Z_HM = log n - logsumexp(-ll).
+int mcg_combine_tiles(int32_t D, int64_t ntiles, const double* tiles, double* mean, double* sd,
+                      double* log_z_hm) {
+  if (D < 1 || ntiles < 1 || !tiles) return MCG_EINVAL;
+  const int W = 2 * D + 3;
+  std::vector<double> acc(W, 0.0);
+  acc[2 * D + 1] = -HUGE_VAL;
+  for (int64_t t = 0; t < ntiles; ++t) {
+    const double* b = tiles + t * W;
+    const double na = acc[0], nb = b[0];
+    if (nb == 0.0) continue;
+    if (na == 0.0) {
+      std::copy(b, b + W, acc.begin());
+      continue;
+    }
+    const double n = na + nb, fb = nb / n, fab = (na * nb) / n;
+    for (int d = 0; d < D; ++d) {
+      const double delta = b[1 + d] - acc[1 + d];
+      acc[1 + d] = acc[1 + d] + delta * fb;
+      acc[1 + D + d] = (acc[1 + D + d] + b[1 + D + d]) + (delta * delta) * fab;
+    }
+    const double ma = acc[2 * D + 1], sa = acc[2 * D + 2], mb = b[2 * D + 1], sb = b[2 * D + 2];
+    const double mm = ma > mb ? ma : mb;
+    acc[2 * D + 1] = mm;
+    acc[2 * D + 2] = sa * host_pexp(ma - mm) + sb * host_pexp(mb - mm);
+    acc[0] = n;
+  }
+  const double n = acc[0];
+  for (int d = 0; d < D; ++d) {
+    if (mean) mean[d] = acc[1 + d];
+    if (sd) sd[d] = std::sqrt(acc[1 + D + d] / (n - 1.0));
+  }
+  if (log_z_hm) *log_z_hm = std::log(n) - (acc[2 * D + 1] + std::log(acc[2 * D + 2]));
+  return MCG_OK;
+}
+
+int mcg_stats(mcg_ctx* ctx, double* mean, double* sd, double* log_z_hm) {
+  if (!ctx) return MCG_EINVAL;
+  const int64_t nt = mcg_num_tiles(ctx);
+  std::vector<double> tiles((size_t)nt * (2 * ctx->D + 3));
+  int rc = mcg_tile_stats(ctx, tiles.data());
+  if (rc) return rc;
+  return mcg_combine_tiles(ctx->D, nt, tiles.data(), mean, sd, log_z_hm);
+}
+
+double mcg_log_total_error_estimate(double log_ev, double log_dev, int64_t nlive) {
+  // nested.ml:148-150
+  const double lre2 = -std::log((double)nlive);
+  double a = 2.0 * log_dev, b = lre2 + 2.0 * log_ev;
+  if (a == -HUGE_VAL && b == -HUGE_VAL) return -HUGE_VAL;
+  if (b > a) std::swap(a, b);
+  return 0.5 * (a + std::log1p(std::exp(b - a)));
+}
+
+int mcg_set_timing(mcg_ctx* ctx, int32_t enabled) {
+  if (!ctx) return MCG_EINVAL;
+  timing_harvest(ctx);
+  ctx->timing = enabled != 0;
+  ctx->t_mh = mcg_kernel_timing{};
+  ctx->t_mh_steps = 0;
+  return MCG_OK;
+}
+
+int mcg_get_kernel_timing(mcg_ctx* ctx, const char* kernel, mcg_kernel_timing* out) {
+  if (!ctx || !out) return MCG_EINVAL;
+  std::string k = kernel ? kernel : "mh";
+  timing_harvest(ctx);
+  if (k == "mh") {
+    *out = ctx->t_mh;
+    return MCG_OK;
+  }
+  if (k == "nested_walk") {
+    *out = ctx->t_walk;
+    return MCG_OK;
+  }
+  return set_error(ctx, MCG_EINVAL, "unknown kernel '%s'", k.c_str());
+}
+
+int mcg_sync(mcg_ctx* ctx) {
+  if (!ctx) return MCG_EINVAL;
+  return hip_check(ctx, hipStreamSynchronize(ctx->stream), "sync");
+}
+
+}  // extern "C"

@@ -1,0 +1,93 @@
+// mcg_runtime.h -- internal host-side state of a sampling context.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "mcg.h"
+#include "mcg_device.h"
+
+namespace mcg {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf();
+  hipError_t ensure(size_t n);
+  void release();
+};
+
+struct KdState {
+  bool built = false;
+  int64_t M = 0;
+  int64_t nnodes = 0, nleaves = 0;
+  std::vector<KdNode> nodes;
+  std::vector<double> logq, box, pts, root;
+  std::vector<int32_t> count;
+  DevBuf d_nodes, d_logq, d_box, d_pts, d_root;
+};
+
+struct NestedState {
+  // last run, host copies (dead points in retirement order, then live ascending)
+  std::vector<double> pts, ll, lp, wts;
+  int64_t n_total = 0, n_dead = 0, n_gen = 0, nlive = 0;
+  double log_ev = 0.0, log_dev = 0.0;
+};
+
+}  // namespace mcg
+
+struct mcg_ctx {
+  mcg_opts opts{};
+  std::string err;
+  std::string arch;
+  int num_cus = 256;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // model
+  int D = 0;
+  int32_t lik_kind = -1, prior_kind = MCG_PRIOR_FLAT, prop_kind = MCG_PROP_GAUSS;
+  int32_t is_cauchy = 0;
+  int64_t data_n = 0;
+  std::vector<double> lik_host, pri_host, prop_host;
+  mcg::DevBuf d_lik, d_pri, d_prop;
+  mcg::KdState kd;
+  // chains
+  int64_t N = 0;
+  mcg::DevBuf d_x, d_ll, d_lp, d_nacc;
+  uint64_t steps_done = 0;      // global RNG step counter (all runs)
+  int64_t nsteps_total = 0;     // steps since the last counter reset
+  int64_t last_nsteps = 0;
+  int lanes = 1;
+  // records and statistics
+  mcg::DevBuf d_rec_x, d_rec_ll, d_rec_lp, d_bits, d_mean, d_m2, d_hm_m, d_hm_s, d_tiles;
+  int64_t nrec_total = 0, rec_stored = 0;
+  bool rec_x_valid = false, rec_llp_valid = false, last_record_accept = false;
+  // nested sampling
+  mcg::NestedState nested;
+  // timing: per-launch HIP event pairs on the launch stream, harvested lazily (no host sync
+  // inside mcg_run)
+  bool timing = false;
+  mcg_kernel_timing t_mh{}, t_walk{};
+  int64_t t_mh_steps = 0;
+  std::vector<hipEvent_t> ev_free;
+  struct Pending { hipEvent_t a, b; int kind; };
+  std::vector<Pending> ev_pending;
+};
+
+namespace mcg {
+int set_error(mcg_ctx* ctx, int code, const char* fmt, ...);
+int hip_check(mcg_ctx* ctx, hipError_t e, const char* what);
+MhArgs base_args(mcg_ctx* ctx);
+int choose_lanes(mcg_ctx* ctx);
+double host_pexp(double x);
+void timing_begin(mcg_ctx* ctx, hipEvent_t* a, hipEvent_t* b);
+void timing_end(mcg_ctx* ctx, hipEvent_t a, hipEvent_t b, int kind);
+void timing_harvest(mcg_ctx* ctx);
+int kd_build(mcg_ctx* ctx, const double* pts, int64_t M, int D, const double* low, const double* high);
+}  // namespace mcg

@@ -1,0 +1,139 @@
+"""ctypes binding of libmcg.so (the C-ABI in include/mcg.h).
+
+The HIP library is the only compute path: if it is missing or no GPU is visible, every
+entry point raises (McgError / RuntimeError) -- there is no CPU fallback.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(HERE)
+LIB_PATH = os.environ.get("MCG_LIBRARY", os.path.join(PKG_ROOT, "lib", "libmcg.so"))
+
+MCG_OK, MCG_EINVAL, MCG_EFAIL, MCG_EDEVICE, MCG_ENOMEM, MCG_ESTATE = 0, -1, -2, -3, -4, -5
+LIK_FLAT, LIK_DIAG_GAUSS, LIK_FULLCOV_GAUSS, LIK_GAUSS_SHELL, LIK_GAUSS_DATA, LIK_CAUCHY_DATA = range(6)
+PRIOR_FLAT, PRIOR_BOX, PRIOR_OPEN_BOX = 0, 1, 2
+PROP_GAUSS, PROP_WRAP_UNIFORM, PROP_KD_INTERP, PROP_DE = 1, 2, 3, 4
+FLAG_NESTED_FIXED_STOP = 1
+
+_dp = C.POINTER(C.c_double)
+_u64p = C.POINTER(C.c_uint64)
+_i32p = C.POINTER(C.c_int32)
+
+
+class McgOpts(C.Structure):
+    _fields_ = [("device", C.c_int32), ("flags", C.c_uint32), ("seed", C.c_uint64),
+                ("chain_offset", C.c_uint64), ("lanes_per_chain", C.c_int32),
+                ("steps_per_launch", C.c_int32)]
+
+
+class McgRunOpts(C.Structure):
+    _fields_ = [("nbin", C.c_int64), ("nskip", C.c_int64), ("n_rec", C.c_int64),
+                ("record_x", C.c_int32), ("record_llp", C.c_int32),
+                ("record_accept", C.c_int32), ("accumulate", C.c_int32), ("append", C.c_int32)]
+
+
+class McgNestedOpts(C.Structure):
+    _fields_ = [("nlive", C.c_int64), ("nmcmc", C.c_int64), ("k", C.c_int64),
+                ("epsrel", C.c_double), ("mode_hop", C.c_double), ("max_dead", C.c_int64)]
+
+
+class McgNestedResult(C.Structure):
+    _fields_ = [("log_ev", C.c_double), ("log_dev", C.c_double), ("n_dead", C.c_int64),
+                ("n_total", C.c_int64), ("n_gen", C.c_int64)]
+
+
+class McgKernelTiming(C.Structure):
+    _fields_ = [("launches", C.c_int64), ("total_ms", C.c_double), ("last_ms", C.c_double)]
+
+
+OBSERVER = C.CFUNCTYPE(None, C.c_void_p, _dp, _dp, _dp, C.c_int64)
+
+# every symbol include/mcg.h declares, with its ctypes signature
+SIGNATURES = {
+    "mcg_abi_version": ([], C.c_int),
+    "mcg_device_arch": ([], C.c_char_p),
+    "mcg_ctx_create": ([C.POINTER(C.c_void_p), C.POINTER(McgOpts)], C.c_int),
+    "mcg_ctx_destroy": ([C.c_void_p], None),
+    "mcg_last_error": ([C.c_void_p], C.c_char_p),
+    "mcg_set_likelihood": ([C.c_void_p, C.c_int32, C.c_int32, _dp, C.c_size_t], C.c_int),
+    "mcg_set_prior": ([C.c_void_p, C.c_int32, _dp, C.c_size_t], C.c_int),
+    "mcg_set_proposal": ([C.c_void_p, C.c_int32, _dp, C.c_size_t], C.c_int),
+    "mcg_set_kd_proposal": ([C.c_void_p, _dp, C.c_int64, _dp, _dp], C.c_int),
+    "mcg_kd_info": ([C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)], C.c_int),
+    "mcg_kd_export": ([C.c_void_p, _i32p, _dp, _i32p, _i32p, _i32p, _dp, _dp], C.c_int),
+    "mcg_init": ([C.c_void_p, C.c_int64, _dp, _dp, _dp], C.c_int),
+    "mcg_get_state": ([C.c_void_p, _dp, _dp, _dp], C.c_int),
+    "mcg_run": ([C.c_void_p, C.POINTER(McgRunOpts)], C.c_int),
+    "mcg_get_records": ([C.c_void_p, _dp, _dp, _dp, _u64p], C.c_int),
+    "mcg_last_run_steps": ([C.c_void_p], C.c_int64),
+    "mcg_get_counters": ([C.c_void_p, _u64p, _u64p], C.c_int),
+    "mcg_reset_counters": ([C.c_void_p], C.c_int),
+    "mcg_num_tiles": ([C.c_void_p], C.c_int64),
+    "mcg_tile_stats": ([C.c_void_p, _dp], C.c_int),
+    "mcg_tile_stats_device": ([C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)], C.c_int),
+    "mcg_combine_tiles": ([C.c_int32, C.c_int64, _dp, _dp, _dp, _dp], C.c_int),
+    "mcg_stats": ([C.c_void_p, _dp, _dp, _dp], C.c_int),
+    "mcg_nested": ([C.c_void_p, C.POINTER(McgNestedOpts), C.POINTER(McgNestedResult), OBSERVER,
+                    C.c_void_p], C.c_int),
+    "mcg_nested_get": ([C.c_void_p, _dp, _dp, _dp, _dp], C.c_int),
+    "mcg_log_total_error_estimate": ([C.c_double, C.c_double, C.c_int64], C.c_double),
+    "mcg_get_kernel_timing": ([C.c_void_p, C.c_char_p, C.POINTER(McgKernelTiming)], C.c_int),
+    "mcg_set_timing": ([C.c_void_p, C.c_int32], C.c_int),
+    "mcg_sync": ([C.c_void_p], C.c_int),
+}
+
+
+class McgError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("mcg error %d: %s" % (code, msg))
+        self.code = code
+
+
+class InvalidArgument(McgError):
+    """Raised where the reference raises Invalid_argument."""
+
+
+class Failure(McgError):
+    """Raised where the reference raises Failure (e.g. nested.ml:70-72)."""
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("libmcg.so not built (%s): run `python -c 'import __graft_entry__ as g; "
+                               "g.build()'` -- there is no CPU fallback" % LIB_PATH)
+        L = C.CDLL(LIB_PATH)
+        for name, (args, res) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = L
+    return _lib
+
+
+def check(rc, ctx_ptr=None):
+    if rc == MCG_OK:
+        return
+    msg = lib().mcg_last_error(ctx_ptr).decode() if ctx_ptr else ""
+    if rc == MCG_EINVAL:
+        raise InvalidArgument(rc, msg)
+    if rc == MCG_EFAIL:
+        raise Failure(rc, msg)
+    raise McgError(rc, msg)
+
+
+def dptr(a):
+    return None if a is None else a.ctypes.data_as(_dp)
+
+
+def u64ptr(a):
+    return None if a is None else a.ctypes.data_as(_u64p)
+
+
+def i32ptr(a):
+    return None if a is None else a.ctypes.data_as(_i32p)

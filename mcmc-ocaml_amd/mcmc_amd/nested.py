@@ -1,0 +1,62 @@
+"""Mirror of the reference's Nested module (nested.mli) over the HIP sampler."""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+from .context import Context
+
+
+def nested_evidence(log_likelihood, log_prior, epsrel=0.01, nmcmc=1000, nlive=1000,
+                    mode_hopping_frac=0.1, k=1, observer=None, ctx=None, seed=0, max_dead=0):
+    """Nested.nested_evidence (nested.ml:122-146).
+
+    log_prior must be a box prior (draw_prior = uniform in the box).  Returns the
+    nested_output tuple (nested.ml:20): (log_ev, log_dev, points (n, D), log_wts (n,)) where the
+    points are dead points in retirement order followed by the final live points ascending in
+    log-likelihood; `ll`, `lp` of every point are in the returned .ll / .lp attributes."""
+    ctx = ctx or Context(seed=seed)
+    ctx.set_model(log_likelihood, log_prior, None)
+    o = L.McgNestedOpts(nlive, nmcmc, k, epsrel, mode_hopping_frac, max_dead)
+    r = L.McgNestedResult()
+    D = log_likelihood.ndim
+
+    def _obs(user, pts, ll, lp, n):
+        if observer is not None:
+            p = np.ctypeslib.as_array(pts, shape=(n, D)).copy()
+            a = np.ctypeslib.as_array(ll, shape=(n,)).copy()
+            b = np.ctypeslib.as_array(lp, shape=(n,)).copy()
+            for i in range(n):
+                observer((p[i], a[i], b[i]))
+
+    cb = L.OBSERVER(_obs) if observer is not None else L.OBSERVER()
+    L.check(L.lib().mcg_nested(ctx.ptr, C.byref(o), C.byref(r), cb, None), ctx.ptr)
+    n = r.n_total
+    pts = np.zeros((n, D)); ll = np.zeros(n); lp = np.zeros(n); w = np.zeros(n)
+    L.check(L.lib().mcg_nested_get(ctx.ptr, L.dptr(pts), L.dptr(ll), L.dptr(lp), L.dptr(w)),
+            ctx.ptr)
+    return NestedOutput(r.log_ev, r.log_dev, pts, w, ll, lp, r.n_dead, r.n_gen)
+
+
+class NestedOutput(tuple):
+    def __new__(cls, log_ev, log_dev, pts, log_wts, ll, lp, n_dead, n_gen):
+        t = super().__new__(cls, (log_ev, log_dev, pts, log_wts))
+        t.ll, t.lp, t.n_dead, t.n_gen = ll, lp, n_dead, n_gen
+        return t
+
+
+def log_total_error_estimate(log_ev, log_dev, nlive):
+    """Nested.log_total_error_estimate (nested.ml:148-150)."""
+    return L.lib().mcg_log_total_error_estimate(log_ev, log_dev, nlive)
+
+
+def posterior_samples(n, output, rng=None):
+    """Nested.posterior_samples (nested.ml:152-178): multinomial resampling by cumulative weight
+    and the reference's binary search (host-side post-processing of the nested output)."""
+    _, _, pts, log_wts = output
+    rng = rng or np.random.default_rng(0)
+    sums = np.cumsum(np.exp(log_wts))
+    u = rng.random(n)
+    idx = np.searchsorted(sums, u, side="left")
+    idx = np.minimum(idx, len(sums) - 1)
+    return pts[idx]

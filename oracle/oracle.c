@@ -1,0 +1,1076 @@
+/*
+ * oracle.c -- CPU restatement of the farr/mcmc-ocaml hot path.  TEST INFRASTRUCTURE ONLY:
+ * loaded by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the CHECKER;
+ * the product library (libmcg.so) never links or calls it.
+ *
+ * Parity status: see oracle.h.  Every function cites the reference file:line it restates
+ * (paths relative to the farr/mcmc-ocaml root).  The randomness is injected: the OCaml stdlib
+ * Random stream is replaced by the Philox4x32-10 stream specified in DESIGN.md §RNG, which the
+ * HIP kernels draw identically, so GPU and oracle agree bit for bit.
+ *
+ * Build: oracle/Makefile  (gcc -O2 -ffp-contract=off; fma() is always explicit).
+ */
+#include "oracle.h"
+#include "mcg.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ======================================================================================
+ * RNG: Philox4x32-10 (Salmon et al. 2011) and variate conversions
+ * ====================================================================================== */
+#define PH_M0 0xD2511F53u
+#define PH_M1 0xCD9E8D57u
+#define PH_W0 0x9E3779B9u
+#define PH_W1 0xBB67AE85u
+
+void or_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+  uint32_t k0 = key[0], k1 = key[1];
+  for (int r = 0; r < 10; ++r) {
+    if (r > 0) { k0 += PH_W0; k1 += PH_W1; }
+    uint64_t p0 = (uint64_t)PH_M0 * c0;
+    uint64_t p1 = (uint64_t)PH_M1 * c2;
+    uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    uint32_t n1 = (uint32_t)p1;
+    uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    uint32_t n3 = (uint32_t)p0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* counter layout: (c0, c1, c2, (tag << 16) | hi16) ; key = (seed_lo, seed_hi) */
+#define TAG_MH 1u
+#define TAG_NEST_WALK 3u
+#define TAG_NEST_PRIOR 4u
+#define CALL_ACCEPT 0xFFFF0000u
+#define CALL_DE_IDX 0xFFFF0001u
+#define CALL_DE_SCALE 0xFFFF0002u
+#define CALL_KD_PICK 0xFFFF0003u
+#define CALL_START 0xFFFF0004u
+
+static inline void rng4(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t tag,
+                        uint32_t hi16, uint32_t out[4]) {
+  uint32_t ctr[4] = {c0, c1, c2, (tag << 16) | (hi16 & 0xFFFFu)};
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  or_philox(ctr, key, out);
+}
+
+/* uniform on (0,1): 52 random bits m -> (2m+1) 2^-53 */
+double or_u53(uint32_t w0, uint32_t w1) {
+  uint64_t m = ((uint64_t)w0 << 20) | (uint64_t)(w1 >> 12);
+  return (double)((m << 1) | 1u) * 0x1p-53;
+}
+
+/* uniform integer in [0,n): floor(u64 * n / 2^64) */
+uint32_t or_randint(uint32_t w0, uint32_t w1, uint32_t n) {
+  uint64_t u = ((uint64_t)w0 << 32) | (uint64_t)w1;
+  return (uint32_t)(((unsigned __int128)u * (unsigned __int128)n) >> 64);
+}
+
+/* ======================================================================================
+ * Portable fp64 math: identical operation sequence on the device (csrc/mcg_math.h).
+ * ====================================================================================== */
+static inline uint64_t dbits(double x) { uint64_t b; memcpy(&b, &x, 8); return b; }
+static inline double bitsd(uint64_t b) { double x; memcpy(&x, &b, 8); return x; }
+
+/* log for positive normal finite x (fdlibm e_log.c reduction and polynomial) */
+double or_log(double x) {
+  const double ln2_hi = 0x1.62e42fee00000p-1, ln2_lo = 0x1.a39ef35793c76p-33;
+  const double Lg1 = 0x1.5555555555593p-1, Lg2 = 0x1.999999997fa04p-2, Lg3 = 0x1.2492494229359p-2,
+               Lg4 = 0x1.c71c51d8e78afp-3, Lg5 = 0x1.7466496cb03dep-3, Lg6 = 0x1.39a09d078c69fp-3,
+               Lg7 = 0x1.2f112df3e5244p-3;
+  uint64_t b = dbits(x);
+  int k = (int)(b >> 52) - 1023;
+  double m = bitsd((b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
+  int big = m > 0x1.6a09e667f3bcdp+0;
+  m = big ? m * 0.5 : m;
+  k += big;
+  double f = m - 1.0;
+  double s = f / (2.0 + f);
+  double dk = (double)k;
+  double z = s * s;
+  double w = z * z;
+  double t1 = w * fma(w, fma(w, Lg6, Lg4), Lg2);
+  double t2 = z * fma(w, fma(w, fma(w, Lg7, Lg5), Lg3), Lg1);
+  double R = t2 + t1;
+  double hfsq = 0.5 * f * f;
+  return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+}
+
+/* exp for x <= 0 (used by log-space accumulators); returns 0 below -708, 1 at 0. */
+double or_exp(double x) {
+  if (!(x > -708.0)) return 0.0;   /* also NaN -> 0 is never reached by callers */
+  const double inv_ln2 = 0x1.71547652b82fep+0;
+  const double ln2_hi = 0x1.62e42fee00000p-1, ln2_lo = 0x1.a39ef35793c76p-33;
+  double kd = floor(fma(x, inv_ln2, 0.5));
+  double r = fma(-kd, ln2_hi, x);
+  r = fma(-kd, ln2_lo, r);
+  double p = 0x1.1eed8eff8d898p-29;          /* 1/12! */
+  p = fma(p, r, 0x1.ae64567f544e4p-26);      /* 1/11! */
+  p = fma(p, r, 0x1.27e4fb7789f5cp-22);      /* 1/10! */
+  p = fma(p, r, 0x1.71de3a556c734p-19);
+  p = fma(p, r, 0x1.a01a01a01a01ap-16);
+  p = fma(p, r, 0x1.a01a01a01a01ap-13);
+  p = fma(p, r, 0x1.6c16c16c16c17p-10);
+  p = fma(p, r, 0x1.1111111111111p-7);
+  p = fma(p, r, 0x1.5555555555555p-5);
+  p = fma(p, r, 0x1.5555555555555p-3);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  int k = (int)kd;
+  return p * bitsd((uint64_t)(k + 1023) << 52);
+}
+
+/* sqrt via a bit-trick rsqrt seed, 4 Newton steps and one residual correction */
+double or_sqrt(double a) {
+  double y = bitsd(0x5FE6EB50C7B537A9ull - (dbits(a) >> 1));
+  for (int i = 0; i < 4; ++i) {
+    double h = 0.5 * a * y;
+    double e = fma(-h, y, 0.5);
+    y = fma(y, e, y);
+  }
+  double r = a * y;
+  double d = fma(-r, r, a);
+  return fma(0.5 * y, d, r);
+}
+
+/* sin/cos on |t| <= pi/4 (fdlibm __kernel_sin/__kernel_cos coefficients, tail y = 0) */
+void or_sincos_kernel(double t, double* s, double* c) {
+  const double S1 = -0x1.5555555555549p-3, S2 = 0x1.111111110f8a6p-7, S3 = -0x1.a01a019c161d5p-13,
+               S4 = 0x1.71de357b1fe7dp-19, S5 = -0x1.ae5e68a2b9cebp-26, S6 = 0x1.5d93a5acfd57cp-33;
+  const double C1 = 0x1.555555555554cp-5, C2 = -0x1.6c16c16c15177p-10, C3 = 0x1.a01a019cb1590p-16,
+               C4 = -0x1.27e4f809c52adp-22, C5 = 0x1.1ee9ebdb4b1c4p-29, C6 = -0x1.8fae9be8838d4p-37;
+  double z = t * t;
+  double ps = fma(z, S6, S5);
+  ps = fma(z, ps, S4);
+  ps = fma(z, ps, S3);
+  ps = fma(z, ps, S2);
+  ps = fma(z, ps, S1);
+  double v = z * t;
+  *s = fma(v, ps, t);
+  double pc = fma(z, C6, C5);
+  pc = fma(z, pc, C4);
+  pc = fma(z, pc, C3);
+  pc = fma(z, pc, C2);
+  pc = fma(z, pc, C1);
+  double r = z * pc;
+  double hz = 0.5 * z;
+  double w = 1.0 - hz;
+  *c = w + (((1.0 - w) - hz) + z * r);
+}
+
+/* Box-Muller from two 32-bit words: radius from a, angle from b (quadrant-exact reduction). */
+void or_normal_pair(uint32_t a, uint32_t b, double* z0, double* z1) {
+  double u1 = ((double)a + 0.5) * 0x1p-32;
+  double rho = or_sqrt(-2.0 * or_log(u1));
+  uint64_t bb = (uint64_t)b + 0x20000000ull;
+  uint32_t q = (uint32_t)(bb >> 30) & 3u;
+  int64_t ri = (int64_t)(bb & 0x3FFFFFFFull) - 0x20000000ll;
+  double th = (((double)ri + 0.5) * 0x1p-30) * 0x1.921fb54442d18p+0;
+  double s, c;
+  or_sincos_kernel(th, &s, &c);
+  double cs = (q == 0) ? c : (q == 1) ? -s : (q == 2) ? -c : s;
+  double sn = (q == 0) ? s : (q == 1) ? c : (q == 2) ? -s : -c;
+  *z0 = rho * cs;
+  *z1 = rho * sn;
+}
+
+/* dims 4c..4c+3 of a step take Philox call c: pair (w0,w1) -> z[4c], z[4c+1]; (w2,w3) -> +2,+3 */
+static void normals_tagged(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t tag, uint32_t hi16,
+                           int D, double* z) {
+  for (int c = 0; 4 * c < D; ++c) {
+    uint32_t w[4];
+    rng4(seed, c0, c1, (uint32_t)c, tag, hi16, w);
+    double t[4];
+    or_normal_pair(w[0], w[1], &t[0], &t[1]);
+    or_normal_pair(w[2], w[3], &t[2], &t[3]);
+    for (int j = 0; j < 4 && 4 * c + j < D; ++j) z[4 * c + j] = t[j];
+  }
+}
+
+void or_step_normals(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, int D, double* z) {
+  normals_tagged(seed, chain, (uint32_t)step, tag, (uint32_t)(step >> 32), D, z);
+}
+
+/* ======================================================================================
+ * Stats restatements (stats.ml)
+ * ====================================================================================== */
+double or_log_sum_logs(double a, double b) {      /* stats.ml:240-248 */
+  if (a == -INFINITY && b == -INFINITY) return -INFINITY;
+  if (b > a) { double t = a; a = b; b = t; }
+  return a + log1p(exp(b - a));
+}
+
+double or_mean(const double* xs, int64_t n) {     /* stats.ml:17-23 */
+  double s = 0.0;
+  for (int64_t i = 0; i < n; ++i) s = s + xs[i];
+  return s / (double)n;
+}
+
+double or_std(const double* xs, int64_t n) {      /* stats.ml:35-43 */
+  double mu = or_mean(xs, n), v = 0.0;
+  for (int64_t i = 0; i < n; ++i) { double x = xs[i] - mu; v = v + x * x; }
+  return sqrt(v / (double)(n - 1));
+}
+
+void or_multi_mean(const double* xs, int64_t n, int d, double* mu) {   /* stats.ml:58-70 */
+  for (int j = 0; j < d; ++j) mu[j] = 0.0;
+  for (int64_t i = 0; i < n; ++i)
+    for (int j = 0; j < d; ++j) mu[j] = mu[j] + xs[i * d + j];
+  for (int j = 0; j < d; ++j) mu[j] = mu[j] / (double)n;
+}
+
+void or_multi_std(const double* xs, int64_t n, int d, double* sd) {    /* stats.ml:72-87 */
+  double* mu = (double*)malloc(sizeof(double) * (size_t)d);
+  or_multi_mean(xs, n, d, mu);
+  for (int j = 0; j < d; ++j) sd[j] = 0.0;
+  for (int64_t i = 0; i < n; ++i)
+    for (int j = 0; j < d; ++j) { double dx = xs[i * d + j] - mu[j]; sd[j] = sd[j] + dx * dx; }
+  for (int j = 0; j < d; ++j) sd[j] = sqrt(sd[j] / (double)(n - 1));
+  free(mu);
+}
+
+static const double NEG_HALF_LOG_2PI = -0.91893853320467274178;
+static const double OR_PI = 3.14159265358979323846;
+
+double or_log_gaussian(double mu, double sigma, double x) {            /* stats.ml:98-101 */
+  double dx = (x - mu) / sigma;
+  return NEG_HALF_LOG_2PI - log(sigma) - 0.5 * dx * dx;
+}
+
+double or_log_cauchy(double x0, double gamma, double x) {             /* stats.ml:93-96 */
+  double dx = (x - x0) / gamma;
+  return 0.0 - log(OR_PI * gamma) - log(1.0 + dx * dx);
+}
+
+double or_log_multi_gaussian(const double* mu, const double* sigma, const double* x, int d) {
+  double r = 0.0;                                                      /* stats.ml:103-108 */
+  for (int i = 0; i < d; ++i) r = r + or_log_gaussian(mu[i], sigma[i], x[i]);
+  return r + 0.0;
+}
+
+double or_log_lognormal(double mu, double sigma, double x) {          /* stats.ml:217-221 */
+  double lx = log(x), d = (lx - mu) / sigma, ls = log(sigma);
+  return NEG_HALF_LOG_2PI - lx - ls - 0.5 * d * d;
+}
+
+/* ======================================================================================
+ * Model preparation (host-side constants shared with libmcg's mcg_set_* semantics)
+ * ====================================================================================== */
+typedef struct {
+  int D, lik, prior, prop;
+  double* mu; double* isig; double C;          /* DIAG_GAUSS / FULLCOV (mu) */
+  const double* U;                             /* FULLCOV */
+  double* ctr; double R, iw;                   /* SHELL */
+  int nd; int64_t nsamp; const double* data;   /* GAUSS_DATA / CAUCHY_DATA */
+  const double* lo; const double* hi; double lp_in;   /* BOX priors */
+  double* s;                                   /* GAUSS proposal scales [D] */
+  const double* wlo; const double* whi; const double* wdx;   /* WRAP_UNIFORM */
+  const or_kd* kd;
+} prep_t;
+
+static void prep_free(prep_t* p) {
+  free(p->mu); free(p->isig); free(p->ctr); free(p->s);
+}
+
+static int prep_model(const or_model* m, prep_t* p) {
+  memset(p, 0, sizeof(*p));
+  int D = m->ndim;
+  p->D = D; p->lik = m->lik_kind; p->prior = m->prior_kind; p->prop = m->prop_kind;
+  const double* q = m->lik_params;
+  switch (p->lik) {
+    case MCG_LIK_FLAT: break;
+    case MCG_LIK_DIAG_GAUSS:
+      p->mu = (double*)malloc(sizeof(double) * D);
+      p->isig = (double*)malloc(sizeof(double) * D);
+      p->C = 0.0;
+      for (int d = 0; d < D; ++d) {
+        p->mu[d] = q[d];
+        p->isig[d] = 1.0 / q[D + d];
+        p->C = p->C + (NEG_HALF_LOG_2PI - log(q[D + d]));
+      }
+      break;
+    case MCG_LIK_FULLCOV_GAUSS:
+      p->mu = (double*)malloc(sizeof(double) * D);
+      for (int d = 0; d < D; ++d) p->mu[d] = q[d];
+      p->U = q + D;
+      p->C = 0.0;
+      for (int i = 0; i < D; ++i) p->C = p->C + (log(p->U[i * D + i]) + NEG_HALF_LOG_2PI);
+      break;
+    case MCG_LIK_GAUSS_SHELL:
+      p->ctr = (double*)malloc(sizeof(double) * D);
+      for (int d = 0; d < D; ++d) p->ctr[d] = q[d];
+      p->R = q[D];
+      p->iw = 1.0 / q[D + 1];
+      p->C = NEG_HALF_LOG_2PI - log(q[D + 1]);
+      break;
+    case MCG_LIK_GAUSS_DATA:
+    case MCG_LIK_CAUCHY_DATA:
+      p->nd = (int)q[0];
+      p->data = q + 1;
+      p->nsamp = (m->n_lik_params - 1) / p->nd;
+      break;
+    default: return -1;
+  }
+  if (p->prior == MCG_PRIOR_BOX || p->prior == MCG_PRIOR_OPEN_BOX) {
+    p->lo = m->prior_params; p->hi = m->prior_params + D; p->lp_in = m->prior_params[2 * D];
+  }
+  if (p->prop == MCG_PROP_GAUSS) {
+    p->s = (double*)malloc(sizeof(double) * D);
+    for (int d = 0; d < D; ++d) p->s[d] = (m->n_prop_params == 1) ? m->prop_params[0] : m->prop_params[d];
+  } else if (p->prop == MCG_PROP_WRAP_UNIFORM) {
+    p->wlo = m->prop_params; p->whi = m->prop_params + D; p->wdx = m->prop_params + 2 * D;
+  } else if (p->prop == MCG_PROP_KD_INTERP) {
+    p->kd = (const or_kd*)m->kd;
+  }
+  return 0;
+}
+
+/* canonical 8-accumulator sum: term of dim d goes to A[(d>>2)&7] (sequential in d), then
+   S = ((A0+A4)+(A2+A6)) + ((A1+A5)+(A3+A7)).  Independent of how many lanes share a chain. */
+static inline double canon8(const double* A) {
+  return ((A[0] + A[4]) + (A[2] + A[6])) + ((A[1] + A[5]) + (A[3] + A[7]));
+}
+
+static double lik_eval(const prep_t* p, const double* x) {
+  int D = p->D;
+  double A[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  switch (p->lik) {
+    case MCG_LIK_FLAT: return 0.0;
+    case MCG_LIK_DIAG_GAUSS: {
+      for (int d = 0; d < D; ++d) {
+        double e = (x[d] - p->mu[d]) * p->isig[d];
+        A[(d >> 2) & 7] = fma(e, e, A[(d >> 2) & 7]);
+      }
+      return p->C - 0.5 * canon8(A);
+    }
+    case MCG_LIK_FULLCOV_GAUSS: {
+      double r[256];
+      for (int d = 0; d < D; ++d) r[d] = x[d] - p->mu[d];
+      for (int i = 0; i < D; ++i) {
+        double t = 0.0;
+        for (int j = i; j < D; ++j) t = fma(p->U[i * D + j], r[j], t);
+        A[(i >> 2) & 7] = fma(t, t, A[(i >> 2) & 7]);
+      }
+      return p->C - 0.5 * canon8(A);
+    }
+    case MCG_LIK_GAUSS_SHELL: {
+      for (int d = 0; d < D; ++d) {
+        double e = x[d] - p->ctr[d];
+        A[(d >> 2) & 7] = fma(e, e, A[(d >> 2) & 7]);
+      }
+      double r = or_sqrt(canon8(A));
+      double qq = (r - p->R) * p->iw;
+      return p->C - 0.5 * qq * qq;
+    }
+    case MCG_LIK_GAUSS_DATA:
+    case MCG_LIK_CAUCHY_DATA: {
+      /* bin/gaussian_cauchy.ml:149-164: sum_i sum_j prob mu_j sigma_j samp_ij */
+      int nd = p->nd;
+      const double* mu = x;
+      const double* sg = x + nd;
+      double lterm[64];
+      for (int j = 0; j < nd; ++j)
+        lterm[j] = (p->lik == MCG_LIK_GAUSS_DATA) ? or_log(sg[j]) : or_log(OR_PI * sg[j]);
+      double acc = 0.0;
+      for (int64_t i = 0; i < p->nsamp; ++i) {
+        for (int j = 0; j < nd; ++j) {
+          double dx = (p->data[i * nd + j] - mu[j]) / sg[j];
+          double term;
+          if (p->lik == MCG_LIK_GAUSS_DATA)
+            term = (NEG_HALF_LOG_2PI - lterm[j]) - 0.5 * dx * dx;     /* stats.ml:98-101 */
+          else
+            term = (0.0 - lterm[j]) - or_log(1.0 + dx * dx);          /* stats.ml:93-96 */
+          acc = acc + term;
+        }
+      }
+      return acc + 0.0;
+    }
+  }
+  return NAN;
+}
+
+static double prior_eval(const prep_t* p, const double* x) {
+  if (p->prior == MCG_PRIOR_FLAT) return 0.0;
+  int inb = 1;
+  for (int d = 0; d < p->D; ++d) {
+    if (p->prior == MCG_PRIOR_BOX) inb &= (x[d] >= p->lo[d]) & (x[d] <= p->hi[d]);
+    else inb &= (x[d] > p->lo[d]) & (x[d] < p->hi[d]);
+  }
+  return inb ? p->lp_in : -INFINITY;
+}
+
+double or_loglik(const or_model* m, const double* x) {
+  prep_t p; prep_model(m, &p); double v = lik_eval(&p, x); prep_free(&p); return v;
+}
+double or_logprior(const or_model* m, const double* x) {
+  prep_t p; prep_model(m, &p); double v = prior_eval(&p, x); prep_free(&p); return v;
+}
+
+/* Mcmc.uniform_wrapping (mcmc.ml:187-196) with the uniform injected */
+static double wrap_uniform(double xmin, double xmax, double dx, double x, double u) {
+  double nx = x + (u - 0.5) * dx;
+  for (int it = 0; it < 64; ++it) {
+    if (nx < xmin) nx = xmin + (xmin - nx);
+    else if (nx >= xmax) nx = xmax - (nx - xmax);
+    else break;
+  }
+  return nx;
+}
+
+/* ======================================================================================
+ * kD tree (kd_tree.ml) + Interpolate_pdf (interpolate_pdf.ml) -- declared here, defined below
+ * ====================================================================================== */
+struct or_kd {
+  int D; int64_t M;
+  int64_t nn, nl, cap_n, cap_l;
+  int32_t* dim; double* split; int32_t* right; int32_t* leaf;
+  int32_t* lcount; double* lbox; double* llogq;
+  double* root_lo; double* root_hi;
+  double* pts;                               /* copy of the M training points [M][D] */
+};
+
+static int64_t kd_find_leaf_idx(const or_kd* t, const double* pt);
+
+/* ======================================================================================
+ * One MH step (mcmc.ml:37-56) for one chain, RNG injected
+ * ====================================================================================== */
+typedef struct {
+  double x[256]; double ll, lp; double lq;   /* lq: cached log q(x) for KD_INTERP */
+} chain_t;
+
+static int mh_step(const prep_t* p, uint64_t seed, uint32_t gid, uint64_t T, chain_t* c) {
+  int D = p->D;
+  uint32_t lo = (uint32_t)T, hi = (uint32_t)(T >> 32);
+  double y[256];
+  double lf = 0.0, lb = 0.0, lqy = 0.0;
+  switch (p->prop) {
+    case MCG_PROP_GAUSS: {
+      double z[256];
+      normals_tagged(seed, gid, lo, TAG_MH, hi, D, z);
+      for (int d = 0; d < D; ++d) y[d] = c->x[d] + p->s[d] * z[d];
+      break;
+    }
+    case MCG_PROP_WRAP_UNIFORM: {
+      for (int d = 0; d < D; d += 2) {
+        uint32_t w[4];
+        rng4(seed, gid, lo, (uint32_t)(d >> 1), TAG_MH, hi, w);
+        y[d] = wrap_uniform(p->wlo[d], p->whi[d], p->wdx[d], c->x[d], or_u53(w[0], w[1]));
+        if (d + 1 < D)
+          y[d + 1] = wrap_uniform(p->wlo[d + 1], p->whi[d + 1], p->wdx[d + 1], c->x[d + 1],
+                                  or_u53(w[2], w[3]));
+      }
+      break;
+    }
+    case MCG_PROP_KD_INTERP: {
+      /* Interpolate_pdf.draw (interpolate_pdf.ml:114-119): pick a training point, find its
+         leaf, draw uniformly in the leaf box. */
+      const or_kd* t = p->kd;
+      uint32_t w[4];
+      rng4(seed, gid, lo, CALL_KD_PICK, TAG_MH, hi, w);
+      uint32_t pick = or_randint(w[0], w[1], (uint32_t)t->M);
+      const double* pt = t->pts + (int64_t)pick * D;
+      int64_t L = kd_find_leaf_idx(t, pt);
+      const double* blo = t->lbox + L * 2 * D;
+      const double* bhi = blo + D;
+      for (int d = 0; d < D; d += 2) {
+        rng4(seed, gid, lo, (uint32_t)(d >> 1), TAG_MH, hi, w);
+        y[d] = blo[d] + (bhi[d] - blo[d]) * or_u53(w[0], w[1]);
+        if (d + 1 < D) y[d + 1] = blo[d + 1] + (bhi[d + 1] - blo[d + 1]) * or_u53(w[2], w[3]);
+      }
+      lqy = t->llogq[kd_find_leaf_idx(t, y)];
+      lf = lqy;         /* log_jump_prob start proposed = log q(proposed) */
+      lb = c->lq;       /* log_jump_prob proposed start = log q(start) */
+      break;
+    }
+    default: return -1;
+  }
+  double lly = lik_eval(p, y);
+  double lpy = prior_eval(p, y);
+  double post_y = lly + lpy;
+  double post_x = c->ll + c->lp;
+  double ratio = ((post_y - post_x) + lb) - lf;
+  uint32_t w[4];
+  rng4(seed, gid, lo, CALL_ACCEPT, TAG_MH, hi, w);
+  double lu = or_log(or_u53(w[0], w[1]));
+  if (lu < ratio) {
+    for (int d = 0; d < D; ++d) c->x[d] = y[d];
+    c->ll = lly; c->lp = lpy; c->lq = lqy;
+    return 1;
+  }
+  return 0;
+}
+
+/* ======================================================================================
+ * Batched mcmc_array (mcmc.ml:58-72) with records, bitmap and running accumulators
+ * ====================================================================================== */
+typedef struct {
+  const prep_t* p; uint64_t seed; uint32_t chain_offset; int64_t N; uint64_t step0;
+  double* x; double* ll; double* lp; uint64_t* nacc; const or_run_opts* o;
+  double* rec_x; double* rec_ll; double* rec_lp; uint64_t* bits; or_accum* acc;
+  int64_t i0, i1; int status;
+} mh_job;
+
+static void record_sample(mh_job* j, int64_t i, int64_t r, const chain_t* c) {
+  const or_run_opts* o = j->o;
+  int D = j->p->D;
+  int64_t N = j->N;
+  if (o->record_x && j->rec_x)
+    for (int d = 0; d < D; ++d) j->rec_x[(r * D + d) * N + i] = c->x[d];
+  if (o->record_llp) {
+    if (j->rec_ll) j->rec_ll[r * N + i] = c->ll;
+    if (j->rec_lp) j->rec_lp[r * N + i] = c->lp;
+  }
+  if (o->accumulate && j->acc) {
+    or_accum* a = j->acc;
+    double inv = 1.0 / (double)(r + 1);
+    for (int d = 0; d < D; ++d) {
+      double* mean = &a->mean[(int64_t)d * N + i];
+      double* m2 = &a->m2[(int64_t)d * N + i];
+      double delta = c->x[d] - *mean;
+      *mean = fma(delta, inv, *mean);
+      *m2 = fma(delta, c->x[d] - *mean, *m2);
+    }
+    double v = -c->ll;
+    if (r == 0) { a->hm_m[i] = v; a->hm_s[i] = 1.0; }
+    else {
+      double m = a->hm_m[i], s = a->hm_s[i];
+      double e = (v == m) ? 1.0 : or_exp(-fabs(v - m));
+      if (v > m) { s = s * e + 1.0; m = v; } else { s = s + e; }
+      a->hm_m[i] = m; a->hm_s[i] = s;
+    }
+  }
+}
+
+static void* mh_worker(void* arg) {
+  mh_job* j = (mh_job*)arg;
+  const prep_t* p = j->p;
+  const or_run_opts* o = j->o;
+  int D = p->D;
+  int64_t nsteps = o->nbin + (o->n_rec > 0 ? (o->n_rec - 1) * o->nskip : 0);
+  int64_t words = (j->N + 63) / 64;
+  chain_t c;
+  for (int64_t i = j->i0; i < j->i1; ++i) {
+    for (int d = 0; d < D; ++d) c.x[d] = j->x[(int64_t)d * j->N + i];
+    c.ll = j->ll[i]; c.lp = j->lp[i];
+    c.lq = 0.0;
+    if (p->prop == MCG_PROP_KD_INTERP) c.lq = p->kd->llogq[kd_find_leaf_idx(p->kd, c.x)];
+    uint32_t gid = j->chain_offset + (uint32_t)i;
+    if (o->nbin == 0 && o->n_rec > 0) record_sample(j, i, 0, &c);
+    uint64_t na = 0;
+    for (int64_t t = 0; t < nsteps; ++t) {
+      int a = mh_step(p, j->seed, gid, j->step0 + (uint64_t)t, &c);
+      if (a < 0) { j->status = -1; return NULL; }
+      na += (uint64_t)a;
+      if (o->record_accept && j->bits && a)
+        j->bits[t * words + (i >> 6)] |= (1ull << (i & 63));
+      int64_t t1 = t + 1;
+      if (t1 >= o->nbin && ((t1 - o->nbin) % o->nskip) == 0) {
+        int64_t r = (t1 - o->nbin) / o->nskip;
+        if (r < o->n_rec) record_sample(j, i, r, &c);
+      }
+    }
+    for (int d = 0; d < D; ++d) j->x[(int64_t)d * j->N + i] = c.x[d];
+    j->ll[i] = c.ll; j->lp[i] = c.lp;
+    j->nacc[i] += na;
+  }
+  return NULL;
+}
+
+int or_mh_run(const or_model* m, uint64_t seed, uint32_t chain_offset, int64_t N, uint64_t step0,
+              double* x, double* ll, double* lp, uint64_t* nacc, const or_run_opts* o,
+              double* rec_x, double* rec_ll, double* rec_lp, uint64_t* accept_bits,
+              or_accum* acc, int nthreads) {
+  if (m->ndim < 1 || m->ndim > 256 || N < 1 || o->nskip < 1) return -1;
+  prep_t p;
+  if (prep_model(m, &p) != 0) return -1;
+  if (nthreads < 1) nthreads = 1;
+  int64_t blocks = (N + 63) / 64;
+  if (nthreads > blocks) nthreads = (int)blocks;
+  mh_job* jobs = (mh_job*)calloc((size_t)nthreads, sizeof(mh_job));
+  pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+  int64_t per = (blocks + nthreads - 1) / nthreads;
+  for (int t = 0; t < nthreads; ++t) {
+    mh_job* j = &jobs[t];
+    j->p = &p; j->seed = seed; j->chain_offset = chain_offset; j->N = N; j->step0 = step0;
+    j->x = x; j->ll = ll; j->lp = lp; j->nacc = nacc; j->o = o;
+    j->rec_x = rec_x; j->rec_ll = rec_ll; j->rec_lp = rec_lp; j->bits = accept_bits; j->acc = acc;
+    j->i0 = t * per * 64; j->i1 = (t + 1) * per * 64;
+    if (j->i0 > N) j->i0 = N;
+    if (j->i1 > N) j->i1 = N;
+  }
+  if (nthreads == 1) mh_worker(&jobs[0]);
+  else {
+    for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, mh_worker, &jobs[t]);
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+  }
+  int status = 0;
+  for (int t = 0; t < nthreads; ++t) if (jobs[t].status) status = jobs[t].status;
+  free(jobs); free(th);
+  prep_free(&p);
+  return status;
+}
+
+/* ======================================================================================
+ * Tile statistics: Chan/Welford pairwise combine + log-space harmonic-mean partials
+ * ====================================================================================== */
+static void comb(int D, double* a, const double* b) {
+  /* entry layout: n, mean[D], m2[D], hm_m, hm_s */
+  double na = a[0], nb = b[0];
+  if (nb == 0.0) return;
+  if (na == 0.0) { memcpy(a, b, sizeof(double) * (size_t)(2 * D + 3)); return; }
+  double n = na + nb;
+  double fb = nb / n;
+  double fab = (na * nb) / n;
+  for (int d = 0; d < D; ++d) {
+    double delta = b[1 + d] - a[1 + d];
+    a[1 + d] = a[1 + d] + delta * fb;
+    a[1 + D + d] = (a[1 + D + d] + b[1 + D + d]) + (delta * delta) * fab;
+  }
+  double ma = a[2 * D + 1], sa = a[2 * D + 2], mb = b[2 * D + 1], sb = b[2 * D + 2];
+  double mm = (ma > mb) ? ma : mb;
+  a[2 * D + 1] = mm;
+  a[2 * D + 2] = sa * or_exp(ma - mm) + sb * or_exp(mb - mm);
+  a[0] = n;
+}
+
+void or_tile_stats(int D, int64_t N, int64_t nrec, const or_accum* acc, double* tiles) {
+  int W = 2 * D + 3;
+  int64_t ntiles = (N + 255) / 256;
+  double* e = (double*)malloc(sizeof(double) * 256 * (size_t)W);
+  for (int64_t t = 0; t < ntiles; ++t) {
+    for (int i = 0; i < 256; ++i) {
+      int64_t c = t * 256 + i;
+      double* ei = e + (size_t)i * W;
+      if (c < N && nrec > 0) {
+        ei[0] = (double)nrec;
+        for (int d = 0; d < D; ++d) {
+          ei[1 + d] = acc->mean[(int64_t)d * N + c];
+          ei[1 + D + d] = acc->m2[(int64_t)d * N + c];
+        }
+        ei[2 * D + 1] = acc->hm_m[c];
+        ei[2 * D + 2] = acc->hm_s[c];
+      } else {
+        memset(ei, 0, sizeof(double) * (size_t)W);
+        ei[2 * D + 1] = -INFINITY;
+      }
+    }
+    for (int s = 128; s >= 1; s >>= 1)
+      for (int i = 0; i < s; ++i) comb(D, e + (size_t)i * W, e + (size_t)(i + s) * W);
+    memcpy(tiles + (size_t)t * W, e, sizeof(double) * (size_t)W);
+  }
+  free(e);
+}
+
+void or_combine_tiles(int D, int64_t ntiles, const double* tiles, double* mean, double* sd,
+                      double* log_z_hm) {
+  int W = 2 * D + 3;
+  double* a = (double*)calloc((size_t)W, sizeof(double));
+  a[2 * D + 1] = -INFINITY;
+  for (int64_t t = 0; t < ntiles; ++t) comb(D, a, tiles + (size_t)t * W);
+  double n = a[0];
+  for (int d = 0; d < D; ++d) {
+    mean[d] = a[1 + d];
+    sd[d] = sqrt(a[1 + D + d] / (n - 1.0));
+  }
+  *log_z_hm = log(n) - (a[2 * D + 1] + log(a[2 * D + 2]));
+  free(a);
+}
+
+double or_harmonic_mean_naive(const double* ll, int64_t n) {   /* evidence.ml:101-107 */
+  double linv = 0.0;
+  for (int64_t i = 0; i < n; ++i) linv = linv + 1.0 / exp(ll[i]);
+  return (double)n / linv;
+}
+
+/* ======================================================================================
+ * Nested sampling (nested.ml), slot semantics, k retired per generation
+ * ====================================================================================== */
+typedef struct { double ll; int64_t tie; int32_t slot; } nkey_t;
+
+static int key_less(const nkey_t* a, const nkey_t* b) {
+  if (a->ll < b->ll) return 1;
+  if (a->ll > b->ll) return 0;
+  return a->tie < b->tie;
+}
+
+static int key_cmp(const void* a, const void* b) {
+  const nkey_t* x = (const nkey_t*)a;
+  const nkey_t* y = (const nkey_t*)b;
+  if (key_less(x, y)) return -1;
+  if (key_less(y, x)) return 1;
+  return 0;
+}
+
+/* fixed pairwise tree log-sum over v[0..n): pad to a power of two with -inf, combine i, i+s */
+static double tree_lse(double* v, int64_t n) {
+  int64_t p2 = 1;
+  while (p2 < n) p2 <<= 1;
+  for (int64_t i = n; i < p2; ++i) v[i] = -INFINITY;
+  for (int64_t s = p2 >> 1; s >= 1; s >>= 1)
+    for (int64_t i = 0; i < s; ++i) v[i] = or_log_sum_logs(v[i], v[i + s]);
+  return v[0];
+}
+
+int or_nested(const or_model* m, uint64_t seed, const or_nested_opts* o, double* pts, double* lls,
+              double* lps, double* log_wts, int64_t cap, or_nested_result* res) {
+  prep_t p;
+  if (prep_model(m, &p) != 0) return -1;
+  int D = p.D;
+  int64_t n = o->nlive, k = o->k;
+  if (n < 2 || k < 1 || k >= n || D > 256 || !(p.prior == MCG_PRIOR_BOX || p.prior == MCG_PRIOR_OPEN_BOX)) {
+    prep_free(&p); return -1;
+  }
+  double* lx = (double*)malloc(sizeof(double) * (size_t)(n * D));   /* live AoS [slot][D] */
+  double* lll = (double*)malloc(sizeof(double) * (size_t)n);
+  double* llp = (double*)malloc(sizeof(double) * (size_t)n);
+  nkey_t* keys = (nkey_t*)malloc(sizeof(nkey_t) * (size_t)n);
+  nkey_t* nk = (nkey_t*)malloc(sizeof(nkey_t) * (size_t)n);
+  double* nx = (double*)malloc(sizeof(double) * (size_t)(k * D));
+  double* nll = (double*)malloc(sizeof(double) * (size_t)k);
+  double* nlp = (double*)malloc(sizeof(double) * (size_t)k);
+  int64_t p2 = 1; while (p2 < k) p2 <<= 1;
+  double* tv = (double*)malloc(sizeof(double) * (size_t)p2);
+  double* prefix = (double*)malloc(sizeof(double) * (size_t)(k + 1));
+  /* prefix[j] = sum_{j'<j} log1p(-1/(n-j')) -- volume after j retirements in a generation */
+  prefix[0] = 0.0;
+  for (int64_t j = 0; j < k; ++j) prefix[j + 1] = prefix[j] + log1p(-1.0 / (double)(n - j));
+  /* draw_prior: uniform in the box (Stats.draw_uniform, stats.ml:126-128) */
+  for (int64_t s = 0; s < n; ++s) {
+    for (int d = 0; d < D; d += 2) {
+      uint32_t w[4];
+      rng4(seed, (uint32_t)s, 0u, (uint32_t)(d >> 1), TAG_NEST_PRIOR, 0u, w);
+      lx[s * D + d] = p.lo[d] + (p.hi[d] - p.lo[d]) * or_u53(w[0], w[1]);
+      if (d + 1 < D) lx[s * D + d + 1] = p.lo[d + 1] + (p.hi[d + 1] - p.lo[d + 1]) * or_u53(w[2], w[3]);
+    }
+    lll[s] = lik_eval(&p, lx + s * D);
+    llp[s] = prior_eval(&p, lx + s * D);
+    keys[s].ll = lll[s]; keys[s].tie = s; keys[s].slot = (int32_t)s;
+  }
+  qsort(keys, (size_t)n, sizeof(nkey_t), key_cmp);   /* total order: (ll, tie) unique */
+  double sigma_de = 2.38 / sqrt(2.0 * (double)D);   /* mcmc.ml:212 */
+  double log_vol = 0.0, est = -INFINITY;
+  int64_t mrep = 0, ndead = 0, gen = 0;
+  int status = 0;
+  int64_t max_iter = o->max_iter > 0 ? o->max_iter : 1000 * n;
+  for (;;) {
+    double thr = keys[k - 1].ll;
+    /* k constrained DE-MCMC walkers (nested.ml:50-74) */
+    for (int64_t w = 0; w < k; ++w) {
+      uint32_t wid = (uint32_t)(mrep + w);
+      uint32_t rw[4];
+      int64_t start = -1;
+      for (uint32_t a = 0; a < 4096; ++a) {
+        rng4(seed, wid, a, CALL_START, TAG_NEST_WALK, 0u, rw);
+        uint32_t r = or_randint(rw[0], rw[1], (uint32_t)n);
+        if (lll[r] >= thr) { start = r; break; }
+      }
+      if (start < 0) start = keys[k - 1].slot;
+      double cur[256], y[256];
+      for (int d = 0; d < D; ++d) cur[d] = lx[start * D + d];
+      double cur_l = (lll[start] >= thr) ? llp[start] : -INFINITY;   /* mcmc_logl, :54-59 */
+      for (int64_t s = 0; s < o->nmcmc; ++s) {
+        rng4(seed, wid, (uint32_t)s, CALL_DE_IDX, TAG_NEST_WALK, 0u, rw);
+        uint32_t i = or_randint(rw[0], rw[1], (uint32_t)n);
+        uint32_t jj = or_randint(rw[2], rw[3], (uint32_t)(n - 1));
+        uint32_t j = jj + (jj >= i);
+        rng4(seed, wid, (uint32_t)s, CALL_DE_SCALE, TAG_NEST_WALK, 0u, rw);
+        double dsc;
+        if (o->mode_hop != 0.0 && or_u53(rw[0], rw[1]) < o->mode_hop) dsc = 1.0;
+        else { double z0, z1; or_normal_pair(rw[2], rw[3], &z0, &z1); dsc = sigma_de * z0; }
+        for (int d = 0; d < D; ++d) y[d] = cur[d] + dsc * (lx[(int64_t)j * D + d] - lx[(int64_t)i * D + d]);
+        double lly = lik_eval(&p, y);
+        double ml = (lly >= thr) ? prior_eval(&p, y) : -INFINITY;
+        double ratio = (((ml + 0.0) - (cur_l + 0.0)) + 0.0) - 0.0;
+        rng4(seed, wid, (uint32_t)s, CALL_ACCEPT, TAG_NEST_WALK, 0u, rw);
+        double lu = or_log(or_u53(rw[0], rw[1]));
+        if (lu < ratio) { for (int d = 0; d < D; ++d) cur[d] = y[d]; cur_l = ml; }
+      }
+      for (int d = 0; d < D; ++d) nx[w * D + d] = cur[d];
+      nll[w] = lik_eval(&p, cur);
+      nlp[w] = prior_eval(&p, cur);
+      if (!(nll[w] >= thr)) status = -2;                    /* nested.ml:70-72 */
+    }
+    if (status) break;
+    /* retire the k lowest (in key order), update the running estimate (nested.ml:138-141) */
+    for (int64_t j = 0; j < k; ++j) {
+      int32_t sl = keys[j].slot;
+      if (ndead >= cap) { status = -1; break; }
+      memcpy(pts + ndead * D, lx + (int64_t)sl * D, sizeof(double) * (size_t)D);
+      lls[ndead] = lll[sl]; lps[ndead] = llp[sl];
+      ++ndead;
+      double nj = (double)(n - j);
+      double lv = log_vol + prefix[j];
+      double log_dv = o->ref_stop_quirk ? lv + 1.0 / nj : lv + log(1.0 / nj);
+      tv[j] = lll[sl] + log_dv;
+    }
+    if (status) break;
+    est = (k == 1) ? or_log_sum_logs(est, tv[0]) : or_log_sum_logs(est, tree_lse(tv, k));
+    log_vol = log_vol + prefix[k];
+    /* replace the retired slots (slot semantics of nested.ml:26-43) */
+    for (int64_t j = 0; j < k; ++j) {
+      int32_t sl = keys[j].slot;
+      memcpy(lx + (int64_t)sl * D, nx + j * D, sizeof(double) * (size_t)D);
+      lll[sl] = nll[j]; llp[sl] = nlp[j];
+      nk[j].ll = nll[j]; nk[j].tie = -(mrep + j + 1); nk[j].slot = sl;
+    }
+    qsort(nk, (size_t)k, sizeof(nkey_t), key_cmp);
+    /* merge survivors keys[k..n) with new sorted nk[0..k) */
+    {
+      nkey_t* out = (nkey_t*)malloc(sizeof(nkey_t) * (size_t)n);
+      int64_t a = k, b = 0, q = 0;
+      while (a < n && b < k) out[q++] = key_less(&nk[b], &keys[a]) ? nk[b++] : keys[a++];
+      while (a < n) out[q++] = keys[a++];
+      while (b < k) out[q++] = nk[b++];
+      memcpy(keys, out, sizeof(nkey_t) * (size_t)n);
+      free(out);
+    }
+    mrep += k; ++gen;
+    /* remaining_integral_negligable (nested.ml:45-48) on the replaced live set */
+    double live_est = log_vol + keys[n - 1].ll;
+    if (live_est - or_log_sum_logs(est, live_est) <= log(o->epsrel)) break;
+    if (ndead >= max_iter) break;
+  }
+  int64_t ntot = ndead + n;
+  if (status == 0 && ntot > cap) status = -1;
+  if (status == 0) {
+    for (int64_t j = 0; j < n; ++j) {
+      int32_t sl = keys[j].slot;
+      memcpy(pts + (ndead + j) * D, lx + (int64_t)sl * D, sizeof(double) * (size_t)D);
+      lls[ndead + j] = lll[sl]; lps[ndead + j] = llp[sl];
+    }
+    or_evidence_weights(ntot, n, k, lls, &res->log_ev, &res->log_dev, log_wts);
+  }
+  res->n_dead = ndead; res->n_total = ntot; res->n_gen = gen; res->status = status;
+  free(lx); free(lll); free(llp); free(keys); free(nk); free(nx); free(nll); free(nlp);
+  free(tv); free(prefix);
+  prep_free(&p);
+  return status;
+}
+
+/* nested.ml:81-120.  Dead point i was retired with n_i = nlive - (i mod k) live points; its
+   remaining volume is logX_i = (i div k) * L_k + prefix[i mod k].  With k = 1 this is exactly
+   log_vol_fraction + i * log_reduction_frac of nested.ml:96. */
+void or_evidence_weights(int64_t n, int64_t nlive, int64_t k, const double* ll,
+                         double* log_ev, double* log_dev, double* wts) {
+  const double log_half = -0.69314718055994530942;
+  int64_t ilive = n - nlive;
+  double* prefix = (double*)malloc(sizeof(double) * (size_t)(k + 1));
+  prefix[0] = 0.0;
+  for (int64_t j = 0; j < k; ++j) prefix[j + 1] = prefix[j] + log1p(-1.0 / (double)(nlive - j));
+  for (int64_t i = 0; i < n; ++i) wts[i] = -INFINITY;
+  double low = -INFINITY, high = -INFINITY;
+  double last_dv = 0.0;
+  for (int64_t i = 0; i < ilive; ++i) {
+    int64_t j = i % k, g = i / k;
+    double logx = (double)g * prefix[k] + prefix[j];
+    double log_dv = log(1.0 / (double)(nlive - j)) + logx;
+    if (k == 1) log_dv = log(1.0 / (double)nlive) + (double)i * log1p(-1.0 / (double)nlive);
+    double dlow = log_dv + ll[i], dhigh = log_dv + ll[i + 1];
+    low = or_log_sum_logs(low, dlow);
+    high = or_log_sum_logs(high, dhigh);
+    wts[i] = or_log_sum_logs(wts[i], log_half + dlow);
+    wts[i + 1] = or_log_sum_logs(wts[i + 1], log_half + dhigh);
+    last_dv = log_dv;
+  }
+  double log_dv;
+  if (k == 1) log_dv = log(1.0 / (double)nlive) + (double)(ilive - 1) * log1p(-1.0 / (double)nlive);
+  else {
+    /* remaining volume X_final shared by the nlive final points */
+    int64_t g = ilive / k, j = ilive % k;
+    log_dv = ((double)g * prefix[k] + prefix[j]) + log(1.0 / (double)nlive);
+    (void)last_dv;
+  }
+  for (int64_t i = ilive; i < n; ++i) {
+    double dlow = log_dv + ll[i - 1], dhigh = log_dv + ll[i];
+    low = or_log_sum_logs(low, dlow);
+    high = or_log_sum_logs(high, dhigh);
+    wts[i - 1] = or_log_sum_logs(wts[i - 1], log_half + dlow);
+    wts[i] = or_log_sum_logs(wts[i], log_half + dhigh);
+  }
+  *log_ev = log_half + or_log_sum_logs(low, high);
+  *log_dev = high + log1p(-exp(low - high));
+  for (int64_t i = 0; i < n; ++i) wts[i] = wts[i] - *log_ev;
+  free(prefix);
+}
+
+double or_log_total_error_estimate(double log_ev, double log_dev, int64_t nlive) {
+  double lre2 = -log((double)nlive);                                     /* nested.ml:148-150 */
+  return 0.5 * or_log_sum_logs(2.0 * log_dev, lre2 + 2.0 * log_ev);
+}
+
+int64_t or_weight_binary_search_index(double x, const double* sums, int64_t n) { /* :152-165 */
+  if (x <= sums[0]) return 0;
+  int64_t lo = 0, hi = n - 1;
+  while (hi - lo > 1) {
+    int64_t mid = (lo + hi) / 2;
+    if (x <= sums[mid]) hi = mid; else lo = mid;
+  }
+  return hi;
+}
+
+/* ======================================================================================
+ * kD tree build (kd_tree.ml:155-175) -- geometry is deterministic: the i-th order statistic
+ * found by the randomized find_ith (kd_tree.ml:69-86) is unique, so a sort replaces it.
+ * ====================================================================================== */
+typedef struct { const double* pts; int D; int dim; } sortctx_t;
+static __thread sortctx_t g_sc;
+static int cmp_idx_dim(const void* a, const void* b) {
+  double x = g_sc.pts[(int64_t)(*(const int64_t*)a) * g_sc.D + g_sc.dim];
+  double y = g_sc.pts[(int64_t)(*(const int64_t*)b) * g_sc.D + g_sc.dim];
+  return (x < y) ? -1 : (x > y) ? 1 : 0;
+}
+
+static int32_t kd_new_node(or_kd* t) {
+  if (t->nn == t->cap_n) {
+    t->cap_n = t->cap_n ? 2 * t->cap_n : 64;
+    t->dim = (int32_t*)realloc(t->dim, sizeof(int32_t) * (size_t)t->cap_n);
+    t->split = (double*)realloc(t->split, sizeof(double) * (size_t)t->cap_n);
+    t->right = (int32_t*)realloc(t->right, sizeof(int32_t) * (size_t)t->cap_n);
+    t->leaf = (int32_t*)realloc(t->leaf, sizeof(int32_t) * (size_t)t->cap_n);
+  }
+  return (int32_t)t->nn++;
+}
+
+static int32_t kd_new_leaf(or_kd* t, int32_t count, const double* lo, const double* hi) {
+  if (t->nl == t->cap_l) {
+    t->cap_l = t->cap_l ? 2 * t->cap_l : 64;
+    t->lcount = (int32_t*)realloc(t->lcount, sizeof(int32_t) * (size_t)t->cap_l);
+    t->lbox = (double*)realloc(t->lbox, sizeof(double) * (size_t)t->cap_l * 2 * (size_t)t->D);
+    t->llogq = (double*)realloc(t->llogq, sizeof(double) * (size_t)t->cap_l);
+  }
+  int32_t L = (int32_t)t->nl++;
+  t->lcount[L] = count;
+  memcpy(t->lbox + (int64_t)L * 2 * t->D, lo, sizeof(double) * (size_t)t->D);
+  memcpy(t->lbox + (int64_t)L * 2 * t->D + t->D, hi, sizeof(double) * (size_t)t->D);
+  /* jump_prob = nobjs / (v * n) (interpolate_pdf.ml:135-142), v = bounds_volume (kd_tree.ml:177-182) */
+  double v = 1.0;
+  for (int d = 0; d < t->D; ++d) v = v * (hi[d] - lo[d]);
+  v = v + 0.0;
+  t->llogq[L] = log((double)count / (v * (double)t->M));
+  return L;
+}
+
+/* build over idx[0..n) with cell box lo/hi; preorder layout: left child = node + 1 */
+static int32_t kd_build_rec(or_kd* t, const double* pts, int64_t* idx, int64_t n,
+                            const double* lo, const double* hi) {
+  int D = t->D;
+  int32_t node = kd_new_node(t);
+  int all_eq = 1;
+  for (int64_t i = 1; i < n && all_eq; ++i)
+    for (int d = 0; d < D; ++d)
+      if (pts[idx[i] * D + d] != pts[idx[0] * D + d]) { all_eq = 0; break; }
+  if (n == 1 || all_eq) {                                  /* kd_tree.ml:158-160 */
+    t->dim[node] = -1; t->split[node] = 0.0; t->right[node] = -1;
+    t->leaf[node] = kd_new_leaf(t, (int32_t)n, lo, hi);
+    return node;
+  }
+  /* bounds_of_objects + longest_dim (kd_tree.ml:96-110, 120-130) */
+  double* bl = (double*)malloc(sizeof(double) * D);
+  double* bh = (double*)malloc(sizeof(double) * D);
+  for (int d = 0; d < D; ++d) bl[d] = bh[d] = pts[idx[0] * D + d];
+  for (int64_t i = 1; i < n; ++i)
+    for (int d = 0; d < D; ++d) {
+      double c = pts[idx[i] * D + d];
+      if (c < bl[d]) bl[d] = c;
+      if (c > bh[d]) bh[d] = c;
+    }
+  int dim = -1; double dxm = -INFINITY;
+  for (int d = 0; d < D; ++d) { double dx = bh[d] - bl[d]; if (dx > dxm) { dim = d; dxm = dx; } }
+  free(bl); free(bh);
+  /* pivot = (n/2)-th order statistic along dim; lte = coord <= pivot (kd_tree.ml:162-168) */
+  sortctx_t saved = g_sc;
+  g_sc.pts = pts; g_sc.D = D; g_sc.dim = dim;
+  qsort(idx, (size_t)n, sizeof(int64_t), cmp_idx_dim);
+  g_sc = saved;
+  double pv = pts[idx[n / 2] * D + dim];
+  int64_t nlte = 0;
+  while (nlte < n && pts[idx[nlte] * D + dim] <= pv) ++nlte;
+  if (nlte == n) {                                         /* adjust_for_empty_split :150-152 */
+    double mx = pts[idx[n - 1] * D + dim];
+    nlte = 0;
+    while (nlte < n && pts[idx[nlte] * D + dim] < mx) ++nlte;
+  }
+  double lt_bound = pts[idx[nlte - 1] * D + dim];          /* find_max comp lte */
+  double gt_bound = pts[idx[nlte] * D + dim];              /* find_min comp gt */
+  double x = 0.5 * (lt_bound + gt_bound);                  /* split_bounds :112-118 */
+  double* nhi = (double*)malloc(sizeof(double) * D);
+  double* nlo = (double*)malloc(sizeof(double) * D);
+  memcpy(nhi, hi, sizeof(double) * D); nhi[dim] = x;
+  memcpy(nlo, lo, sizeof(double) * D); nlo[dim] = x;
+  t->dim[node] = dim; t->split[node] = x; t->leaf[node] = -1;
+  kd_build_rec(t, pts, idx, nlte, lo, nhi);
+  int32_t r = kd_build_rec(t, pts, idx + nlte, n - nlte, nlo, hi);
+  t->right[node] = r;
+  free(nhi); free(nlo);
+  return node;
+}
+
+or_kd* or_kd_build(const double* pts, int64_t M, int D, const double* low, const double* high) {
+  if (M < 1 || D < 1) return NULL;
+  or_kd* t = (or_kd*)calloc(1, sizeof(or_kd));
+  t->D = D; t->M = M;
+  t->root_lo = (double*)malloc(sizeof(double) * D);
+  t->root_hi = (double*)malloc(sizeof(double) * D);
+  memcpy(t->root_lo, low, sizeof(double) * D);
+  memcpy(t->root_hi, high, sizeof(double) * D);
+  int64_t* idx = (int64_t*)malloc(sizeof(int64_t) * (size_t)M);
+  for (int64_t i = 0; i < M; ++i) idx[i] = i;
+  kd_build_rec(t, pts, idx, M, low, high);
+  free(idx);
+  t->pts = (double*)malloc(sizeof(double) * (size_t)(M * D));
+  memcpy(t->pts, pts, sizeof(double) * (size_t)(M * D));
+  return t;
+}
+
+void or_kd_free(or_kd* t) {
+  if (!t) return;
+  free(t->pts);
+  free(t->dim); free(t->split); free(t->right); free(t->leaf);
+  free(t->lcount); free(t->lbox); free(t->llogq); free(t->root_lo); free(t->root_hi);
+  free(t);
+}
+
+int64_t or_kd_nnodes(const or_kd* t) { return t->nn; }
+int64_t or_kd_nleaves(const or_kd* t) { return t->nl; }
+
+void or_kd_export(const or_kd* t, int32_t* node_dim, double* node_split, int32_t* node_right,
+                  int32_t* node_leaf, int32_t* leaf_count, double* leaf_box) {
+  memcpy(node_dim, t->dim, sizeof(int32_t) * (size_t)t->nn);
+  memcpy(node_split, t->split, sizeof(double) * (size_t)t->nn);
+  memcpy(node_right, t->right, sizeof(int32_t) * (size_t)t->nn);
+  memcpy(node_leaf, t->leaf, sizeof(int32_t) * (size_t)t->nn);
+  memcpy(leaf_count, t->lcount, sizeof(int32_t) * (size_t)t->nl);
+  memcpy(leaf_box, t->lbox, sizeof(double) * (size_t)t->nl * 2 * (size_t)t->D);
+}
+
+/* find_cell (interpolate_pdf.ml:101-109): go left iff pt lies in the left child's (inclusive)
+   box.  Boxes nest, so a point outside the root box always goes right; inside, the left test
+   reduces to pt[dim] <= split. */
+static int64_t kd_find_leaf_idx(const or_kd* t, const double* pt) {
+  int inside = 1;
+  for (int d = 0; d < t->D; ++d) inside &= (pt[d] >= t->root_lo[d]) & (pt[d] <= t->root_hi[d]);
+  int32_t node = 0;
+  while (t->dim[node] >= 0) {
+    int left = inside && (pt[t->dim[node]] <= t->split[node]);
+    node = left ? node + 1 : t->right[node];
+  }
+  return t->leaf[node];
+}
+
+int64_t or_kd_find_leaf(const or_kd* t, const double* pt) { return kd_find_leaf_idx(t, pt); }
+double or_kd_log_jump_prob(const or_kd* t, const double* pt) { return t->llogq[kd_find_leaf_idx(t, pt)]; }
+double or_kd_jump_prob(const or_kd* t, const double* pt) {
+  int64_t L = kd_find_leaf_idx(t, pt);
+  const double* lo = t->lbox + L * 2 * t->D;
+  const double* hi = lo + t->D;
+  double v = 1.0;
+  for (int d = 0; d < t->D; ++d) v = v * (hi[d] - lo[d]);
+  v = v + 0.0;
+  return (double)t->lcount[L] / (v * (double)t->M);
+}

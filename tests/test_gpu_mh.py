@@ -1,0 +1,235 @@
+"""GPU parity tests of the batched MH kernel against the CPU oracle (bit-exact), through the
+C-ABI (mcmc_amd -> libmcg.so).  Every comparison is exact: accept bitmap, records, final
+state, counters and tile statistics must be bit-identical to oracle/oracle.c on the same seed."""
+import math
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+LIK_FLAT, LIK_DIAG, LIK_FULLCOV, LIK_SHELL, LIK_GDATA, LIK_CDATA = range(6)
+
+
+@pytest.fixture(scope="module")
+def T():
+    from mcmc_amd import targets
+    return targets
+
+
+def run_gpu(lik, prior, prop, x0, seed, nbin, nskip, n_rec, lanes=0, chain_offset=0, spl=0,
+            accumulate=True):
+    from mcmc_amd import Context
+    ctx = Context(seed=seed, lanes_per_chain=lanes, chain_offset=chain_offset, steps_per_launch=spl)
+    ctx.set_model(lik, prior, prop)
+    ctx.init(x0)
+    x_init, ll_init, lp_init = ctx.state()
+    ctx.run(nbin=nbin, nskip=nskip, n_rec=n_rec, record_x=True, record_llp=True,
+            record_accept=True, accumulate=accumulate)
+    rx, rll, rlp, bits = ctx.records(x=True, llp=True, accept=True)
+    x, ll, lp = ctx.state()
+    acc, rej = ctx.counters()
+    tiles = ctx.tile_stats() if accumulate else None
+    out = dict(rec_x=rx, rec_ll=rll, rec_lp=rlp, bits=bits, x=x, ll=ll, lp=lp, nacc=acc,
+               nrej=rej, tiles=tiles, ll0=ll_init, lp0=lp_init, lanes=None)
+    ctx.close()
+    return out
+
+
+def run_oracle(O, lik, prior, prop, x0, seed, nbin, nskip, n_rec, chain_offset=0, kd=None):
+    D = lik.ndim
+    m = O.Model(D, lik.kind, lik.params, prior.kind, prior.params,
+                prop.kind if kd is None else 3, prop.params if kd is None else [0.0], kd)
+    N = x0.shape[1]
+    ll0 = np.array([m.loglik(x0[:, i]) for i in range(N)])
+    lp0 = np.array([m.logprior(x0[:, i]) for i in range(N)])
+    r = O.mh_run(m, seed, x0, ll0, lp0, nbin=nbin, nskip=nskip, n_rec=n_rec, chain_offset=chain_offset,
+                 nthreads=8)
+    r["ll0"], r["lp0"] = ll0, lp0
+    r["tiles"] = O.tile_stats(D, N, n_rec, r)
+    return r
+
+
+def assert_same(g, o):
+    np.testing.assert_array_equal(g["ll0"], o["ll0"])
+    np.testing.assert_array_equal(g["lp0"], o["lp0"])
+    np.testing.assert_array_equal(g["bits"], o["bits"])
+    np.testing.assert_array_equal(g["rec_x"], o["rec_x"])
+    np.testing.assert_array_equal(g["rec_ll"], o["rec_ll"])
+    np.testing.assert_array_equal(g["rec_lp"], o["rec_lp"])
+    np.testing.assert_array_equal(g["x"], o["x"])
+    np.testing.assert_array_equal(g["ll"], o["ll"])
+    assert g["nacc"] == int(o["nacc"].sum())
+    if g["tiles"] is not None:
+        np.testing.assert_array_equal(g["tiles"], o["tiles"])
+
+
+def c2_model(T, D=32, seed=42):
+    rng = np.random.default_rng(seed)
+    mu = rng.uniform(-1, 1, D)
+    sg = rng.uniform(0.5, 2, D)
+    s = 2.38 / math.sqrt(D) * float(np.median(sg))
+    return T.diag_gauss(mu, sg), T.box(-10 * np.ones(D), 10 * np.ones(D)), T.gauss(s), mu, sg
+
+
+@pytest.mark.parametrize("lanes", [1, 2, 4, 8])
+def test_c2_mini_bit_exact(oracle, T, lanes):
+    """C2-mini: D=32 diagonal Gaussian, box prior, isotropic proposal, 192 chains, 300 steps."""
+    lik, pri, prop, mu, sg = c2_model(T)
+    N = 192
+    x0 = np.random.default_rng(1).normal(mu[:, None], sg[:, None], size=(32, N))
+    g = run_gpu(lik, pri, prop, x0, 1, nbin=20, nskip=1, n_rec=280, lanes=lanes)
+    o = run_oracle(oracle, lik, pri, prop, x0, 1, 20, 1, 280)
+    assert_same(g, o)
+
+
+def test_multi_launch_and_thinning_equivalence(oracle, T):
+    """Slicing the run into launches of 7 steps, with nbin/nskip thinning, changes nothing."""
+    lik, pri, prop, mu, sg = c2_model(T, D=16)
+    x0 = np.random.default_rng(2).normal(mu[:, None], sg[:, None], size=(16, 100))
+    g = run_gpu(lik, pri, prop, x0, 3, nbin=13, nskip=5, n_rec=40, spl=7)
+    o = run_oracle(oracle, lik, pri, prop, x0, 3, 13, 5, 40)
+    assert_same(g, o)
+
+
+@pytest.mark.parametrize("lanes", [1, 4])
+def test_gauss_shell_bit_exact(oracle, T, lanes):
+    D = 16
+    lik = T.gauss_shell(np.zeros(D), 2.0, 0.1)
+    pri = T.box(-6 * np.ones(D), 6 * np.ones(D))
+    x0 = np.random.default_rng(4).normal(size=(D, 80))
+    x0 = 2.0 * x0 / np.linalg.norm(x0, axis=0)
+    g = run_gpu(lik, pri, T.gauss(0.03), x0, 5, nbin=0, nskip=2, n_rec=60, lanes=lanes)
+    o = run_oracle(oracle, lik, pri, T.gauss(0.03), x0, 5, 0, 2, 60)
+    assert_same(g, o)
+
+
+@pytest.mark.parametrize("D", [1, 3, 5, 8])
+def test_fullcov_bit_exact(oracle, T, D):
+    rng = np.random.default_rng(D)
+    A = rng.normal(size=(D, D))
+    cov = A @ A.T + D * np.eye(D)
+    mu = rng.normal(size=D)
+    lik = T.fullcov_gauss(mu, cov)
+    x0 = rng.normal(mu[:, None], 1.0, size=(D, 70))
+    g = run_gpu(lik, T.flat_prior(), T.gauss(0.5), x0, 6, nbin=5, nskip=1, n_rec=50)
+    o = run_oracle(oracle, lik, T.flat_prior(), T.gauss(0.5), x0, 6, 5, 1, 50)
+    assert_same(g, o)
+
+
+@pytest.mark.parametrize("cauchy", [False, True])
+def test_gaussian_cauchy_c1_bit_exact(oracle, T, cauchy):
+    """C1: bin/gaussian_cauchy.ml data likelihoods, wrapping-uniform proposal
+    (dx = sigma / (sqrt nsamp * ndim), :118-129), box prior (:133-147)."""
+    rng = np.random.default_rng(9)
+    nd, nsamp = 1, 10
+    mus = rng.uniform(-1, 1, nd); sigmas = rng.uniform(0.1, 0.2, nd)
+    data = rng.normal(mus, sigmas, size=(nsamp, nd))
+    lik = T.cauchy_data(data) if cauchy else T.gauss_data(data)
+    lo = np.concatenate([[-1.0] * nd, [0.1] * nd]); hi = np.concatenate([[1.0] * nd, [0.2] * nd])
+    lp_in = -nd * (math.log(2.0) + math.log(0.1))
+    pri = T.box(lo, hi, lp_in)
+    dx = np.concatenate([sigmas, sigmas]) / (math.sqrt(nsamp) * nd)
+    prop = T.uniform_wrapping(lo, hi, dx)
+    x0 = np.tile(np.concatenate([mus, sigmas])[:, None], (1, 64))
+    g = run_gpu(lik, pri, prop, x0, 7, nbin=0, nskip=1, n_rec=500)
+    o = run_oracle(oracle, lik, pri, prop, x0, 7, 0, 1, 500)
+    assert_same(g, o)
+
+
+def test_kd_interp_proposal_bit_exact(oracle, T):
+    """C4-mini: Interpolate_pdf kD-tree independence proposal, D=3, 256 training points."""
+    rng = np.random.default_rng(10)
+    D = 3
+    mu = np.zeros(D); sg = np.ones(D)
+    pts = rng.normal(size=(256, D))
+    lo, hi = -5 * np.ones(D), 5 * np.ones(D)
+    kdp = T.KdInterp(pts, lo, hi)
+    okd = oracle.KdTree(pts, lo, hi)
+    lik = T.diag_gauss(mu, sg)
+    pri = T.box(lo, hi)
+    x0 = rng.normal(size=(D, 96))
+    g = run_gpu(lik, pri, kdp, x0, 8, nbin=4, nskip=1, n_rec=64)
+    o = run_oracle(oracle, lik, pri, T.gauss(1.0), x0, 8, 4, 1, 64, kd=okd)
+    assert_same(g, o)
+
+
+def test_kd_tree_export_matches_oracle(oracle, T):
+    import ctypes as C
+    import mcmc_amd._lib as L
+    from mcmc_amd import Context
+    rng = np.random.default_rng(11)
+    pts = rng.normal(size=(300, 4))
+    pts[:40] = pts[0]                      # duplicates -> multi-point leaf (kd_tree.ml:159-160)
+    lo, hi = -6 * np.ones(4), 6 * np.ones(4)
+    ctx = Context(seed=0)
+    ctx.set_model(T.diag_gauss(np.zeros(4), np.ones(4)), T.box(lo, hi), T.KdInterp(pts, lo, hi))
+    nn, nl = C.c_int64(), C.c_int64()
+    L.check(L.lib().mcg_kd_info(ctx.ptr, C.byref(nn), C.byref(nl)))
+    g = dict(dim=np.zeros(nn.value, np.int32), split=np.zeros(nn.value), right=np.zeros(nn.value, np.int32),
+             leaf=np.zeros(nn.value, np.int32), count=np.zeros(nl.value, np.int32),
+             box=np.zeros((nl.value, 2, 4)), logq=np.zeros(nl.value))
+    L.check(L.lib().mcg_kd_export(ctx.ptr, L.i32ptr(g["dim"]), L.dptr(g["split"]), L.i32ptr(g["right"]),
+                                  L.i32ptr(g["leaf"]), L.i32ptr(g["count"]), L.dptr(g["box"]),
+                                  L.dptr(g["logq"])))
+    e = oracle.KdTree(pts, lo, hi).export()
+    for k in ("dim", "split", "right", "leaf", "count", "box"):
+        np.testing.assert_array_equal(g[k], e[k], err_msg=k)
+
+
+def test_sharded_chains_equal_single_context(oracle, T):
+    """GPU-count invariance: two contexts holding chains [0,256) and [256,512) (chain_offset)
+    reproduce one context holding all 512, and their tiles combine to identical statistics."""
+    from mcmc_amd.context import combine_tiles
+    lik, pri, prop, mu, sg = c2_model(T)
+    x0 = np.random.default_rng(12).normal(mu[:, None], sg[:, None], size=(32, 512))
+    full = run_gpu(lik, pri, prop, x0, 13, nbin=10, nskip=1, n_rec=100)
+    a = run_gpu(lik, pri, prop, x0[:, :256], 13, nbin=10, nskip=1, n_rec=100, chain_offset=0)
+    b = run_gpu(lik, pri, prop, x0[:, 256:], 13, nbin=10, nskip=1, n_rec=100, chain_offset=256)
+    np.testing.assert_array_equal(full["x"], np.concatenate([a["x"], b["x"]], axis=1))
+    np.testing.assert_array_equal(full["tiles"], np.concatenate([a["tiles"], b["tiles"]]))
+    m1 = combine_tiles(32, full["tiles"])
+    m2 = combine_tiles(32, np.concatenate([a["tiles"], b["tiles"]]))
+    for u, v in zip(m1, m2):
+        np.testing.assert_array_equal(u, v)
+
+
+def test_append_runs_equal_one_run(oracle, T):
+    """mcg_run(append) continues records/statistics: nbin run + 3 appended chunks == one run."""
+    from mcmc_amd import Context
+    lik, pri, prop, mu, sg = c2_model(T, D=8)
+    x0 = np.random.default_rng(14).normal(mu[:, None], sg[:, None], size=(8, 300))
+    ctx = Context(seed=15)
+    ctx.set_model(lik, pri, prop)
+    ctx.init(x0)
+    ctx.run(nbin=10, nskip=1, n_rec=1, record_x=False, record_llp=False, accumulate=True)
+    for _ in range(3):
+        ctx.run(nbin=0, nskip=2, n_rec=5, record_x=False, record_llp=False, accumulate=True,
+                append=True)
+    tiles = ctx.tile_stats()
+    x, _, _ = ctx.state()
+    o = run_oracle(oracle, lik, pri, prop, x0, 15, 10, 2, 16)
+    np.testing.assert_array_equal(x, o["x"])
+    np.testing.assert_array_equal(tiles, o["tiles"])
+
+
+# ---------------------------------------------------------------- statistics at full size
+def test_c2_full_size_properties(T):
+    """C2 at its full size (65,536 chains, D=32): posterior moments from the on-device
+    accumulators match the target (size-independent properties), acceptance is sane."""
+    from mcmc_amd import Context
+    lik, pri, prop, mu, sg = c2_model(T)
+    N = 65536
+    x0 = np.random.default_rng(16).normal(mu[:, None], sg[:, None], size=(32, N))
+    ctx = Context(seed=1)
+    ctx.set_model(lik, pri, prop)
+    ctx.init(x0)
+    ctx.run(nbin=100, nskip=1, n_rec=200, record_x=False, record_llp=False, record_accept=True,
+            accumulate=True)
+    mean, sd, log_z = ctx.stats()
+    acc, rej = ctx.counters()
+    frac = acc / (acc + rej)
+    assert 0.15 < frac < 0.45
+    np.testing.assert_allclose(mean, mu, atol=0.02)
+    np.testing.assert_allclose(sd, sg, rtol=0.02)
+    assert np.isfinite(log_z)

