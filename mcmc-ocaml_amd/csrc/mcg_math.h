@@ -166,6 +166,24 @@ __device__ __forceinline__ void normal_pair(uint32_t a, uint32_t b, double& z0, 
   z1 = rho * sn;
 }
 
+// log1p(r), r in [0,1] (Goldberg: r * log(1+r) / ((1+r)-1)); log-sum-exp on the portable
+// exp/log.  Drives the running nested-sampling estimate (nested.ml:139-142).
+__device__ __forceinline__ double plog1p(double r) {
+  double u = 1.0 + r;
+  if (u == 1.0) return r;
+  return plog(u) * (r / (u - 1.0));
+}
+
+__device__ __forceinline__ double plse(double a, double b) {
+  if (a == -__builtin_inf() && b == -__builtin_inf()) return -__builtin_inf();
+  if (b > a) {
+    double t = a;
+    a = b;
+    b = t;
+  }
+  return a + plog1p(pexp(b - a));
+}
+
 // canonical 8-accumulator reduction tree (DESIGN.md §Canonical sums)
 __device__ __forceinline__ double canon8(const double* A) {
   return ((A[0] + A[4]) + (A[2] + A[6])) + ((A[1] + A[5]) + (A[3] + A[7]));

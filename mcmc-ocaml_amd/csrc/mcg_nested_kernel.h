@@ -1,0 +1,175 @@
+// mcg_nested_kernel.h -- kernels of the batched nested sampler (Nested.nested_evidence,
+// nested.ml:122-146) generalised to k retirements per generation.
+//
+// Device data:
+//   live set     x[slot][D] (AoS rows: the DE proposal gathers two random rows per step),
+//                ll[slot], lp[slot]
+//   order        keys (ll, tie, slot) sorted ascending -- the k lowest are keys[0..k); the
+//                reference's insertion-sorted array (nested.ml:26-43) becomes a merge of the
+//                k sorted new keys into the n-k survivors each generation
+//   dead points  dead_x[m][D], dead_ll[m], dead_lp[m] in retirement order
+//   scalars      NestDevState (running log volume, estimate, stop / error flags)
+#pragma once
+#include "mcg_device.h"
+#include "mcg_math.h"
+#include "mcg_mh_kernel.h"
+#include "mcg.h"
+
+namespace mcg {
+
+struct NestDevState {
+  double log_vol;
+  double est;
+  int32_t stopped;
+  int32_t error;
+  long long gen_done;
+};
+
+struct NestArgs {
+  MhArgs m;                 // likelihood / prior constants (m.lik, m.pri, m.prior_kind, ...)
+  double* x;                // live rows [n][D]
+  double* ll;
+  double* lp;
+  const double* key_ll;     // current sorted keys
+  const long long* key_tie;
+  const int* key_slot;
+  double* nx;               // new points [k][D]
+  double* nll;
+  double* nlp;
+  double* dead_x;
+  double* dead_ll;
+  double* dead_lp;
+  double* newk_ll;          // unsorted keys of the new points
+  long long* newk_tie;
+  int* newk_slot;
+  double* tv;               // ll + log dv of this generation's dead points (padded pow2)
+  const double* prefix;     // [k+1] sum_{j'<j} log1p(-1/(n-j'))
+  const double* qadd;       // [k] 1/(n-j) (nested.ml:140 quirk) or log(1/(n-j))
+  NestDevState* st;
+  int64_t n, k, nmcmc, mrep, tv_len;
+  double mode_hop, sigma_de, log_epsrel;
+  uint32_t k0, k1;
+  uint64_t seed_unused;
+};
+
+// ---- one constrained DE-MCMC walker per lane (draw_new_live_point, nested.ml:50-74) ----
+template <int D, int LIK>
+__global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
+  if (a.st->stopped) return;
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= a.k) return;
+  const Rng rng{a.k0, a.k1};
+  const uint32_t wid = (uint32_t)(a.mrep + w);
+  const double thr = a.key_ll[a.k - 1];
+  const uint32_t n = (uint32_t)a.n;
+  // start: a uniformly random live point satisfying the constraint (nested.ml:63); with k = 1
+  // every live point does, so this is Random.int nlive
+  int64_t start = -1;
+  for (uint32_t att = 0; att < 4096; ++att) {
+    const u32x4 r = rng(wid, att, CALL_START, TAG_NEST_WALK, 0u);
+    const uint32_t s = randint(r.x, r.y, n);
+    if (a.ll[s] >= thr) {
+      start = s;
+      break;
+    }
+  }
+  if (start < 0) start = a.key_slot[a.k - 1];
+  double cur[D], y[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) cur[d] = a.x[start * D + d];
+  double cur_l = (a.ll[start] >= thr) ? a.lp[start] : -__builtin_inf();   // mcmc_logl, :54-59
+  for (int64_t s = 0; s < a.nmcmc; ++s) {
+    // differential_evolution_proposal (mcmc.ml:198-218)
+    const u32x4 ri = rng(wid, (uint32_t)s, CALL_DE_IDX, TAG_NEST_WALK, 0u);
+    const uint32_t i = randint(ri.x, ri.y, n);
+    const uint32_t jj = randint(ri.z, ri.w, n - 1);
+    const uint32_t j = jj + (jj >= i ? 1u : 0u);
+    const u32x4 rs = rng(wid, (uint32_t)s, CALL_DE_SCALE, TAG_NEST_WALK, 0u);
+    double dsc;
+    if (a.mode_hop != 0.0 && u53(rs.x, rs.y) < a.mode_hop) {
+      dsc = 1.0;
+    } else {
+      double z0, z1;
+      normal_pair(rs.z, rs.w, z0, z1);
+      dsc = a.sigma_de * z0;
+    }
+    const double* __restrict__ xi = a.x + (int64_t)i * D;
+    const double* __restrict__ xj = a.x + (int64_t)j * D;
+#pragma unroll
+    for (int d = 0; d < D; ++d) y[d] = cur[d] + dsc * (xj[d] - xi[d]);
+    const double lly = eval_lik<D, 1, LIK>(y, 0, a.m, a.m.lik);
+    const double ml = (lly >= thr) ? eval_prior<D, 1>(y, 0, a.m, a.m.pri) : -__builtin_inf();
+    const double ratio = (((ml + 0.0) - (cur_l + 0.0)) + 0.0) - 0.0;   // mcmc.ml:47-48
+    const u32x4 ra = rng(wid, (uint32_t)s, CALL_ACCEPT, TAG_NEST_WALK, 0u);
+    if (plog(u53(ra.x, ra.y)) < ratio) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) cur[d] = y[d];
+      cur_l = ml;
+    }
+  }
+  const double nl = eval_lik<D, 1, LIK>(cur, 0, a.m, a.m.lik);
+  const double np = eval_prior<D, 1>(cur, 0, a.m, a.m.pri);
+#pragma unroll
+  for (int d = 0; d < D; ++d) a.nx[w * D + d] = cur[d];
+  a.nll[w] = nl;
+  a.nlp[w] = np;
+  if (!(nl >= thr)) a.st->error = 1;                 // nested.ml:70-72 -> Failure
+}
+
+// ---- prior draws of the initial live set (nested.ml:126-129, Stats.draw_uniform) ----
+template <int D, int LIK>
+__global__ void __launch_bounds__(256) nest_init_kernel(const NestArgs a, double* keys_ll,
+                                                         long long* keys_tie, int* keys_slot) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= a.n) return;
+  const Rng rng{a.k0, a.k1};
+  const double* __restrict__ lo = a.m.pri;
+  const double* __restrict__ hi = a.m.pri + D;
+  double x[D];
+#pragma unroll
+  for (int d = 0; d < D; d += 2) {
+    const u32x4 r = rng((uint32_t)s, 0u, (uint32_t)(d >> 1), TAG_NEST_PRIOR, 0u);
+    x[d] = lo[d] + (hi[d] - lo[d]) * u53(r.x, r.y);
+    if (d + 1 < D) x[d + 1] = lo[d + 1] + (hi[d + 1] - lo[d + 1]) * u53(r.z, r.w);
+  }
+#pragma unroll
+  for (int d = 0; d < D; ++d) a.x[s * D + d] = x[d];
+  const double l = eval_lik<D, 1, LIK>(x, 0, a.m, a.m.lik);
+  a.ll[s] = l;
+  a.lp[s] = eval_prior<D, 1>(x, 0, a.m, a.m.pri);
+  keys_ll[s] = l;
+  keys_tie[s] = s;
+  keys_slot[s] = (int)s;
+}
+
+template <int D, int LIK>
+hipError_t launch_nest_walk(const NestArgs& a, hipStream_t st) {
+  const int64_t grid = (a.k + 255) / 256;
+  hipLaunchKernelGGL((nest_walk_kernel<D, LIK>), dim3((unsigned)grid), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+template <int D, int LIK>
+hipError_t launch_nest_init(const NestArgs& a, double* kl, long long* kt, int* ks, hipStream_t st) {
+  const int64_t grid = (a.n + 255) / 256;
+  hipLaunchKernelGGL((nest_init_kernel<D, LIK>), dim3((unsigned)grid), dim3(256), 0, st, a, kl, kt, ks);
+  return hipGetLastError();
+}
+
+// generic kernels (mcg_nested_kernels.hip)
+hipError_t launch_sort_keys(double* ll, long long* tie, int* slot, double* tll, long long* ttie,
+                            int* tslot, int64_t n, bool* result_in_tmp, hipStream_t st,
+                            const NestDevState* stop);
+hipError_t launch_merge_new(const NestArgs& a, double* out_ll, long long* out_tie, int* out_slot,
+                            const double* new_ll, const long long* new_tie, const int* new_slot,
+                            hipStream_t st);
+hipError_t launch_retire(const NestArgs& a, int D, hipStream_t st);
+hipError_t launch_estimate(const NestArgs& a, hipStream_t st);
+hipError_t launch_stop(const NestArgs& a, const double* final_ll, hipStream_t st);
+
+typedef hipError_t (*nest_walk_fn)(const NestArgs&, hipStream_t);
+typedef hipError_t (*nest_init_fn)(const NestArgs&, double*, long long*, int*, hipStream_t);
+nest_walk_fn find_nest_walk(int D, int lik);
+nest_init_fn find_nest_init(int D, int lik);
+
+}  // namespace mcg

@@ -180,6 +180,21 @@ void or_normal_pair(uint32_t a, uint32_t b, double* z0, double* z1) {
   *z1 = rho * sn;
 }
 
+/* log1p(r) for r in [0,1] and log-sum-exp with the portable exp/log (device-reproducible):
+   log1p(r) = r * log(1+r) / ((1+r) - 1) (Goldberg); used for the running nested-sampling
+   estimate that drives the stopping rule (nested.ml:139-142). */
+double or_plog1p(double r) {
+  double u = 1.0 + r;
+  if (u == 1.0) return r;
+  return or_log(u) * (r / (u - 1.0));
+}
+
+double or_plse(double a, double b) {
+  if (a == -INFINITY && b == -INFINITY) return -INFINITY;
+  if (b > a) { double t = a; a = b; b = t; }
+  return a + or_plog1p(or_exp(b - a));
+}
+
 /* dims 4c..4c+3 of a step take Philox call c: pair (w0,w1) -> z[4c], z[4c+1]; (w2,w3) -> +2,+3 */
 static void normals_tagged(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t tag, uint32_t hi16,
                            int D, double* z) {
@@ -713,7 +728,7 @@ static double tree_lse(double* v, int64_t n) {
   while (p2 < n) p2 <<= 1;
   for (int64_t i = n; i < p2; ++i) v[i] = -INFINITY;
   for (int64_t s = p2 >> 1; s >= 1; s >>= 1)
-    for (int64_t i = 0; i < s; ++i) v[i] = or_log_sum_logs(v[i], v[i + s]);
+    for (int64_t i = 0; i < s; ++i) v[i] = or_plse(v[i], v[i + s]);
   return v[0];
 }
 
@@ -810,7 +825,7 @@ int or_nested(const or_model* m, uint64_t seed, const or_nested_opts* o, double*
       tv[j] = lll[sl] + log_dv;
     }
     if (status) break;
-    est = (k == 1) ? or_log_sum_logs(est, tv[0]) : or_log_sum_logs(est, tree_lse(tv, k));
+    est = (k == 1) ? or_plse(est, tv[0]) : or_plse(est, tree_lse(tv, k));
     log_vol = log_vol + prefix[k];
     /* replace the retired slots (slot semantics of nested.ml:26-43) */
     for (int64_t j = 0; j < k; ++j) {
@@ -833,7 +848,7 @@ int or_nested(const or_model* m, uint64_t seed, const or_nested_opts* o, double*
     mrep += k; ++gen;
     /* remaining_integral_negligable (nested.ml:45-48) on the replaced live set */
     double live_est = log_vol + keys[n - 1].ll;
-    if (live_est - or_log_sum_logs(est, live_est) <= log(o->epsrel)) break;
+    if (live_est - or_plse(est, live_est) <= log(o->epsrel)) break;
     if (ndead >= max_iter) break;
   }
   int64_t ntot = ndead + n;

@@ -32,6 +32,8 @@ double or_exp(double x);
 double or_sqrt(double x);
 void or_sincos_kernel(double t, double* s, double* c);
 void or_normal_pair(uint32_t a, uint32_t b, double* z0, double* z1);
+double or_plog1p(double r);
+double or_plse(double a, double b);
 /* normals for the MH proposal of chain c at step t: z[0..D) */
 void or_step_normals(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, int D, double* z);
 
