@@ -1,14 +1,299 @@
-// mcg_nested.cpp -- Nested.nested_evidence driver (placeholder, filled in next).
+// mcg_nested.cpp -- host driver of Nested.nested_evidence (nested.ml:122-146) on the GPU.
+//
+// One generation = walk (k constrained DE-MCMC walkers, one lane each) -> retire (k lowest to the
+// dead buffer, new points into their slots) -> estimate (running evidence + log volume) -> sort
+// the k new keys -> merge them into the n-k survivors -> stop test.  All of it is enqueued
+// asynchronously in batches of generations; the device-side stop flag turns the kernels of any
+// generation after the stopping one into no-ops, so the host only synchronises once per batch.
+// evidence_error_and_weights (nested.ml:81-120) runs once on the host over the final points.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <utility>
+#include <vector>
+
+#include "mcg_nested_kernel.h"
 #include "mcg_runtime.h"
+
 using namespace mcg;
+
+namespace {
+
+struct KeyBuf {
+  DevBuf ll, tie, slot;
+  hipError_t ensure(int64_t n) {
+    hipError_t e;
+    if ((e = ll.ensure(n * 8)) != hipSuccess) return e;
+    if ((e = tie.ensure(n * 8)) != hipSuccess) return e;
+    return slot.ensure(n * 4);
+  }
+  double* l() { return (double*)ll.p; }
+  long long* t() { return (long long*)tie.p; }
+  int* s() { return (int*)slot.p; }
+};
+
+struct NestedBufs {
+  DevBuf x, ll, lp, nx, nll, nlp, tv, prefix, qadd, st, dead_x, dead_ll, dead_lp;
+  KeyBuf keys[2], newk, newk_tmp;
+  int64_t dead_cap = 0;
+};
+
+double lse_host(double a, double b) {            // Stats.log_sum_logs (stats.ml:240-248)
+  if (a == -HUGE_VAL && b == -HUGE_VAL) return -HUGE_VAL;
+  if (b > a) std::swap(a, b);
+  return a + std::log1p(std::exp(b - a));
+}
+
+// nested.ml:81-120; dead point i was retired with n - (i mod k) live points
+void evidence_weights(int64_t n, int64_t nlive, int64_t k, const double* ll, double* log_ev,
+                      double* log_dev, double* wts) {
+  const double log_half = -0.69314718055994530942;
+  const int64_t ilive = n - nlive;
+  std::vector<double> prefix((size_t)k + 1, 0.0);
+  for (int64_t j = 0; j < k; ++j) prefix[j + 1] = prefix[j] + std::log1p(-1.0 / (double)(nlive - j));
+  for (int64_t i = 0; i < n; ++i) wts[i] = -HUGE_VAL;
+  double low = -HUGE_VAL, high = -HUGE_VAL;
+  for (int64_t i = 0; i < ilive; ++i) {
+    const int64_t j = i % k, g = i / k;
+    double log_dv = std::log(1.0 / (double)(nlive - j)) + ((double)g * prefix[k] + prefix[j]);
+    if (k == 1) log_dv = std::log(1.0 / (double)nlive) + (double)i * std::log1p(-1.0 / (double)nlive);
+    const double dl = log_dv + ll[i], dh = log_dv + ll[i + 1];
+    low = lse_host(low, dl);
+    high = lse_host(high, dh);
+    wts[i] = lse_host(wts[i], log_half + dl);
+    wts[i + 1] = lse_host(wts[i + 1], log_half + dh);
+  }
+  double log_dv;
+  if (k == 1) {
+    log_dv = std::log(1.0 / (double)nlive) + (double)(ilive - 1) * std::log1p(-1.0 / (double)nlive);
+  } else {
+    const int64_t g = ilive / k, j = ilive % k;
+    log_dv = ((double)g * prefix[k] + prefix[j]) + std::log(1.0 / (double)nlive);
+  }
+  for (int64_t i = ilive; i < n; ++i) {
+    const double dl = log_dv + ll[i - 1], dh = log_dv + ll[i];
+    low = lse_host(low, dl);
+    high = lse_host(high, dh);
+    wts[i - 1] = lse_host(wts[i - 1], log_half + dl);
+    wts[i] = lse_host(wts[i], log_half + dh);
+  }
+  *log_ev = log_half + lse_host(low, high);
+  *log_dev = high + std::log1p(-std::exp(low - high));
+  for (int64_t i = 0; i < n; ++i) wts[i] = wts[i] - *log_ev;
+}
+
+}  // namespace
+
+struct mcg_nested_bufs_holder {
+  NestedBufs b;
+};
+
 extern "C" {
+
 int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res,
                mcg_observer_fn observer, void* user) {
-  (void)opts; (void)res; (void)observer; (void)user;
-  return set_error(ctx, MCG_EINVAL, "nested sampling not built yet");
+  if (!ctx || !opts) return MCG_EINVAL;
+  const int D = ctx->D;
+  if (D < 1) return set_error(ctx, MCG_ESTATE, "set the likelihood first");
+  if (ctx->prior_kind != MCG_PRIOR_BOX && ctx->prior_kind != MCG_PRIOR_OPEN_BOX)
+    return set_error(ctx, MCG_EINVAL, "nested sampling needs a box prior (draw_prior = uniform in the box)");
+  const int64_t n = opts->nlive > 0 ? opts->nlive : 1000;
+  const int64_t k = opts->k > 0 ? opts->k : 1;
+  const int64_t nmcmc = opts->nmcmc >= 0 ? opts->nmcmc : 1000;
+  const double epsrel = opts->epsrel > 0 ? opts->epsrel : 0.01;
+  if (n < 2 || k >= n || n > 0x7FFFFFFF) return set_error(ctx, MCG_EINVAL, "need 2 <= nlive, 1 <= k < nlive");
+  const int64_t max_dead = opts->max_dead > 0 ? opts->max_dead : 1000 * n;
+  nest_walk_fn walk = find_nest_walk(D, ctx->lik_kind);
+  nest_init_fn init = find_nest_init(D, ctx->lik_kind);
+  if (!walk || !init) return set_error(ctx, MCG_EINVAL, "no compiled nested kernel for D=%d likelihood=%d", D, ctx->lik_kind);
+  (void)hipSetDevice(ctx->opts.device);
+  if (!ctx->nested_bufs) ctx->nested_bufs = new mcg_nested_bufs_holder();
+  NestedBufs& B = ctx->nested_bufs->b;
+  hipStream_t s = ctx->stream;
+  int rc;
+#define HC(expr, what) \
+  if ((rc = hip_check(ctx, (expr), what))) return rc;
+  int64_t p2 = 1;
+  while (p2 < k) p2 <<= 1;
+  HC(B.x.ensure(n * D * 8), "alloc live");
+  HC(B.ll.ensure(n * 8), "alloc live");
+  HC(B.lp.ensure(n * 8), "alloc live");
+  HC(B.keys[0].ensure(n), "alloc keys");
+  HC(B.keys[1].ensure(n), "alloc keys");
+  HC(B.nx.ensure(k * D * 8), "alloc new");
+  HC(B.nll.ensure(k * 8), "alloc new");
+  HC(B.nlp.ensure(k * 8), "alloc new");
+  HC(B.newk.ensure(k), "alloc new keys");
+  HC(B.newk_tmp.ensure(k), "alloc new keys");
+  HC(B.tv.ensure(p2 * 8), "alloc tv");
+  HC(B.prefix.ensure((k + 1) * 8), "alloc prefix");
+  HC(B.qadd.ensure(k * 8), "alloc qadd");
+  HC(B.st.ensure(sizeof(NestDevState)), "alloc state");
+  // host constants: volume prefix sums and the per-retirement log dv term of nested.ml:140
+  const bool quirk = (ctx->opts.flags & MCG_FLAG_NESTED_FIXED_STOP) == 0;
+  std::vector<double> prefix((size_t)k + 1, 0.0), qadd((size_t)k);
+  for (int64_t j = 0; j < k; ++j) {
+    prefix[j + 1] = prefix[j] + std::log1p(-1.0 / (double)(n - j));
+    qadd[j] = quirk ? 1.0 / (double)(n - j) : std::log(1.0 / (double)(n - j));
+  }
+  HC(hipMemcpyAsync(B.prefix.p, prefix.data(), (k + 1) * 8, hipMemcpyHostToDevice, s), "copy prefix");
+  HC(hipMemcpyAsync(B.qadd.p, qadd.data(), k * 8, hipMemcpyHostToDevice, s), "copy qadd");
+  NestDevState st0{0.0, -HUGE_VAL, 0, 0, 0};
+  HC(hipMemcpyAsync(B.st.p, &st0, sizeof st0, hipMemcpyHostToDevice, s), "copy state");
+
+  NestArgs a{};
+  a.m = base_args(ctx);
+  a.x = (double*)B.x.p;
+  a.ll = (double*)B.ll.p;
+  a.lp = (double*)B.lp.p;
+  a.nx = (double*)B.nx.p;
+  a.nll = (double*)B.nll.p;
+  a.nlp = (double*)B.nlp.p;
+  a.newk_ll = B.newk.l();
+  a.newk_tie = B.newk.t();
+  a.newk_slot = B.newk.s();
+  a.tv = (double*)B.tv.p;
+  a.prefix = (const double*)B.prefix.p;
+  a.qadd = (const double*)B.qadd.p;
+  a.st = (NestDevState*)B.st.p;
+  a.n = n;
+  a.k = k;
+  a.nmcmc = nmcmc;
+  a.tv_len = p2;
+  a.mode_hop = opts->mode_hop;
+  a.sigma_de = 2.38 / std::sqrt(2.0 * (double)D);     // mcmc.ml:212
+  a.log_epsrel = std::log(epsrel);
+  a.k0 = (uint32_t)ctx->opts.seed;
+  a.k1 = (uint32_t)(ctx->opts.seed >> 32);
+
+  // initial live set: prior draws, evaluated, stably sorted by likelihood (nested.ml:126-132)
+  HC(init(a, B.keys[0].l(), B.keys[0].t(), B.keys[0].s(), s), "nested init");
+  bool in_tmp = false;
+  HC(launch_sort_keys(B.keys[0].l(), B.keys[0].t(), B.keys[0].s(), B.keys[1].l(), B.keys[1].t(),
+                      B.keys[1].s(), n, &in_tmp, s, nullptr), "sort live keys");
+  const int base = in_tmp ? 1 : 0;                   // generation g reads keys[(base + g) % 2]
+
+  int64_t gen = 0, reported = 0;
+  int64_t batch = 4;
+  NestDevState st{};
+  std::vector<double> hx, hll, hlp;
+  for (;;) {
+    const int64_t remaining = max_dead / k - gen;
+    if (remaining <= 0) break;
+    const int64_t G = std::min(batch, remaining);
+    const int64_t need = (gen + G) * k;
+    if (need > B.dead_cap) {
+      const int64_t cap = std::max<int64_t>(need, std::max<int64_t>(2 * B.dead_cap, 16 * n));
+      DevBuf nxb, nlb, npb;
+      HC(nxb.ensure(cap * D * 8), "alloc dead");
+      HC(nlb.ensure(cap * 8), "alloc dead");
+      HC(npb.ensure(cap * 8), "alloc dead");
+      const int64_t used = gen * k;
+      if (used > 0) {
+        HC(hipMemcpyAsync(nxb.p, B.dead_x.p, used * D * 8, hipMemcpyDeviceToDevice, s), "grow dead");
+        HC(hipMemcpyAsync(nlb.p, B.dead_ll.p, used * 8, hipMemcpyDeviceToDevice, s), "grow dead");
+        HC(hipMemcpyAsync(npb.p, B.dead_lp.p, used * 8, hipMemcpyDeviceToDevice, s), "grow dead");
+      }
+      HC(hipStreamSynchronize(s), "grow dead");
+      std::swap(B.dead_x.p, nxb.p); std::swap(B.dead_x.bytes, nxb.bytes);
+      std::swap(B.dead_ll.p, nlb.p); std::swap(B.dead_ll.bytes, nlb.bytes);
+      std::swap(B.dead_lp.p, npb.p); std::swap(B.dead_lp.bytes, npb.bytes);
+      B.dead_cap = cap;
+    }
+    a.dead_x = (double*)B.dead_x.p;
+    a.dead_ll = (double*)B.dead_ll.p;
+    a.dead_lp = (double*)B.dead_lp.p;
+    for (int64_t g = gen; g < gen + G; ++g) {
+      KeyBuf& cur = B.keys[(base + g) % 2];
+      KeyBuf& nxt = B.keys[(base + g + 1) % 2];
+      a.key_ll = cur.l();
+      a.key_tie = cur.t();
+      a.key_slot = cur.s();
+      a.mrep = g * k;
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      if (ctx->timing) timing_begin(ctx, &e0, &e1);
+      HC(walk(a, s), "nested walk");
+      if (ctx->timing) timing_end(ctx, e0, e1, 1);
+      HC(launch_retire(a, D, s), "nested retire");
+      HC(launch_estimate(a, s), "nested estimate");
+      bool nk_tmp = false;
+      HC(launch_sort_keys(B.newk.l(), B.newk.t(), B.newk.s(), B.newk_tmp.l(), B.newk_tmp.t(),
+                          B.newk_tmp.s(), k, &nk_tmp, s, a.st), "sort new keys");
+      KeyBuf& nk = nk_tmp ? B.newk_tmp : B.newk;
+      HC(launch_merge_new(a, nxt.l(), nxt.t(), nxt.s(), nk.l(), nk.t(), nk.s(), s), "merge keys");
+      HC(launch_stop(a, nxt.l(), s), "stop test");
+    }
+    gen += G;
+    HC(hipMemcpyAsync(&st, B.st.p, sizeof st, hipMemcpyDeviceToHost, s), "read state");
+    HC(hipStreamSynchronize(s), "nested sync");
+    const int64_t ndead = st.gen_done * k;
+    if (observer && ndead > reported) {
+      const int64_t m = ndead - reported;
+      hx.resize(m * D); hll.resize(m); hlp.resize(m);
+      HC(hipMemcpy(hx.data(), (double*)B.dead_x.p + reported * D, m * D * 8, hipMemcpyDeviceToHost), "observer copy");
+      HC(hipMemcpy(hll.data(), (double*)B.dead_ll.p + reported, m * 8, hipMemcpyDeviceToHost), "observer copy");
+      HC(hipMemcpy(hlp.data(), (double*)B.dead_lp.p + reported, m * 8, hipMemcpyDeviceToHost), "observer copy");
+      observer(user, hx.data(), hll.data(), hlp.data(), m);
+      reported = ndead;
+    }
+    if (st.error)
+      return set_error(ctx, MCG_EFAIL, "Error in draw_new_live_point: new log(L) below the threshold");
+    if (st.stopped) break;
+    batch = std::min<int64_t>(batch * 2, 64);
+  }
+  // final: dead points in retirement order, then the live set ascending (nested.ml:143)
+  const int64_t ndead = st.gen_done * k;
+  const int64_t ntot = ndead + n;
+  KeyBuf& fin = B.keys[(base + st.gen_done) % 2];
+  NestedState& R = ctx->nested;
+  R.pts.assign((size_t)ntot * D, 0.0);
+  R.ll.assign((size_t)ntot, 0.0);
+  R.lp.assign((size_t)ntot, 0.0);
+  R.wts.assign((size_t)ntot, 0.0);
+  if (ndead > 0) {
+    HC(hipMemcpy(R.pts.data(), B.dead_x.p, ndead * D * 8, hipMemcpyDeviceToHost), "copy dead");
+    HC(hipMemcpy(R.ll.data(), B.dead_ll.p, ndead * 8, hipMemcpyDeviceToHost), "copy dead");
+    HC(hipMemcpy(R.lp.data(), B.dead_lp.p, ndead * 8, hipMemcpyDeviceToHost), "copy dead");
+  }
+  std::vector<int> slots((size_t)n);
+  std::vector<double> lx((size_t)n * D), lll((size_t)n), llp((size_t)n);
+  HC(hipMemcpy(slots.data(), fin.slot.p, n * 4, hipMemcpyDeviceToHost), "copy keys");
+  HC(hipMemcpy(lx.data(), B.x.p, n * D * 8, hipMemcpyDeviceToHost), "copy live");
+  HC(hipMemcpy(lll.data(), B.ll.p, n * 8, hipMemcpyDeviceToHost), "copy live");
+  HC(hipMemcpy(llp.data(), B.lp.p, n * 8, hipMemcpyDeviceToHost), "copy live");
+  for (int64_t j = 0; j < n; ++j) {
+    const int sl = slots[(size_t)j];
+    std::memcpy(&R.pts[(size_t)(ndead + j) * D], &lx[(size_t)sl * D], sizeof(double) * D);
+    R.ll[(size_t)(ndead + j)] = lll[(size_t)sl];
+    R.lp[(size_t)(ndead + j)] = llp[(size_t)sl];
+  }
+  evidence_weights(ntot, n, k, R.ll.data(), &R.log_ev, &R.log_dev, R.wts.data());
+  R.n_total = ntot;
+  R.n_dead = ndead;
+  R.n_gen = st.gen_done;
+  R.nlive = n;
+  if (res) {
+    res->log_ev = R.log_ev;
+    res->log_dev = R.log_dev;
+    res->n_dead = ndead;
+    res->n_total = ntot;
+    res->n_gen = st.gen_done;
+  }
+#undef HC
+  return MCG_OK;
 }
+
 int mcg_nested_get(mcg_ctx* ctx, double* pts, double* ll, double* lp, double* log_wts) {
-  (void)pts; (void)ll; (void)lp; (void)log_wts;
-  return set_error(ctx, MCG_ESTATE, "no nested run");
+  if (!ctx) return MCG_EINVAL;
+  const NestedState& R = ctx->nested;
+  if (R.n_total == 0) return set_error(ctx, MCG_ESTATE, "no nested run");
+  if (pts) std::copy(R.pts.begin(), R.pts.end(), pts);
+  if (ll) std::copy(R.ll.begin(), R.ll.end(), ll);
+  if (lp) std::copy(R.lp.begin(), R.lp.end(), lp);
+  if (log_wts) std::copy(R.wts.begin(), R.wts.end(), log_wts);
+  return MCG_OK;
 }
-}
+
+}  // extern "C"
+
+void mcg_free_nested_bufs(mcg_nested_bufs_holder* h) { delete h; }

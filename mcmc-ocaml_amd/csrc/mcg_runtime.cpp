@@ -150,6 +150,8 @@ void mcg_ctx_destroy(mcg_ctx* ctx) {
   (void)hipSetDevice(ctx->opts.device);
   (void)hipStreamSynchronize(ctx->stream);
   timing_harvest(ctx);
+  mcg_free_nested_bufs(ctx->nested_bufs);
+  ctx->nested_bufs = nullptr;
   for (hipEvent_t e : ctx->ev_free) (void)hipEventDestroy(e);
   (void)hipEventDestroy(ctx->ev0);
   (void)hipEventDestroy(ctx->ev1);

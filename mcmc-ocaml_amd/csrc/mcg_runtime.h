@@ -42,6 +42,9 @@ struct NestedState {
 
 }  // namespace mcg
 
+struct mcg_nested_bufs_holder;
+void mcg_free_nested_bufs(mcg_nested_bufs_holder* h);
+
 struct mcg_ctx {
   mcg_opts opts{};
   std::string err;
@@ -70,6 +73,7 @@ struct mcg_ctx {
   bool rec_x_valid = false, rec_llp_valid = false, last_record_accept = false;
   // nested sampling
   mcg::NestedState nested;
+  mcg_nested_bufs_holder* nested_bufs = nullptr;
   // timing: per-launch HIP event pairs on the launch stream, harvested lazily (no host sync
   // inside mcg_run)
   bool timing = false;

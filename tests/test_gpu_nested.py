@@ -1,0 +1,134 @@
+"""GPU tests of the nested sampler (Nested.nested_evidence, nested.ml:122-146): bit-exact
+parity with the oracle for k = 1 (the reference algorithm) and k > 1 (batched retirement), and
+the reference's own statistical tests (test/nested_test.ml) on the GPU path."""
+import math
+
+import numpy as np
+import pytest
+
+
+
+@pytest.fixture(scope="module")
+def T():
+    from mcmc_amd import targets
+    return targets
+
+
+def unit_square_gauss(T):
+    # test/nested_test.ml:23-34: N(0.5, 0.1^2) x N(0.5, 0.1^2) on the open unit square
+    return T.diag_gauss([0.5, 0.5], [0.1, 0.1]), T.box([0, 0], [1, 1], 0.0, open_=True)
+
+
+def oracle_nested(O, lik, pri, seed, quirk=True, **kw):
+    m = O.Model(lik.ndim, lik.kind, lik.params, pri.kind, pri.params, 1, [1.0])
+    return O.nested(m, seed, quirk=quirk, **kw)
+
+
+def gpu_nested(lik, pri, seed, fixed_stop=False, **kw):
+    from mcmc_amd import Context, nested
+    ctx = Context(seed=seed, flags=1 if fixed_stop else 0)
+    out = nested.nested_evidence(lik, pri, ctx=ctx, **kw)
+    ctx.close()
+    return out
+
+
+def assert_nested_same(g, o):
+    log_ev, log_dev, pts, w = g
+    assert g.n_dead == o["n_dead"]
+    np.testing.assert_array_equal(g.ll, o["ll"])
+    np.testing.assert_array_equal(g.lp, o["lp"])
+    np.testing.assert_array_equal(pts, o["pts"])
+    np.testing.assert_array_equal(w, o["log_wts"])
+    assert log_ev == o["log_ev"] and log_dev == o["log_dev"]
+
+
+@pytest.mark.gpu
+def test_nested_k1_bit_exact(oracle, T):
+    lik, pri = unit_square_gauss(T)
+    g = gpu_nested(lik, pri, 3, nlive=64, nmcmc=20, mode_hopping_frac=0.1, k=1)
+    o = oracle_nested(oracle, lik, pri, 3, nlive=64, nmcmc=20, mode_hop=0.1, k=1)
+    assert_nested_same(g, o)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,fixed", [(4, False), (16, True), (100, False)])
+def test_nested_batched_bit_exact(oracle, T, k, fixed):
+    D = 3
+    lik = T.gauss_shell(np.zeros(D), 1.0, 0.2)
+    pri = T.box(-2 * np.ones(D), 2 * np.ones(D))
+    g = gpu_nested(lik, pri, 5, fixed_stop=fixed, nlive=300, nmcmc=15, mode_hopping_frac=0.1, k=k)
+    o = oracle_nested(oracle, lik, pri, 5, quirk=not fixed, nlive=300, nmcmc=15, mode_hop=0.1, k=k)
+    assert_nested_same(g, o)
+    assert np.all(np.diff(g.ll) >= 0)
+
+
+@pytest.mark.gpu
+def test_nested_initial_sort_multi_chunk(oracle, T):
+    """nlive > 2048 exercises the chunked bitonic sort + merge passes of the initial live set."""
+    lik = T.diag_gauss([0.3, -0.2, 0.1, 0.0], [0.5, 0.4, 0.3, 0.6])
+    pri = T.box(-3 * np.ones(4), 3 * np.ones(4))
+    g = gpu_nested(lik, pri, 9, nlive=5000, nmcmc=5, mode_hopping_frac=0.0, k=512, max_dead=512 * 6)
+    o = oracle_nested(oracle, lik, pri, 9, nlive=5000, nmcmc=5, mode_hop=0.0, k=512, max_iter=512 * 6)
+    assert_nested_same(g, o)
+
+
+@pytest.mark.gpu
+def test_nested_single_gaussian_reference_test(T):
+    """test/nested_test.ml:23-39 on the GPU path (k = 1): Z = 1 within 2 err, err < 0.1;
+    weights sum to 1 and the weighted mean is 0.5 +- 0.1 (:66-85)."""
+    from mcmc_amd import nested
+    lik, pri = unit_square_gauss(T)
+    out = gpu_nested(lik, pri, 21, nlive=1000, nmcmc=200, k=1)
+    log_ev, log_dev, pts, w = out
+    err = math.exp(nested.log_total_error_estimate(log_ev, log_dev, 1000))
+    assert abs(math.exp(log_ev) - 1.0) < 2 * err
+    assert err < 0.1
+    ww = np.exp(w)
+    assert abs(ww.sum() - 1.0) < 1e-8
+    assert abs((ww * pts[:, 0]).sum() - 0.5) < 0.1
+    # posterior_samples (nested.ml:167-178): mean 0.5 +- 0.05 from 100 draws
+    ps = nested.posterior_samples(100, out)
+    assert len(pts) > 100 and abs(ps[:, 0].mean() - 0.5) < 0.05
+
+
+@pytest.mark.gpu
+def test_nested_observer_sees_every_dead_point(T):
+    from mcmc_amd import Context, nested
+    lik, pri = unit_square_gauss(T)
+    seen = []
+    out = nested.nested_evidence(lik, pri, nlive=200, nmcmc=20, k=8, ctx=Context(seed=4),
+                                 observer=lambda s: seen.append(s[1]))
+    assert len(seen) == out.n_dead
+    np.testing.assert_array_equal(np.array(seen), out.ll[:out.n_dead])
+
+
+def shell_log_z(D, r, w, half):
+    """Analytic log Z of the Gaussian shell in [-half, half]^D by radial quadrature."""
+    from scipy import integrate, special
+    logS = math.log(2.0) + (D / 2) * math.log(math.pi) - special.gammaln(D / 2)
+    f = lambda t: math.exp((D - 1) * math.log(t) - 0.5 * ((t - r) / w) ** 2 - (D - 1) * math.log(r))
+    val, _ = integrate.quad(f, max(1e-9, r - 12 * w), r + 12 * w, limit=200)
+    return logS + (D - 1) * math.log(r) + math.log(val) - 0.5 * math.log(2 * math.pi * w * w) - D * math.log(2 * half)
+
+
+def test_shell_analytic_value():
+    assert abs(shell_log_z(16, 2.0, 0.1, 6.0) - (-27.7814)) < 1e-3
+    # Feroz & Hobson's published two-shell values (twice the single-shell evidence)
+    for D, pub in [(2, -1.75), (5, -5.67), (10, -14.59), (20, -36.09), (30, -60.13)]:
+        assert abs(shell_log_z(D, 2.0, 0.1, 6.0) + math.log(2.0) - pub) < 0.01, D
+
+
+@pytest.mark.gpu
+def test_c3_shell_batched_reduced_size(T):
+    """C3 shape at reduced size (D=16 shell, nlive=16384, k=512): log Z within 3 sigma_H of the
+    analytic value (sigma_H = sqrt(H/nlive))."""
+    D = 16
+    lik = T.gauss_shell(np.zeros(D), 2.0, 0.1)
+    pri = T.box(-6 * np.ones(D), 6 * np.ones(D))
+    out = gpu_nested(lik, pri, 31, nlive=16384, nmcmc=100, mode_hopping_frac=0.1, k=512)
+    log_ev, _, pts, w = out
+    ww = np.exp(w)
+    H = float((ww * (out.ll - log_ev)).sum())
+    sig = math.sqrt(H / 16384)
+    truth = shell_log_z(D, 2.0, 0.1, 6.0)
+    assert abs(log_ev - truth) < 3 * sig + 0.02, (log_ev, truth, sig)
