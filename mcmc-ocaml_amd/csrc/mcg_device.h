@@ -49,6 +49,8 @@ struct MhArgs {
   int64_t next_r;       // absolute record index of that record
   int64_t rec_end;      // absolute record index bound (exclusive)
   int64_t rec_base;     // absolute index of this run's record 0 (storage index = r - rec_base)
+  const double* inv_n;  // inv_n[R - next_r0] = 1/(R+1) for the records of this launch
+  int64_t next_r0;      // first record index covered by inv_n
   int64_t data_n;       // GAUSS_DATA / CAUCHY_DATA: number of data rows
   uint32_t k0, k1;      // Philox key = seed
   uint32_t chain_offset;

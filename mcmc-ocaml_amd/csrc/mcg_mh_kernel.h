@@ -196,7 +196,6 @@ __device__ __forceinline__ double eval_prior(const double* y, int sub, const MhA
   using L = Layout<D, P>;
   if (a.prior_kind == MCG_PRIOR_FLAT) return 0.0;
   int inb = 1;
-  bool open = a.prior_kind == MCG_PRIOR_OPEN_BOX;
 #pragma unroll
   for (int i = 0; i < L::NCL; ++i)
 #pragma unroll
@@ -204,9 +203,7 @@ __device__ __forceinline__ double eval_prior(const double* y, int sub, const MhA
       if (!L::valid(sub, i, k)) continue;
       int d = L::dim(sub, i, k);
       double v = y[4 * i + k];
-      const int okc = (int)(v >= q[d]) & (int)(v <= q[D + d]);
-      const int oko = (int)(v > q[d]) & (int)(v < q[D + d]);
-      inb &= open ? oko : okc;
+      inb &= (int)(v >= q[d]) & (int)(v <= q[D + d]);   // closed form of the box (see above)
     }
   inb = and_lanes<P>(inb);
   return inb ? q[2 * D] : -__builtin_inf();
@@ -220,12 +217,19 @@ struct AccumCfg {
   static constexpr int kLdsBytes = kLds ? 2 * Layout<D, P>::NL * 256 * 8 : 0;
 };
 
+#ifndef MCG_MH_MIN_WAVES
+#define MCG_MH_MIN_WAVES 1
+#endif
+
 template <int D, int P, int LIK, int PROP>
-__global__ void __launch_bounds__(256) mh_kernel(const MhArgs a) {
+__global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs a) {
   using L = Layout<D, P>;
   constexpr bool kSeparable = (LIK == MCG_LIK_DIAG_GAUSS || LIK == MCG_LIK_GAUSS_SHELL ||
                                LIK == MCG_LIK_FLAT) && PROP == MCG_PROP_GAUSS;
   extern __shared__ double lds_acc[];
+  __shared__ double2 s_lt[92];                       // log table staged in LDS (LDS gather)
+  for (int i = threadIdx.x; i < 92; i += blockDim.x) s_lt[i] = kLogTab[i];
+  __syncthreads();
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int sub = (int)(tid & (P - 1));
   const int64_t chain = tid / P;
@@ -288,7 +292,7 @@ __global__ void __launch_bounds__(256) mh_kernel(const MhArgs a) {
       a.rec_lp[s * N + c] = lp;
     }
     if (accum) {
-      const double inv = 1.0 / (double)(R + 1);
+      const double inv = a.inv_n[R - a.next_r0];      // 1/(R+1), host IEEE division
 #pragma unroll
       for (int i = 0; i < L::NCL; ++i)
 #pragma unroll
@@ -324,6 +328,7 @@ __global__ void __launch_bounds__(256) mh_kernel(const MhArgs a) {
     ++r;
   }
 
+  double lu_own = 0.0;
   for (int64_t t = 0; t < a.nsteps; ++t) {
     const uint64_t T = a.step_base + (uint64_t)t;
     const uint32_t tlo = (uint32_t)T, thi = (uint32_t)(T >> 32);
@@ -343,7 +348,6 @@ __global__ void __launch_bounds__(256) mh_kernel(const MhArgs a) {
       for (int j = 0; j < L::NA; ++j) A[j] = 0.0;
       int inb = 1;
       const bool box = a.prior_kind != MCG_PRIOR_FLAT;
-      const bool open = a.prior_kind == MCG_PRIOR_OPEN_BOX;
 #pragma unroll
       for (int i = 0; i < L::NCL; ++i) {
         if (P == 1 && 4 * i >= D) continue;
@@ -351,8 +355,8 @@ __global__ void __launch_bounds__(256) mh_kernel(const MhArgs a) {
         const int cc = sub + P * i;
         const u32x4 w = rng(gid, tlo, (uint32_t)cc, TAG_MH, thi);
         double z[4];
-        normal_pair(w.x, w.y, z[0], z[1]);
-        normal_pair(w.z, w.w, z[2], z[3]);
+        normal_pair(w.x, w.y, z[0], z[1], s_lt);
+        normal_pair(w.z, w.w, z[2], z[3], s_lt);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           if (!L::valid(sub, i, k)) continue;
@@ -367,11 +371,10 @@ __global__ void __launch_bounds__(256) mh_kernel(const MhArgs a) {
             A[i % L::NA] = fma(e, e, A[i % L::NA]);
           }
           {
-            // branch-free box test; the host pads FLAT priors with a valid (unused) box
+            // branch-free closed-box test: the host stores an OPEN box as its closed equivalent
+            // [nextafter(lo, +inf), nextafter(hi, -inf)] and pads FLAT priors with (-inf, inf)
             const double lo = qpri[d], hi = qpri[D + d];
-            const int okc = (int)(yv >= lo) & (int)(yv <= hi);
-            const int oko = (int)(yv > lo) & (int)(yv < hi);
-            inb &= open ? oko : okc;
+            inb &= (int)(yv >= lo) & (int)(yv <= hi);
           }
         }
       }
@@ -398,8 +401,8 @@ __global__ void __launch_bounds__(256) mh_kernel(const MhArgs a) {
           if (P == 1 && 4 * i >= D) continue;
           const u32x4 w = rng(gid, tlo, (uint32_t)cc, TAG_MH, thi);
           double z[4];
-          normal_pair(w.x, w.y, z[0], z[1]);
-          normal_pair(w.z, w.w, z[2], z[3]);
+          normal_pair(w.x, w.y, z[0], z[1], s_lt);
+          normal_pair(w.z, w.w, z[2], z[3], s_lt);
 #pragma unroll
           for (int k = 0; k < 4; ++k)
             if (L::valid(sub, i, k)) y[4 * i + k] = x[4 * i + k] + qprop[L::dim(sub, i, k)] * z[k];
@@ -441,8 +444,21 @@ __global__ void __launch_bounds__(256) mh_kernel(const MhArgs a) {
     const double post_y = lly + lpy;
     const double post_x = ll + lp;
     const double ratio = ((post_y - post_x) + lb) - lf;
-    const u32x4 wa = rng(gid, tlo, CALL_ACCEPT, TAG_MH, thi);
-    const double lu = plog(u53(wa.x, wa.y));
+    double lu;
+    if constexpr (P == 1) {
+      const u32x4 wa = rng(gid, tlo, CALL_ACCEPT, TAG_MH, thi);
+      lu = plog(u53(wa.x, wa.y), s_lt);
+    } else {
+      // staggered accept uniforms: at the first step of each group of P steps, lane `sub` of the
+      // chain draws log u for step t + sub; step t + q reads it from lane q (one shuffle)
+      const int q = (int)(t & (P - 1));
+      if (q == 0) {
+        const uint64_t Tj = T + (uint64_t)sub;
+        const u32x4 wa = rng(gid, (uint32_t)Tj, CALL_ACCEPT, TAG_MH, (uint32_t)(Tj >> 32));
+        lu_own = plog(u53(wa.x, wa.y), s_lt);
+      }
+      lu = __shfl(lu_own, (lane & ~(P - 1)) | q, 64);
+    }
     const bool acc = lu < ratio;
     if (acc) {
 #pragma unroll

@@ -55,6 +55,9 @@ struct NestArgs {
 // ---- one constrained DE-MCMC walker per lane (draw_new_live_point, nested.ml:50-74) ----
 template <int D, int LIK>
 __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
+  __shared__ double2 s_lt[92];
+  for (int i = threadIdx.x; i < 92; i += blockDim.x) s_lt[i] = kLogTab[i];
+  __syncthreads();
   if (a.st->stopped) return;
   const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= a.k) return;
@@ -90,7 +93,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
       dsc = 1.0;
     } else {
       double z0, z1;
-      normal_pair(rs.z, rs.w, z0, z1);
+      normal_pair(rs.z, rs.w, z0, z1, s_lt);
       dsc = a.sigma_de * z0;
     }
     const double* __restrict__ xi = a.x + (int64_t)i * D;
@@ -101,7 +104,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
     const double ml = (lly >= thr) ? eval_prior<D, 1>(y, 0, a.m, a.m.pri) : -__builtin_inf();
     const double ratio = (((ml + 0.0) - (cur_l + 0.0)) + 0.0) - 0.0;   // mcmc.ml:47-48
     const u32x4 ra = rng(wid, (uint32_t)s, CALL_ACCEPT, TAG_NEST_WALK, 0u);
-    if (plog(u53(ra.x, ra.y)) < ratio) {
+    if (plog(u53(ra.x, ra.y), s_lt) < ratio) {
 #pragma unroll
       for (int d = 0; d < D; ++d) cur[d] = y[d];
       cur_l = ml;

@@ -132,7 +132,8 @@ int mcg_ctx_create(mcg_ctx** out, const mcg_opts* opts) {
   mcg_ctx* ctx = new mcg_ctx();
   ctx->opts = o;
   if (hipSetDevice(o.device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) {
+      hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
+      hipEventCreate(&ctx->inv_ev[0]) != hipSuccess || hipEventCreate(&ctx->inv_ev[1]) != hipSuccess) {
     delete ctx;
     return MCG_EDEVICE;
   }
@@ -155,6 +156,8 @@ void mcg_ctx_destroy(mcg_ctx* ctx) {
   for (hipEvent_t e : ctx->ev_free) (void)hipEventDestroy(e);
   (void)hipEventDestroy(ctx->ev0);
   (void)hipEventDestroy(ctx->ev1);
+  (void)hipEventDestroy(ctx->inv_ev[0]);
+  (void)hipEventDestroy(ctx->inv_ev[1]);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -257,6 +260,11 @@ int mcg_set_prior(mcg_ctx* ctx, int32_t kind, const double* params, size_t n) {
     if (!params || n != (size_t)(2 * D + 1))
       return set_error(ctx, MCG_EINVAL, "BOX: params = lo[D], hi[D], lp_in");
     dev.assign(params, params + n);
+    if (kind == MCG_PRIOR_OPEN_BOX)            // lo < x < hi  <=>  nextup(lo) <= x <= nextdown(hi)
+      for (int d = 0; d < D; ++d) {
+        dev[d] = std::nextafter(params[d], HUGE_VAL);
+        dev[D + d] = std::nextafter(params[D + d], -HUGE_VAL);
+      }
   } else {
     return set_error(ctx, MCG_EINVAL, "unknown prior kind %d", kind);
   }
@@ -464,6 +472,23 @@ int mcg_run(mcg_ctx* ctx, const mcg_run_opts* o) {
   a.nskip = o->nskip;
   a.rec_base = rec_base;
   a.rec_end = rec_base + n_rec;
+  // Welford weights 1/(R+1) of every record of this run (IEEE division on the host, so the
+  // kernel needs no per-step division).  Two buffers alternate between runs; an event guards the
+  // reuse of the one a still-running previous run may read.
+  {
+    const int slot = ctx->inv_slot;
+    ctx->inv_slot ^= 1;
+    std::vector<double>& ih = ctx->inv_host[slot];
+    if ((rc = hip_check(ctx, hipEventSynchronize(ctx->inv_ev[slot]), "inv wait"))) return rc;
+    ih.resize((size_t)std::max<int64_t>(n_rec, 1));
+    for (int64_t q = 0; q < n_rec; ++q) ih[(size_t)q] = 1.0 / (double)(rec_base + q + 1);
+    if ((rc = hip_check(ctx, ctx->d_inv[slot].ensure(ih.size() * 8), "alloc inv"))) return rc;
+    if ((rc = hip_check(ctx, hipMemcpyAsync(ctx->d_inv[slot].p, ih.data(), ih.size() * 8,
+                                            hipMemcpyHostToDevice, ctx->stream), "copy inv"))) return rc;
+    a.inv_n = (const double*)ctx->d_inv[slot].p;
+    a.next_r0 = rec_base;
+    ctx->inv_cur = slot;
+  }
   int64_t spl = ctx->opts.steps_per_launch;
   if (const char* env = std::getenv("MCG_STEPS_PER_LAUNCH")) spl = std::atoll(env);
   if (spl <= 0) spl = std::max<int64_t>(1, std::min<int64_t>(4096, ((int64_t)1 << 26) / N));
@@ -498,6 +523,7 @@ int mcg_run(mcg_ctx* ctx, const mcg_run_opts* o) {
     t0 += n;
     first = false;
   } while (t0 < nsteps);
+  (void)hipEventRecord(ctx->inv_ev[ctx->inv_cur], ctx->stream);
   ctx->steps_done += (uint64_t)nsteps;
   ctx->nsteps_total += nsteps;
   ctx->last_nsteps = nsteps;

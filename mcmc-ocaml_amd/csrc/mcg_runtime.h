@@ -70,6 +70,10 @@ struct mcg_ctx {
   // records and statistics
   mcg::DevBuf d_rec_x, d_rec_ll, d_rec_lp, d_bits, d_mean, d_m2, d_hm_m, d_hm_s, d_tiles;
   int64_t nrec_total = 0, rec_stored = 0;
+  mcg::DevBuf d_inv[2];                  // Welford 1/(R+1) tables, double-buffered per launch
+  hipEvent_t inv_ev[2] = {nullptr, nullptr};
+  int inv_slot = 0, inv_cur = 0;
+  std::vector<double> inv_host[2];
   bool rec_x_valid = false, rec_llp_valid = false, last_record_accept = false;
   // nested sampling
   mcg::NestedState nested;
