@@ -209,11 +209,17 @@ __device__ __forceinline__ double eval_prior(const double* y, int sub, const MhA
   return inb ? q[2 * D] : -__builtin_inf();
 }
 
+#ifndef MCG_ACC_REG_MAX
+#define MCG_ACC_REG_MAX 8
+#endif
+
 template <int D, int P>
 struct AccumCfg {
-  // Welford accumulators live in LDS ([NL][256] doubles each, conflict-free) when they fit in
-  // 64 KiB per block, else they are read-modified-written in HBM at each record.
-  static constexpr bool kLds = Layout<D, P>::NL <= 16;
+  // Welford accumulators of the lane's NL dims: in VGPRs when NL <= MCG_ACC_REG_MAX, else in LDS
+  // ([NL][256] doubles each, conflict-free) when they fit in 64 KiB per block, else
+  // read-modified-written in HBM at each record.
+  static constexpr bool kReg = Layout<D, P>::NL <= MCG_ACC_REG_MAX;
+  static constexpr bool kLds = !kReg && Layout<D, P>::NL <= 16;
   static constexpr int kLdsBytes = kLds ? 2 * Layout<D, P>::NL * 256 * 8 : 0;
 };
 
@@ -253,17 +259,21 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
 
   const bool accum = (a.flags & RUNF_ACCUMULATE) != 0;
   double hm_m = 0.0, hm_s = 0.0;
-  // accumulator slot j of this lane: LDS [j][threadIdx] or HBM [dim][chain]
+  // accumulator slot j of this lane: VGPR, LDS [j][threadIdx] or HBM [dim][chain]
+  constexpr int NR = AccumCfg<D, P>::kReg ? L::NL : 1;
+  double rmean[NR], rm2[NR];
   auto acc_mean = [&](int i, int k) -> double& {
-    if constexpr (AccumCfg<D, P>::kLds) return lds_acc[(4 * i + k) * 256 + threadIdx.x];
+    if constexpr (AccumCfg<D, P>::kReg) return rmean[4 * i + k];
+    else if constexpr (AccumCfg<D, P>::kLds) return lds_acc[(4 * i + k) * 256 + threadIdx.x];
     else return a.mean[(int64_t)L::dim(sub, i, k) * N + c];
   };
   auto acc_m2 = [&](int i, int k) -> double& {
-    if constexpr (AccumCfg<D, P>::kLds) return lds_acc[(L::NL + 4 * i + k) * 256 + threadIdx.x];
+    if constexpr (AccumCfg<D, P>::kReg) return rm2[4 * i + k];
+    else if constexpr (AccumCfg<D, P>::kLds) return lds_acc[(L::NL + 4 * i + k) * 256 + threadIdx.x];
     else return a.m2[(int64_t)L::dim(sub, i, k) * N + c];
   };
   if (accum) {
-    if constexpr (AccumCfg<D, P>::kLds) {
+    if constexpr (AccumCfg<D, P>::kReg || AccumCfg<D, P>::kLds) {
 #pragma unroll
       for (int i = 0; i < L::NCL; ++i)
 #pragma unroll
@@ -298,7 +308,7 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           if (!L::valid(sub, i, k)) continue;
-          if constexpr (!AccumCfg<D, P>::kLds) { if (!active) continue; }
+          if constexpr (!AccumCfg<D, P>::kLds && !AccumCfg<D, P>::kReg) { if (!active) continue; }
           double& mu = acc_mean(i, k);
           double& m2 = acc_m2(i, k);
           const double xv = x[4 * i + k];
@@ -500,7 +510,7 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
     a.nacc[c] += na;
   }
   if (accum) {
-    if constexpr (AccumCfg<D, P>::kLds) {
+    if constexpr (AccumCfg<D, P>::kReg || AccumCfg<D, P>::kLds) {
 #pragma unroll
       for (int i = 0; i < L::NCL; ++i)
 #pragma unroll
