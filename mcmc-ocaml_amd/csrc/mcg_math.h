@@ -22,6 +22,8 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 
 __device__ __forceinline__ u32x4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                         uint32_t k0, uint32_t k1) {
+  // keep the 20 round keys out of long-lived SGPRs: recompute them (SALU adds) per call
+  asm volatile("" : "+s"(k0), "+s"(k1));
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
@@ -229,18 +231,17 @@ __device__ __forceinline__ double pexp(double x) {
   return tiny ? 0.0 : v;
 }
 
-// sqrt: bit-trick rsqrt seed, 4 Newton steps, one residual correction
+// sqrt (spec v3): bit-trick rsqrt seed, 4 Newton steps on 1/sqrt(a), then a * y
 __device__ __forceinline__ double psqrt(double a) {
   double y = bitsd(0x5FE6EB50C7B537A9ull - (dbits(a) >> 1));
+  const double ha = 0.5 * a;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    double h = 0.5 * a * y;
-    double e = fma(-h, y, 0.5);
+    const double h = ha * y;
+    const double e = fma(-h, y, 0.5);
     y = fma(y, e, y);
   }
-  double r = a * y;
-  double d = fma(-r, r, a);
-  return fma(0.5 * y, d, r);
+  return a * y;
 }
 
 // sin/cos on |t| <= pi/4 (fdlibm kernel coefficients)
@@ -262,10 +263,8 @@ __device__ __forceinline__ void psincos(double t, double& s, double& c) {
   pc = fma(z, pc, C3);
   pc = fma(z, pc, C2);
   pc = fma(z, pc, C1);
-  double r = z * pc;
-  double hz = 0.5 * z;
-  double w = 1.0 - hz;
-  c = w + (((1.0 - w) - hz) + z * r);
+  const double qc = fma(z, pc, -0.5);   // spec v3: cos = 1 + z (-1/2 + z P(z))
+  c = fma(z, qc, 1.0);
 }
 
 // Box-Muller pair from two words

@@ -127,7 +127,7 @@ __device__ __forceinline__ double eval_lik(const double* y, int sub, const MhArg
   if constexpr (LIK == MCG_LIK_FLAT) {
     return 0.0;
   } else if constexpr (LIK == MCG_LIK_DIAG_GAUSS || LIK == MCG_LIK_GAUSS_SHELL) {
-    // DIAG: q = mu[D], isig[D], C        SHELL: q = c[D], R, iw, C
+    // DIAG: q = mu/sigma[D], 1/sigma[D], C        SHELL: q = c[D], R, iw, C
     double A[L::NA];
 #pragma unroll
     for (int j = 0; j < L::NA; ++j) A[j] = 0.0;
@@ -137,8 +137,9 @@ __device__ __forceinline__ double eval_lik(const double* y, int sub, const MhArg
       for (int k = 0; k < 4; ++k) {
         if (!L::valid(sub, i, k)) continue;
         int d = L::dim(sub, i, k);
-        double e = y[4 * i + k] - q[d];
-        if constexpr (LIK == MCG_LIK_DIAG_GAUSS) e = e * q[D + d];
+        double e;
+        if constexpr (LIK == MCG_LIK_DIAG_GAUSS) e = fma(y[4 * i + k], q[D + d], -q[d]);
+        else e = y[4 * i + k] - q[d];
         A[i % L::NA] = fma(e, e, A[i % L::NA]);
       }
     double S = reduce_canon<P>(A);
@@ -371,10 +372,10 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
         for (int k = 0; k < 4; ++k) {
           if (!L::valid(sub, i, k)) continue;
           const int d = 4 * cc + k;
-          const double yv = x[4 * i + k] + qprop[d] * z[k];
+          const double yv = fma(qprop[d], z[k], x[4 * i + k]);
           y[4 * i + k] = yv;
           if constexpr (LIK == MCG_LIK_DIAG_GAUSS) {
-            const double e = (yv - qlik[d]) * qlik[D + d];
+            const double e = fma(yv, qlik[D + d], -qlik[d]);   // (y - mu)/sigma
             A[i % L::NA] = fma(e, e, A[i % L::NA]);
           } else if constexpr (LIK == MCG_LIK_GAUSS_SHELL) {
             const double e = yv - qlik[d];
@@ -415,7 +416,7 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
           normal_pair(w.z, w.w, z[2], z[3], s_lt);
 #pragma unroll
           for (int k = 0; k < 4; ++k)
-            if (L::valid(sub, i, k)) y[4 * i + k] = x[4 * i + k] + qprop[L::dim(sub, i, k)] * z[k];
+            if (L::valid(sub, i, k)) y[4 * i + k] = fma(qprop[L::dim(sub, i, k)], z[k], x[4 * i + k]);
         }
       } else if constexpr (PROP == MCG_PROP_WRAP_UNIFORM) {
         static_assert(P == 1, "WRAP: one lane per chain");

@@ -126,8 +126,8 @@ __global__ void __launch_bounds__(256) nest_init_kernel(const NestArgs a, double
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= a.n) return;
   const Rng rng{a.k0, a.k1};
-  const double* __restrict__ lo = a.m.pri;
-  const double* __restrict__ hi = a.m.pri + D;
+  const double* __restrict__ lo = a.m.pri + 2 * D + 1;     // caller's bounds (see mcg_set_prior)
+  const double* __restrict__ hi = a.m.pri + 3 * D + 1;
   double x[D];
 #pragma unroll
   for (int d = 0; d < D; d += 2) {

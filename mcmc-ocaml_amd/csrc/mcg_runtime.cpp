@@ -176,13 +176,13 @@ int mcg_set_likelihood(mcg_ctx* ctx, int32_t kind, int32_t ndim, const double* p
     case MCG_LIK_DIAG_GAUSS: {
       if (D < 1 || n != (size_t)(2 * D) || !params)
         return set_error(ctx, MCG_EINVAL, "DIAG_GAUSS: params = mu[D], sigma[D]");
-      // [mu[D], 1/sigma[D], C = sum_d (-1/2 log 2pi - log sigma_d)]   (stats.ml:98-108)
+      // [mu/sigma[D], 1/sigma[D], C = sum_d (-1/2 log 2pi - log sigma_d)]   (stats.ml:98-108)
       double C = 0.0;
       dev.resize(2 * D + 1);
       for (int d = 0; d < D; ++d) {
         if (!(params[D + d] > 0.0)) return set_error(ctx, MCG_EINVAL, "DIAG_GAUSS: sigma > 0");
-        dev[d] = params[d];
         dev[D + d] = 1.0 / params[D + d];
+        dev[d] = params[d] * dev[D + d];
         C = C + (kNegHalfLog2Pi - std::log(params[D + d]));
       }
       dev[2 * D] = C;
@@ -237,7 +237,7 @@ int mcg_set_likelihood(mcg_ctx* ctx, int32_t kind, int32_t ndim, const double* p
   rc = hip_check(ctx, hipMemcpy(ctx->d_lik.p, dev.data(), dev.size() * 8, hipMemcpyHostToDevice), "copy likelihood");
   if (rc) return rc;
   // keep a padded flat prior / default proposal consistent with D
-  if (ctx->pri_host.size() != (size_t)(2 * D + 1)) {
+  if (ctx->pri_host.size() != (size_t)(4 * D + 1)) {
     double z = 0.0;
     rc = mcg_set_prior(ctx, MCG_PRIOR_FLAT, &z, 0);
     if (rc) return rc;
@@ -249,17 +249,20 @@ int mcg_set_prior(mcg_ctx* ctx, int32_t kind, const double* params, size_t n) {
   if (!ctx) return MCG_EINVAL;
   int D = ctx->D;
   if (D < 1) return set_error(ctx, MCG_ESTATE, "set the likelihood (ndim) first");
-  std::vector<double> dev(2 * D + 1);
+  // device layout: [check_lo[D], check_hi[D], lp_in, lo[D], hi[D]]: the closed-form bounds used
+  // by the kernels' box test, then the caller's bounds (uniform draws of nested sampling)
+  std::vector<double> dev(4 * D + 1);
   if (kind == MCG_PRIOR_FLAT) {
     for (int d = 0; d < D; ++d) {
-      dev[d] = -HUGE_VAL;
-      dev[D + d] = HUGE_VAL;
+      dev[d] = dev[2 * D + 1 + d] = -HUGE_VAL;
+      dev[D + d] = dev[3 * D + 1 + d] = HUGE_VAL;
     }
     dev[2 * D] = 0.0;
   } else if (kind == MCG_PRIOR_BOX || kind == MCG_PRIOR_OPEN_BOX) {
     if (!params || n != (size_t)(2 * D + 1))
       return set_error(ctx, MCG_EINVAL, "BOX: params = lo[D], hi[D], lp_in");
-    dev.assign(params, params + n);
+    std::copy(params, params + n, dev.begin());
+    std::copy(params, params + 2 * D, dev.begin() + 2 * D + 1);
     if (kind == MCG_PRIOR_OPEN_BOX)            // lo < x < hi  <=>  nextup(lo) <= x <= nextdown(hi)
       for (int d = 0; d < D; ++d) {
         dev[d] = std::nextafter(params[d], HUGE_VAL);

@@ -227,17 +227,16 @@ double or_exp(double x) {
   return p * bitsd((uint64_t)(k + 1023) << 52);
 }
 
-/* sqrt via a bit-trick rsqrt seed, 4 Newton steps and one residual correction */
+/* sqrt (spec v3): bit-trick rsqrt seed, 4 Newton steps on 1/sqrt(a), then a * y (<= 2 ulp) */
 double or_sqrt(double a) {
   double y = bitsd(0x5FE6EB50C7B537A9ull - (dbits(a) >> 1));
+  double ha = 0.5 * a;
   for (int i = 0; i < 4; ++i) {
-    double h = 0.5 * a * y;
+    double h = ha * y;
     double e = fma(-h, y, 0.5);
     y = fma(y, e, y);
   }
-  double r = a * y;
-  double d = fma(-r, r, a);
-  return fma(0.5 * y, d, r);
+  return a * y;
 }
 
 /* sin/cos on |t| <= pi/4 (fdlibm __kernel_sin/__kernel_cos coefficients, tail y = 0) */
@@ -259,10 +258,8 @@ void or_sincos_kernel(double t, double* s, double* c) {
   pc = fma(z, pc, C3);
   pc = fma(z, pc, C2);
   pc = fma(z, pc, C1);
-  double r = z * pc;
-  double hz = 0.5 * z;
-  double w = 1.0 - hz;
-  *c = w + (((1.0 - w) - hz) + z * r);
+  double qc = fma(z, pc, -0.5);       /* spec v3: cos = 1 + z (-1/2 + z P(z)), plain Horner */
+  *c = fma(z, qc, 1.0);
 }
 
 /* Box-Muller from two 32-bit words: radius from a, angle from b (quadrant-exact reduction). */
@@ -402,12 +399,13 @@ static int prep_model(const or_model* m, prep_t* p) {
   switch (p->lik) {
     case MCG_LIK_FLAT: break;
     case MCG_LIK_DIAG_GAUSS:
+      /* constants: 1/sigma_d, mu_d/sigma_d (= RN(mu_d * RN(1/sigma_d))), C */
       p->mu = (double*)malloc(sizeof(double) * D);
       p->isig = (double*)malloc(sizeof(double) * D);
       p->C = 0.0;
       for (int d = 0; d < D; ++d) {
-        p->mu[d] = q[d];
         p->isig[d] = 1.0 / q[D + d];
+        p->mu[d] = q[d] * p->isig[d];
         p->C = p->C + (NEG_HALF_LOG_2PI - log(q[D + d]));
       }
       break;
@@ -460,7 +458,7 @@ static double lik_eval(const prep_t* p, const double* x) {
     case MCG_LIK_FLAT: return 0.0;
     case MCG_LIK_DIAG_GAUSS: {
       for (int d = 0; d < D; ++d) {
-        double e = (x[d] - p->mu[d]) * p->isig[d];
+        double e = fma(x[d], p->isig[d], -p->mu[d]);     /* (x - mu)/sigma as x/s - mu/s */
         A[(d >> 2) & 7] = fma(e, e, A[(d >> 2) & 7]);
       }
       return p->C - 0.5 * canon8(A);
@@ -569,7 +567,7 @@ static int mh_step(const prep_t* p, uint64_t seed, uint32_t gid, uint64_t T, cha
     case MCG_PROP_GAUSS: {
       double z[256];
       normals_tagged(seed, gid, lo, TAG_MH, hi, D, z);
-      for (int d = 0; d < D; ++d) y[d] = c->x[d] + p->s[d] * z[d];
+      for (int d = 0; d < D; ++d) y[d] = fma(p->s[d], z[d], c->x[d]);
       break;
     }
     case MCG_PROP_WRAP_UNIFORM: {
