@@ -101,7 +101,7 @@ def main():
     dev = torch.device("cuda", local)
 
     from mcmc_amd import Context, targets as T
-    from mcmc_amd.context import combine_tiles
+    from mcmc_amd.parallel import reduce_stats
 
     D, N, S = args.ndim, args.chains, args.sweeps
     mu, sg, s = c2_target(D)
@@ -128,13 +128,7 @@ def main():
         ctx.run(nbin=0, nskip=1, n_rec=S, record_x=False, record_llp=False, record_accept=False,
                 accumulate=True, append=True)
     # end-of-run reduction: tile kernel -> RCCL all-gather of tile partials -> host combine
-    tiles = ctx.tile_stats()
-    if dist:
-        t = torch.from_numpy(tiles).to(dev)
-        out = [torch.empty_like(t) for _ in range(world)]
-        tdist.all_gather(out, t)
-        tiles = torch.cat(out).cpu().numpy()
-    mean, sd, log_z_hm = combine_tiles(D, tiles)
+    mean, sd, log_z_hm = reduce_stats(D, ctx.tile_stats(), device=dev)
     barrier()
     elapsed = time.perf_counter() - t0
     if dist:
