@@ -75,6 +75,20 @@ def cpu_baseline(args, mu, sg, s):
                        % (nch, nsteps, threads))
 
 
+def pmc_traffic(D, N, S):
+    """HBM bytes per launch of the dominant kernel from the committed PMC passes
+    (profiles/pmc_traffic.json, written by scripts/pmc_traffic.py from scripts/gpu_profile.sh),
+    when they were collected on this exact workload; else None."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as fh:
+            t = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    if t.get("config") != {"ndim": D, "chains_per_gpu": N, "sweeps_per_step": S}:
+        return None
+    return t["traffic_bytes"]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -171,7 +185,9 @@ def main():
                    "ndim": D, "chains_per_gpu": N, "sweeps_per_step": S,
                    "lanes_per_chain": ctx_lanes(ctx), "parallelism": "chains sharded, dp%d" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(D, N, S),
+                     "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+                     "algorithmic_bytes_per_launch": launch_steps * bytes_per_step,
                      "kernel": "mcg::mh_kernel<32,P,DIAG_GAUSS,GAUSS>",
                      "bytes_per_step": bytes_per_step, "avg_launch_ms": per_launch,
                      "launches": timing["launches"]},

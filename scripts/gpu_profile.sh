@@ -7,3 +7,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/trace -o r
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof/fetch -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/prof/fetch.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof/write -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/prof/write.log 2>&1 || exit $?
 echo profile-ok
+python3 scripts/pmc_traffic.py gpurun_out/prof gpurun_out/prof/pmc_traffic.json
