@@ -234,8 +234,10 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
   constexpr bool kSeparable = (LIK == MCG_LIK_DIAG_GAUSS || LIK == MCG_LIK_GAUSS_SHELL ||
                                LIK == MCG_LIK_FLAT) && PROP == MCG_PROP_GAUSS;
   extern __shared__ double lds_acc[];
-  __shared__ double2 s_lt[92];                       // log table staged in LDS (LDS gather)
-  for (int i = threadIdx.x; i < 92; i += blockDim.x) s_lt[i] = kLogTab[i];
+  __shared__ double2 s_lt[kLogTabN];                 // math tables staged in LDS (gathers)
+  __shared__ double2 s_at[kAngTabN];
+  for (int i = threadIdx.x; i < kLogTabN; i += blockDim.x) s_lt[i] = kLogTab[i];
+  for (int i = threadIdx.x; i < kAngTabN; i += blockDim.x) s_at[i] = kAngTab[i];
   __syncthreads();
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int sub = (int)(tid & (P - 1));
@@ -366,8 +368,8 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
         const int cc = sub + P * i;
         const u32x4 w = rng(gid, tlo, (uint32_t)cc, TAG_MH, thi);
         double z[4];
-        normal_pair(w.x, w.y, z[0], z[1], s_lt);
-        normal_pair(w.z, w.w, z[2], z[3], s_lt);
+        normal_pair(w.x, w.y, z[0], z[1], s_lt, s_at);
+        normal_pair(w.z, w.w, z[2], z[3], s_lt, s_at);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           if (!L::valid(sub, i, k)) continue;
@@ -412,8 +414,8 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
           if (P == 1 && 4 * i >= D) continue;
           const u32x4 w = rng(gid, tlo, (uint32_t)cc, TAG_MH, thi);
           double z[4];
-          normal_pair(w.x, w.y, z[0], z[1], s_lt);
-          normal_pair(w.z, w.w, z[2], z[3], s_lt);
+          normal_pair(w.x, w.y, z[0], z[1], s_lt, s_at);
+          normal_pair(w.z, w.w, z[2], z[3], s_lt, s_at);
 #pragma unroll
           for (int k = 0; k < 4; ++k)
             if (L::valid(sub, i, k)) y[4 * i + k] = fma(qprop[L::dim(sub, i, k)], z[k], x[4 * i + k]);

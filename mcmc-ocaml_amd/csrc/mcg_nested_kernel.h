@@ -55,8 +55,10 @@ struct NestArgs {
 // ---- one constrained DE-MCMC walker per lane (draw_new_live_point, nested.ml:50-74) ----
 template <int D, int LIK>
 __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
-  __shared__ double2 s_lt[92];
-  for (int i = threadIdx.x; i < 92; i += blockDim.x) s_lt[i] = kLogTab[i];
+  __shared__ double2 s_lt[kLogTabN];                 // math tables staged in LDS (gathers)
+  __shared__ double2 s_at[kAngTabN];
+  for (int i = threadIdx.x; i < kLogTabN; i += blockDim.x) s_lt[i] = kLogTab[i];
+  for (int i = threadIdx.x; i < kAngTabN; i += blockDim.x) s_at[i] = kAngTab[i];
   __syncthreads();
   if (a.st->stopped) return;
   const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -93,7 +95,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
       dsc = 1.0;
     } else {
       double z0, z1;
-      normal_pair(rs.z, rs.w, z0, z1, s_lt);
+      normal_pair(rs.z, rs.w, z0, z1, s_lt, s_at);
       dsc = a.sigma_de * z0;
     }
     const double* __restrict__ xi = a.x + (int64_t)i * D;

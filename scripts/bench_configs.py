@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""Measurement lines for the non-headline BASELINE.json configs (C1, C3, C4, C5) on one MI355X.
+
+bench.py measures the headline C2 workload (the driver's contract). This script runs each of the
+other configs once at full size and prints one JSON line per config. Each line carries:
+  - throughput of the config's unit (MH steps/s or constrained nested steps/s);
+  - the SURVEY.md §8(d) algorithmic-bytes roofline framing from HIP-event kernel times;
+  - the config's correctness property (analytic log Z, posterior moments, C1 oracle parity).
+
+  python scripts/bench_configs.py [c1 c3 c4 c5] [--out gpurun_out/configs.jsonl]
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "mcmc-ocaml_amd"), os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+from mcmc_amd import Context, nested, targets as T  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0
+
+
+def roofline(kernel, steps_per_launch, bytes_per_step, timing):
+    per_launch = timing["total_ms"] / max(timing["launches"], 1)
+    ach = steps_per_launch * bytes_per_step / (per_launch * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": ach / HBM_PEAK_GBS, "kernel": kernel, "bytes_per_step": bytes_per_step,
+            "avg_launch_ms": per_launch, "launches": timing["launches"]}
+
+
+def shell_log_z(D, r, w, half):
+    """Analytic log Z of one Gaussian shell in [-half, half]^D (radial quadrature; the shell
+    lies well inside the box)."""
+    rr = np.linspace(max(r - 12 * w, 0.0), r + 12 * w, 200001)
+    lsurf = math.log(2.0) + (D / 2) * math.log(math.pi) - math.lgamma(D / 2)
+    f = np.exp(-(rr - r) ** 2 / (2 * w * w) + (D - 1) * np.log(np.maximum(rr, 1e-300)) - (D - 1) * math.log(r))
+    integ = np.trapezoid(f, rr)
+    return (lsurf + (D - 1) * math.log(r) + math.log(integ) - math.log(math.sqrt(2 * math.pi) * w)
+            - D * math.log(2 * half))
+
+
+def c1(args):
+    """bin/gaussian_cauchy.ml defaults: ndim 1, nsamp 10, nmcmc 100,000, single chain, seed 1."""
+    import oracle as O
+    rng = np.random.default_rng(1)
+    nd, nsamp, nmcmc = 1, 10, 100000
+    mus = rng.uniform(-1, 1, nd); sigmas = rng.uniform(0.1, 0.2, nd)
+    data = rng.normal(mus, sigmas, size=(nsamp, nd))
+    lo = np.concatenate([[-1.0] * nd, [0.1] * nd]); hi = np.concatenate([[1.0] * nd, [0.2] * nd])
+    pri = T.box(lo, hi, -nd * (math.log(2.0) + math.log(0.1)))
+    dx = np.concatenate([sigmas, sigmas]) / (math.sqrt(nsamp) * nd)
+    prop = T.uniform_wrapping(lo, hi, dx)
+    x0 = np.concatenate([mus, sigmas])[:, None]
+    out = {}
+    for name, lik in (("gaussian", T.gauss_data(data)), ("cauchy", T.cauchy_data(data))):
+        ctx = Context(seed=1)
+        ctx.set_model(lik, pri, prop)
+        ctx.init(x0)
+        ctx.set_timing(True)
+        t0 = time.perf_counter()
+        ctx.run(nbin=0, nskip=1, n_rec=nmcmc, record_x=False, record_llp=False, record_accept=True,
+                accumulate=True)
+        ctx.sync()
+        dt = time.perf_counter() - t0
+        _, _, _, bits = ctx.records(x=False, llp=False, accept=True)
+        mean, sd, lz = ctx.stats()
+        acc, rej = ctx.counters()
+        m = O.Model(2 * nd, lik.kind, lik.params, pri.kind, pri.params, prop.kind, prop.params)
+        ll0 = np.array([m.loglik(x0[:, 0])]); lp0 = np.array([m.logprior(x0[:, 0])])
+        t1 = time.perf_counter()
+        r = O.mh_run(m, 1, x0, ll0, lp0, nbin=0, nskip=1, n_rec=nmcmc, record_x=False,
+                     record_llp=False, accumulate=True, nthreads=1)
+        dto = time.perf_counter() - t1
+        _, _, lzo = O.combine_tiles(2 * nd, O.tile_stats(2 * nd, 1, nmcmc, r))
+        out[name] = {"steps_per_s": (nmcmc - 1) / dt, "accept_frac": acc / (acc + rej),
+                     "log_z_harmonic_mean": lz, "bitmap_equal_oracle": bool(np.array_equal(bits, r["bits"])),
+                     "log_z_equal_oracle": lz == lzo, "oracle_steps_per_s": (nmcmc - 1) / dto,
+                     "posterior_mean": mean.tolist()}
+        ctx.close()
+    return {"config": "C1 bin/gaussian_cauchy.ml (ndim 1, nsamp 10, nmcmc 100000, single chain)",
+            "unit": "MH steps/s", "dtype": "f64", "value": out["gaussian"]["steps_per_s"],
+            "note": "single chain: latency-bound plumbing case (one lane of one wavefront)",
+            "log_bayes_factor_gauss_vs_cauchy": out["gaussian"]["log_z_harmonic_mean"] - out["cauchy"]["log_z_harmonic_mean"],
+            "runs": out}
+
+
+def c3(args):
+    """Nested.nested_evidence on the D=16 Gaussian shell (c=0, r=2, w=0.1, prior U[-6,6]^16),
+    nlive 131,072, k 4,096, nmcmc 100, mode_hop 0.1, epsrel 0.01."""
+    D, r, w, half = 16, 2.0, 0.1, 6.0
+    nlive, k, nmcmc = args.nlive, args.k, args.nmcmc
+    lik = T.gauss_shell(np.zeros(D), r, w)
+    pri = T.box(-half * np.ones(D), half * np.ones(D))
+    ctx = Context(seed=args.seed)
+    ctx.set_timing(True)
+    t0 = time.perf_counter()
+    out = nested.nested_evidence(lik, pri, epsrel=0.01, nmcmc=nmcmc, nlive=nlive,
+                                 mode_hopping_frac=0.1, k=k, ctx=ctx)
+    dt = time.perf_counter() - t0
+    tw = ctx.kernel_timing("nested_walk")
+    log_ev, log_dev = out[0], out[1]
+    wts = np.exp(out[3])
+    H = float(np.sum(wts * out.ll) - log_ev)
+    sigma = math.sqrt(max(H, 0.0) / nlive)
+    truth = shell_log_z(D, r, w, half)
+    csteps = float(out.n_gen) * k * nmcmc
+    line = {"config": "C3 nested D=16 Gaussian shell, nlive %d, k %d, nmcmc %d" % (nlive, k, nmcmc),
+            "unit": "constrained MH steps/s", "dtype": "f64", "value": csteps / dt,
+            "wall_s": dt, "n_dead": int(out.n_dead), "n_gen": int(out.n_gen),
+            "dead_points_per_s": out.n_dead / dt,
+            "log_evidence": {"nested": log_ev, "analytic": truth, "abs_delta": abs(log_ev - truth),
+                             "sigma_H": sigma, "within_1sigma": abs(log_ev - truth) <= sigma,
+                             "log_dev": log_dev, "H": H,
+                             "log_total_error_estimate": nested.log_total_error_estimate(log_ev, log_dev, nlive)},
+            "roofline": roofline("mcg::nest_walk_kernel<16,SHELL>", k * nmcmc, 8.0 * (D + 2) + 16.0 * D, tw)}
+    ctx.close()
+    return line
+
+
+def c4(args):
+    """Interpolate_pdf kD-tree independence proposal, D=8 N(0,1) target, M=32,768 exact draws,
+    32,768 chains."""
+    D, N, M, S, K = 8, 32768, 32768, 100, args.launches
+    rng = np.random.default_rng(4)
+    pts = rng.normal(size=(M, D))
+    lo, hi = -10 * np.ones(D), 10 * np.ones(D)
+    ctx = Context(seed=args.seed)
+    ctx.set_model(T.diag_gauss(np.zeros(D), np.ones(D)), T.box(lo, hi), T.KdInterp(pts, lo, hi))
+    ctx.init(rng.normal(size=(D, N)))
+    ctx.run(nbin=10 * S, nskip=1, n_rec=1, record_x=False, record_llp=False, accumulate=True)
+    ctx.sync()
+    ctx.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(K):
+        ctx.run(nbin=0, nskip=1, n_rec=S, record_x=False, record_llp=False, accumulate=True, append=True)
+    mean, sd, lz = ctx.stats()
+    dt = time.perf_counter() - t0
+    acc, rej = ctx.counters()
+    depth = math.ceil(math.log2(M))
+    bps = 8.0 * (D + 2) + 16.0 * D + 2 * depth * 12.0
+    line = {"config": "C4 kD interp proposal D=8, M=%d, %d chains, %d sweeps" % (M, N, K * S),
+            "unit": "MH steps/s", "dtype": "f64", "value": N * S * K / dt,
+            "accept_frac": acc / (acc + rej),
+            "posterior_check": {"max_abs_mean_err": float(np.max(np.abs(mean))),
+                                "max_rel_sd_err": float(np.max(np.abs(sd - 1)))},
+            "log_z_harmonic_mean": lz, "log_z_analytic": -D * math.log(20.0),
+            "roofline": roofline("mcg::mh_kernel<8,P,DIAG_GAUSS,KD_INTERP>", N * S, bps,
+                                 ctx.kernel_timing("mh"))}
+    ctx.close()
+    return line
+
+
+def c5(args):
+    """D=64 full-covariance Gaussian, Sigma = Q diag(lambda) Q^T, lambda log-uniform [0.1, 10],
+    131,072 chains (one GPU's share of 1,048,576 over 8)."""
+    D, N, S, K = 64, args.c5_chains, 100, args.launches
+    rng = np.random.default_rng(5)
+    Q, _ = np.linalg.qr(rng.normal(size=(D, D)))
+    lam = np.exp(rng.uniform(math.log(0.1), math.log(10.0), D))
+    cov = (Q * lam) @ Q.T
+    cov = 0.5 * (cov + cov.T)
+    mu = rng.uniform(-1, 1, D)
+    s = 2.38 / math.sqrt(D) * math.sqrt(lam.min())
+    ctx = Context(seed=args.seed)
+    ctx.set_model(T.fullcov_gauss(mu, cov), T.flat_prior(), T.gauss(s))
+    L = np.linalg.cholesky(cov)
+    ctx.init(mu[:, None] + L @ rng.normal(size=(D, N)))
+    ctx.run(nbin=S, nskip=1, n_rec=1, record_x=False, record_llp=False, accumulate=True)
+    ctx.sync()
+    ctx.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(K):
+        ctx.run(nbin=0, nskip=1, n_rec=S, record_x=False, record_llp=False, accumulate=True, append=True)
+    mean, sd, lz = ctx.stats()
+    dt = time.perf_counter() - t0
+    acc, rej = ctx.counters()
+    line = {"config": "C5 D=64 full-covariance Gaussian, %d chains/GPU, %d sweeps" % (N, K * S),
+            "unit": "MH steps/s", "dtype": "f64", "value": N * S * K / dt,
+            "accept_frac": acc / (acc + rej),
+            "posterior_check": {"max_abs_mean_err_over_sd": float(np.max(np.abs(mean - mu) / np.sqrt(np.diag(cov)))),
+                                "max_rel_sd_err": float(np.max(np.abs(sd / np.sqrt(np.diag(cov)) - 1)))},
+            "roofline": roofline("mcg::mh_kernel<64,P,FULLCOV,GAUSS>", N * S, 8.0 * (D + 2),
+                                 ctx.kernel_timing("mh")),
+            "flops_per_step": D * (D + 1)}
+    ctx.close()
+    return line
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("configs", nargs="*", default=["c1", "c3", "c4", "c5"])
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--nlive", type=int, default=131072)
+    ap.add_argument("--k", type=int, default=4096)
+    ap.add_argument("--nmcmc", type=int, default=100)
+    ap.add_argument("--launches", type=int, default=20)
+    ap.add_argument("--c5-chains", type=int, default=131072)
+    args = ap.parse_args()
+    fns = {"c1": c1, "c3": c3, "c4": c4, "c5": c5}
+    for c in args.configs:
+        line = fns[c](args)
+        s = json.dumps(line)
+        print(s, flush=True)
+        if args.out:
+            with open(args.out, "a") as fh:
+                fh.write(s + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -75,20 +75,31 @@ def test_nested_initial_sort_multi_chunk(oracle, T):
 @pytest.mark.gpu
 def test_nested_single_gaussian_reference_test(T):
     """test/nested_test.ml:23-39 on the GPU path (k = 1): Z = 1 within 2 err, err < 0.1;
-    weights sum to 1 and the weighted mean is 0.5 +- 0.1 (:66-85)."""
+    weights sum to 1 and the weighted mean is 0.5 +- 0.1 (:66-85).
+
+    The reference's `within 2 err` is a ~95 % statistical test on one unseeded run, and its
+    error estimate (nested.ml:148-150) understates the run-to-run spread by ~1.4x at this size
+    (40 oracle seeds: sd of (Z-1)/err = 1.38).  So: 6 seeds, all within 4 err, at least 4 of 6
+    within 2 err, and the mean of Z within 2 err / sqrt(6) * 1.5 of 1."""
     from mcmc_amd import nested
     lik, pri = unit_square_gauss(T)
-    out = gpu_nested(lik, pri, 21, nlive=1000, nmcmc=200, k=1)
-    log_ev, log_dev, pts, w = out
-    err = math.exp(nested.log_total_error_estimate(log_ev, log_dev, 1000))
-    assert abs(math.exp(log_ev) - 1.0) < 2 * err
-    assert err < 0.1
-    ww = np.exp(w)
-    assert abs(ww.sum() - 1.0) < 1e-8
-    assert abs((ww * pts[:, 0]).sum() - 0.5) < 0.1
-    # posterior_samples (nested.ml:167-178): mean 0.5 +- 0.05 from 100 draws
-    ps = nested.posterior_samples(100, out)
-    assert len(pts) > 100 and abs(ps[:, 0].mean() - 0.5) < 0.05
+    zs, errs, inside = [], [], 0
+    for seed in (21, 22, 23, 24, 25, 26):
+        out = gpu_nested(lik, pri, seed, nlive=1000, nmcmc=200, k=1)
+        log_ev, log_dev, pts, w = out
+        err = math.exp(nested.log_total_error_estimate(log_ev, log_dev, 1000))
+        assert err < 0.1
+        assert abs(math.exp(log_ev) - 1.0) < 4 * err
+        inside += abs(math.exp(log_ev) - 1.0) < 2 * err
+        zs.append(math.exp(log_ev)); errs.append(err)
+        ww = np.exp(w)
+        assert abs(ww.sum() - 1.0) < 1e-8
+        assert abs((ww * pts[:, 0]).sum() - 0.5) < 0.1
+        # posterior_samples (nested.ml:167-178): mean 0.5 +- 0.05 from 100 draws
+        ps = nested.posterior_samples(100, out)
+        assert len(pts) > 100 and abs(ps[:, 0].mean() - 0.5) < 0.05
+    assert inside >= 4
+    assert abs(np.mean(zs) - 1.0) < 1.5 * 2 * np.mean(errs) / math.sqrt(len(zs))
 
 
 @pytest.mark.gpu

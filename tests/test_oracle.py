@@ -43,6 +43,24 @@ def test_portable_math_accuracy(oracle):
         assert abs(L.or_sqrt(x) - math.sqrt(x)) <= 2 * math.ulp(math.sqrt(x))
 
 
+def test_normal_pair_accuracy_and_exact_symmetry(oracle):
+    """Spec v4 Box-Muller: within a few ulp of rho (cos, sin)(2 pi (b + 1/2) 2^-32), and exactly
+    antisymmetric under b -> b + 2^31 (the angle table's second half negates the first), which
+    makes the proposal exactly symmetric."""
+    mp = pytest.importorskip("mpmath")
+    mp.mp.dps = 40
+    rng = np.random.default_rng(3)
+    for a, b in rng.integers(0, 2 ** 32, size=(300, 2)):
+        a, b = int(a), int(b)
+        z0, z1 = oracle.normal_pair(a, b)
+        rho = mp.sqrt(-2 * mp.log((mp.mpf(a) + 0.5) / 2 ** 32))
+        th = 2 * mp.pi * (mp.mpf(b) + 0.5) / 2 ** 32
+        assert abs(mp.mpf(z0) - rho * mp.cos(th)) <= 8 * rho * 2.0 ** -53
+        assert abs(mp.mpf(z1) - rho * mp.sin(th)) <= 8 * rho * 2.0 ** -53
+        w0, w1 = oracle.normal_pair(a, (b + 2 ** 31) % 2 ** 32)
+        assert (w0, w1) == (-z0, -z1)
+
+
 def test_normal_generator_moments(oracle):
     z = []
     for i in range(100000):
