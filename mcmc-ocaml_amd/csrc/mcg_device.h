@@ -24,8 +24,8 @@ struct MhArgs {
   unsigned long long* nacc;  // [N] accepted-step counters (mcmc.ml:27-35)
   double* mean;         // [D][N] Welford accumulators over recorded samples
   double* m2;           // [D][N]
-  double* hm_m;         // [N] log-space harmonic-mean partial: max of -ll
-  double* hm_s;         // [N]                                   sum exp(-ll - max)
+  double* hm_m;         // [8][N] log-space harmonic-mean partials of the record classes R & 7:
+  double* hm_s;         // [8][N]   max of -ll and sum exp(-ll - max) (s == 0: empty class)
   double* rec_x;        // [n_rec][D][N]
   double* rec_ll;       // [n_rec][N]
   double* rec_lp;       // [n_rec][N]

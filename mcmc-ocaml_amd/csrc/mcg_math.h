@@ -193,6 +193,24 @@ __device__ __forceinline__ double plse(double a, double b) {
   return a + plog1p(pexp(b - a));
 }
 
+// log-space harmonic-mean partial (m, s) += v = -ll (evidence.ml:101-107 in log space);
+// s == 0 marks an empty partial.  Branch-free form of oracle.c hm_update.
+__device__ __forceinline__ void hm_update(double& m, double& s, double v) {
+  const double e = (v == m) ? 1.0 : pexp(-fabs(v - m));
+  const double s_up = (v > m) ? s * e + 1.0 : s + e;
+  const bool empty = s == 0.0;
+  s = empty ? 1.0 : s_up;
+  m = (empty || v > m) ? v : m;
+}
+
+__device__ __forceinline__ void hm_comb(double& ma, double& sa, double mb, double sb) {
+  if (sb == 0.0) return;
+  if (sa == 0.0) { ma = mb; sa = sb; return; }
+  const double mm = (ma > mb) ? ma : mb;
+  sa = sa * pexp(ma - mm) + sb * pexp(mb - mm);
+  ma = mm;
+}
+
 // canonical 8-accumulator reduction tree (DESIGN.md §Canonical sums)
 __device__ __forceinline__ double canon8(const double* A) {
   return ((A[0] + A[4]) + (A[2] + A[6])) + ((A[1] + A[5]) + (A[3] + A[7]));

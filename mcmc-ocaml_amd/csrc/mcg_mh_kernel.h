@@ -261,7 +261,13 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
   unsigned long long na = 0;
 
   const bool accum = (a.flags & RUNF_ACCUMULATE) != 0;
-  double hm_m = 0.0, hm_s = 0.0;
+  // harmonic-mean partials of the 8 record classes R & 7: lane `sub` owns the
+  // classes c = sub + P l.  The -ll of record R is parked in lane R mod P and folded when the
+  // group of P records is complete, so each lane evaluates one exp per P records.
+  constexpr int NH = P >= 8 ? 1 : 8 / P;
+  double hcm[NH], hcs[NH];
+  double hm_pv = 0.0;
+  bool hm_pok = false;
   // accumulator slot j of this lane: VGPR, LDS [j][threadIdx] or HBM [dim][chain]
   constexpr int NR = AccumCfg<D, P>::kReg ? L::NL : 1;
   double rmean[NR], rm2[NR];
@@ -286,9 +292,22 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
           acc_m2(i, k) = L::valid(sub, i, k) ? a.m2[o] : 0.0;
         }
     }
-    hm_m = a.hm_m[c];
-    hm_s = a.hm_s[c];
+#pragma unroll
+    for (int l = 0; l < NH; ++l) {
+      hcm[l] = a.hm_m[(int64_t)(sub + P * l) * N + c];
+      hcs[l] = a.hm_s[(int64_t)(sub + P * l) * N + c];
+    }
   }
+  // fold the parked record of the group starting at record R0 (R0 % P == 0)
+  auto hm_flush = [&](int64_t R0) {
+    const int li = (int)((R0 & 7) / P);
+    if (hm_pok) {
+#pragma unroll
+      for (int l = 0; l < NH; ++l)
+        if (l == li) hm_update(hcm[l], hcs[l], hm_pv);
+    }
+    hm_pok = false;
+  };
 
   int64_t next_rec = a.next_rec, r = a.next_r;
   auto record = [&](int64_t R) {
@@ -320,19 +339,12 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
           m2 = fma(delta, xv - mnew, m2);
           mu = mnew;
         }
-      const double v = -ll;
-      if (R == 0) {
-        hm_m = v;
-        hm_s = 1.0;
-      } else {
-        const double e = (v == hm_m) ? 1.0 : pexp(-fabs(v - hm_m));
-        if (v > hm_m) {
-          hm_s = hm_s * e + 1.0;
-          hm_m = v;
-        } else {
-          hm_s = hm_s + e;
-        }
+      const int jr = (int)(R & (P - 1));
+      if (sub == jr) {
+        hm_pv = -ll;
+        hm_pok = true;
       }
+      if (jr == P - 1) hm_flush(R - (P - 1));
     }
   };
 
@@ -524,9 +536,12 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
             a.m2[o] = acc_m2(i, k);
           }
     }
-    if (sub == 0) {
-      a.hm_m[c] = hm_m;
-      a.hm_s[c] = hm_s;
+    // a partial group at the end of the launch: fold it now (the classes keep record order)
+    hm_flush((r - 1) & ~(int64_t)(P - 1));
+#pragma unroll
+    for (int l = 0; l < NH; ++l) {
+      a.hm_m[(int64_t)(sub + P * l) * N + c] = hcm[l];
+      a.hm_s[(int64_t)(sub + P * l) * N + c] = hcs[l];
     }
   }
 }

@@ -455,11 +455,13 @@ int mcg_run(mcg_ctx* ctx, const mcg_run_opts* o) {
   if (o->accumulate) {
     if ((rc = hip_check(ctx, ctx->d_mean.ensure(Nz * D * 8), "alloc mean"))) return rc;
     if ((rc = hip_check(ctx, ctx->d_m2.ensure(Nz * D * 8), "alloc m2"))) return rc;
-    if ((rc = hip_check(ctx, ctx->d_hm_m.ensure(Nz * 8), "alloc hm"))) return rc;
-    if ((rc = hip_check(ctx, ctx->d_hm_s.ensure(Nz * 8), "alloc hm"))) return rc;
+    if ((rc = hip_check(ctx, ctx->d_hm_m.ensure(8 * Nz * 8), "alloc hm"))) return rc;
+    if ((rc = hip_check(ctx, ctx->d_hm_s.ensure(8 * Nz * 8), "alloc hm"))) return rc;
     if (!append) {
       if ((rc = hip_check(ctx, hipMemsetAsync(ctx->d_mean.p, 0, Nz * D * 8, ctx->stream), "zero"))) return rc;
       if ((rc = hip_check(ctx, hipMemsetAsync(ctx->d_m2.p, 0, Nz * D * 8, ctx->stream), "zero"))) return rc;
+      // harmonic-mean class partials: s == 0 marks an empty class
+      if ((rc = hip_check(ctx, hipMemsetAsync(ctx->d_hm_s.p, 0, 8 * Nz * 8, ctx->stream), "zero"))) return rc;
     }
   }
   MhArgs a = base_args(ctx);

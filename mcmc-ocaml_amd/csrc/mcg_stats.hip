@@ -49,10 +49,23 @@ __global__ void __launch_bounds__(256) tile_stats_kernel(const TileArgs a) {
     }
     __syncthreads();
   }
-  // harmonic-mean partials
+  // harmonic-mean partials: the chain's 8 record classes in the canonical tree
+  // ((0,4),(2,6)),((1,5),(3,7)) (oracle.c hm_classes), then the tile tree
+  double hm = -__builtin_inf(), hs = 0.0;
+  if (valid) {
+    double cm[8], cs[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { cm[k] = a.hm_m[(int64_t)k * a.N + c]; cs[k] = a.hm_s[(int64_t)k * a.N + c]; }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) hm_comb(cm[k], cs[k], cm[k + 4], cs[k + 4]);
+    hm_comb(cm[0], cs[0], cm[2], cs[2]);
+    hm_comb(cm[1], cs[1], cm[3], cs[3]);
+    hm_comb(cm[0], cs[0], cm[1], cs[1]);
+    hm = cm[0]; hs = cs[0];
+  }
   sn[t] = valid ? 1.0 : 0.0;
-  sm[t] = valid ? a.hm_m[c] : -__builtin_inf();
-  s2[t] = valid ? a.hm_s[c] : 0.0;
+  sm[t] = hm;
+  s2[t] = hs;
   __syncthreads();
   for (int s = 128; s >= 1; s >>= 1) {
     if (t < s) {

@@ -522,6 +522,33 @@ typedef struct {
   int64_t i0, i1; int status;
 } mh_job;
 
+/* log-space harmonic-mean partial (m, s) = (max v, sum exp(v - max)) of v = -ll
+   (evidence.ml:101-107 in log space); s == 0 marks an empty partial. */
+static void hm_update(double* m, double* s, double v) {
+  if (*s == 0.0) { *m = v; *s = 1.0; return; }
+  double e = (v == *m) ? 1.0 : or_exp(-fabs(v - *m));
+  if (v > *m) { *s = *s * e + 1.0; *m = v; } else { *s = *s + e; }
+}
+
+static void hm_comb(double* ma, double* sa, double mb, double sb) {
+  if (sb == 0.0) return;
+  if (*sa == 0.0) { *ma = mb; *sa = sb; return; }
+  double mm = (*ma > mb) ? *ma : mb;
+  *sa = *sa * or_exp(*ma - mm) + sb * or_exp(mb - mm);
+  *ma = mm;
+}
+
+/* the 8 record classes of one chain in the canonical tree ((0,4),(2,6)),((1,5),(3,7)) */
+static void hm_classes(const or_accum* acc, int64_t N, int64_t c, double* m, double* s) {
+  double cm[8], cs[8];
+  for (int k = 0; k < 8; ++k) { cm[k] = acc->hm_m[k * N + c]; cs[k] = acc->hm_s[k * N + c]; }
+  for (int k = 0; k < 4; ++k) hm_comb(&cm[k], &cs[k], cm[k + 4], cs[k + 4]);
+  hm_comb(&cm[0], &cs[0], cm[2], cs[2]);
+  hm_comb(&cm[1], &cs[1], cm[3], cs[3]);
+  hm_comb(&cm[0], &cs[0], cm[1], cs[1]);
+  *m = cm[0]; *s = cs[0];
+}
+
 static void record_sample(mh_job* j, int64_t i, int64_t r, const chain_t* c) {
   const or_run_opts* o = j->o;
   int D = j->p->D;
@@ -542,14 +569,9 @@ static void record_sample(mh_job* j, int64_t i, int64_t r, const chain_t* c) {
       *mean = fma(delta, inv, *mean);
       *m2 = fma(delta, c->x[d] - *mean, *m2);
     }
-    double v = -c->ll;
-    if (r == 0) { a->hm_m[i] = v; a->hm_s[i] = 1.0; }
-    else {
-      double m = a->hm_m[i], s = a->hm_s[i];
-      double e = (v == m) ? 1.0 : or_exp(-fabs(v - m));
-      if (v > m) { s = s * e + 1.0; m = v; } else { s = s + e; }
-      a->hm_m[i] = m; a->hm_s[i] = s;
-    }
+    /* harmonic-mean partials in 8 record classes: record r updates class r & 7 */
+    int64_t hc = (int64_t)(r & 7) * N + i;
+    hm_update(&a->hm_m[hc], &a->hm_s[hc], -c->ll);
   }
 }
 
@@ -659,8 +681,7 @@ void or_tile_stats(int D, int64_t N, int64_t nrec, const or_accum* acc, double* 
           ei[1 + d] = acc->mean[(int64_t)d * N + c];
           ei[1 + D + d] = acc->m2[(int64_t)d * N + c];
         }
-        ei[2 * D + 1] = acc->hm_m[c];
-        ei[2 * D + 2] = acc->hm_s[c];
+        hm_classes(acc, N, c, &ei[2 * D + 1], &ei[2 * D + 2]);
       } else {
         memset(ei, 0, sizeof(double) * (size_t)W);
         ei[2 * D + 1] = -INFINITY;

@@ -74,7 +74,8 @@ typedef struct {
 } or_run_opts;
 
 typedef struct {
-  /* per-chain accumulators over recorded samples ([D][N] SoA for mean/m2) */
+  /* per-chain accumulators over recorded samples: mean/m2 [D][N] (Welford), hm_m/hm_s [8][N]
+     log-space harmonic-mean partials of the 8 record classes r & 7 (s == 0: empty) */
   double* mean; double* m2; double* hm_m; double* hm_s;
 } or_accum;
 

@@ -225,7 +225,7 @@ def mh_run(model, seed, x, ll, lp, nbin=0, nskip=1, n_rec=1, record_x=True, reco
     rec_ll = np.zeros((n_rec, N)) if record_llp else None
     rec_lp = np.zeros((n_rec, N)) if record_llp else None
     bits = np.zeros((max(nsteps, 1), (N + 63) // 64), np.uint64) if record_accept else None
-    mean = np.zeros((D, N)); m2 = np.zeros((D, N)); hm_m = np.zeros(N); hm_s = np.zeros(N)
+    mean = np.zeros((D, N)); m2 = np.zeros((D, N)); hm_m = np.zeros((8, N)); hm_s = np.zeros((8, N))
     acc = OrAccum(dptr(mean), dptr(m2), dptr(hm_m), dptr(hm_s))
     o = OrRunOpts(nbin, nskip, n_rec, int(record_x), int(record_llp), int(record_accept),
                   int(accumulate))

