@@ -38,6 +38,7 @@ struct MhArgs {
   const double* kd_box;    // [nleaves][2][D]
   const double* kd_pts;    // [M][D]
   const double* kd_root;   // [2][D]
+  const int32_t* kd_pt_leaf;  // [M] leaf of each training point
   int64_t kd_M;
   int64_t N;
   int64_t bits_row_bytes;

@@ -108,6 +108,19 @@ int kd_build(mcg_ctx* ctx, const double* pts, int64_t M, int D, const double* lo
   k.pts.assign(pts, pts + M * D);
   k.root.assign(low, low + D);
   k.root.insert(k.root.end(), high, high + D);
+  // leaf of every training point (Interpolate_pdf.draw's find_cell of the picked point,
+  // interpolate_pdf.ml:114-119) -- the same descent as kd_find_leaf on the device
+  k.pt_leaf.assign((size_t)M, 0);
+  for (int64_t i = 0; i < M; ++i) {
+    bool inside = true;
+    for (int d = 0; d < D; ++d) inside = inside && pts[i * D + d] >= low[d] && pts[i * D + d] <= high[d];
+    int32_t node = 0;
+    while (k.nodes[(size_t)node].dim >= 0) {
+      const KdNode& nd = k.nodes[(size_t)node];
+      node = (inside && pts[i * D + nd.dim] <= nd.split) ? node + 1 : nd.right;
+    }
+    k.pt_leaf[(size_t)i] = -1 - k.nodes[(size_t)node].dim;
+  }
   int rc;
   auto up = [&](DevBuf& d, const void* h, size_t bytes) {
     int r = hip_check(ctx, d.ensure(bytes), "alloc kd");
@@ -119,6 +132,7 @@ int kd_build(mcg_ctx* ctx, const double* pts, int64_t M, int D, const double* lo
   if ((rc = up(k.d_box, k.box.data(), k.box.size() * 8))) return rc;
   if ((rc = up(k.d_pts, k.pts.data(), k.pts.size() * 8))) return rc;
   if ((rc = up(k.d_root, k.root.data(), k.root.size() * 8))) return rc;
+  if ((rc = up(k.d_pt_leaf, k.pt_leaf.data(), k.pt_leaf.size() * 4))) return rc;
   k.built = true;
   return MCG_OK;
 }

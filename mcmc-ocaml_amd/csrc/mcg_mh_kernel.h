@@ -447,18 +447,24 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
         // Interpolate_pdf.draw (interpolate_pdf.ml:114-119)
         const u32x4 w = rng(gid, tlo, CALL_KD_PICK, TAG_MH, thi);
         const uint32_t pick = randint(w.x, w.y, (uint32_t)a.kd_M);
-        double pt[D];
-#pragma unroll
-        for (int d = 0; d < D; ++d) pt[d] = a.kd_pts[(int64_t)pick * D + d];
-        const int leaf = kd_find_leaf<D>(a.kd_nodes, a.kd_root, pt);
+        const int leaf = a.kd_pt_leaf[pick];            // find_cell of the picked point
         const double* __restrict__ bx = a.kd_box + (int64_t)leaf * 2 * D;
+        bool strict = true;
 #pragma unroll
         for (int d = 0; d < D; d += 2) {
           const u32x4 v = rng(gid, tlo, (uint32_t)(d >> 1), TAG_MH, thi);
           y[d] = bx[d] + (bx[D + d] - bx[d]) * u53(v.x, v.y);
-          if (d + 1 < D) y[d + 1] = bx[d + 1] + (bx[D + d + 1] - bx[d + 1]) * u53(v.z, v.w);
+          strict = strict && (y[d] > bx[d]) && (y[d] < bx[D + d]);
+          if (d + 1 < D) {
+            y[d + 1] = bx[d + 1] + (bx[D + d + 1] - bx[d + 1]) * u53(v.z, v.w);
+            strict = strict && (y[d + 1] > bx[d + 1]) && (y[d + 1] < bx[D + d + 1]);
+          }
         }
-        lqy = a.kd_logq[kd_find_leaf<D>(a.kd_nodes, a.kd_root, y)];
+        // a point strictly inside a leaf box descends to that leaf (boxes nest and each split
+        // plane is a box face); only a draw rounded onto a face needs the descent
+        int ly = leaf;
+        if (!strict) ly = kd_find_leaf<D>(a.kd_nodes, a.kd_root, y);
+        lqy = a.kd_logq[ly];
         lf = lqy;   // log_jump_prob start proposed = log q(proposed)
         lb = lq;    // log_jump_prob proposed start = log q(start)
       }

@@ -385,6 +385,7 @@ MhArgs base_args(mcg_ctx* ctx) {
   a.kd_box = (const double*)ctx->kd.d_box.p;
   a.kd_pts = (const double*)ctx->kd.d_pts.p;
   a.kd_root = (const double*)ctx->kd.d_root.p;
+  a.kd_pt_leaf = (const int32_t*)ctx->kd.d_pt_leaf.p;
   a.kd_M = ctx->kd.M;
   return a;
 }

@@ -29,8 +29,8 @@ struct KdState {
   int64_t nnodes = 0, nleaves = 0;
   std::vector<KdNode> nodes;
   std::vector<double> logq, box, pts, root;
-  std::vector<int32_t> count;
-  DevBuf d_nodes, d_logq, d_box, d_pts, d_root;
+  std::vector<int32_t> count, pt_leaf;
+  DevBuf d_nodes, d_logq, d_box, d_pts, d_root, d_pt_leaf;
 };
 
 struct NestedState {
