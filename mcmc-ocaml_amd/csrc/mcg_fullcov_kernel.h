@@ -1,0 +1,277 @@
+// mcg_fullcov_kernel.h -- batched MH step for the full-covariance Gaussian (BASELINE C5) with the
+// quadratic form on the matrix cores.
+//
+// Same step as mh_kernel (mcmc.ml:37-56 driven by mcmc.ml:58-72), specialised for
+// LIK = FULLCOV_GAUSS, PROP = GAUSS and D in {16, 32, 48, 64}:
+//   * one wave = 16 chains x 4 lane quadrants; lane (n, q) = lane n + 16 q owns the dims
+//     4 kb + q (kb = 0 .. D/4-1) of chain n -- exactly the B-operand layout of
+//     v_mfma_f64_16x16x4_f64, so the proposal's residuals r = y - mu feed the matrix core with
+//     no data movement;
+//   * e = U r (U = upper Cholesky factor of the precision) is a (D x D) x (D x 16 chains) product:
+//     row block ib (16 rows) x column block kb (4 columns) per MFMA, blocks below the diagonal
+//     skipped (kb >= 4 ib), U's fragments staged in LDS in lane order (conflict-free reads);
+//     the MFMA accumulates in k order with an fma per term (measured bit-exact against an fma
+//     chain, scripts/probes), so e_i is the fma chain over j of the oracle (oracle.c);
+//   * the MFMA output holds rows 16 ib + 4 ri + q in lane quadrant q, i.e. the same rows the lane
+//     owns dims of; S = sum e_i^2 uses FULLCOV's canonical accumulator k(i) = (i & 3) |
+//     ((i >> 4) & 1) << 2, which keeps every accumulator inside one lane;
+//   * Philox call c still yields dims 4c .. 4c+3 (spec v4): lane q draws calls 4 m + q and a
+//     4 x 4 transpose across the lane quadrants (v_permlane32_swap + v_permlane16_swap, gfx950)
+//     hands every lane its dims.
+#pragma once
+#include "mcg_mh_kernel.h"
+
+namespace mcg {
+
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+template <int D>
+struct FcLayout {
+  static_assert(D % 16 == 0 && D >= 16 && D <= 64, "MFMA full-covariance path: D in {16,32,48,64}");
+  static constexpr int NKB = D / 4;      // column blocks of 4 = dims per lane
+  static constexpr int NIB = D / 16;     // row blocks of 16
+  static constexpr int NM = D / 16;      // Philox calls per lane (calls 4 m + q)
+  static constexpr int frag(int ib, int kb) {
+    int f = 0;
+    for (int i = 0; i < ib; ++i) f += NKB - 4 * i;
+    return f + (kb - 4 * ib);
+  }
+  static constexpr int NFRAG = frag(NIB, 4 * NIB);
+};
+
+// 4 x 4 transpose across the lane quadrants: on entry v[k] in quadrant q is M[q][k], on exit it
+// is M[k][q].  Stage 1 swaps the upper half of v[0..1] with the lower half of v[2..3]; stage 2
+// swaps the odd 16-lane rows of v[0], v[2] with the even rows of v[1], v[3].
+__device__ __forceinline__ void swap32(double& a, double& b) {
+  auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(a), __double2loint(b), false, false);
+  auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(a), __double2hiint(b), false, false);
+  a = __hiloint2double((int)hi[0], (int)lo[0]);
+  b = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+__device__ __forceinline__ void swap16(double& a, double& b) {
+  auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(a), __double2loint(b), false, false);
+  auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(a), __double2hiint(b), false, false);
+  a = __hiloint2double((int)hi[0], (int)lo[0]);
+  b = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+__device__ __forceinline__ void transpose_quadrants(double* v) {
+  swap32(v[0], v[2]);
+  swap32(v[1], v[3]);
+  swap16(v[0], v[1]);
+  swap16(v[2], v[3]);
+}
+
+template <int D>
+__global__ void __launch_bounds__(256) mh_fullcov_kernel(const MhArgs a) {
+  using F = FcLayout<D>;
+  constexpr int NL = F::NKB;
+  __shared__ double2 s_lt[kLogTabN];
+  __shared__ double2 s_at[kAngTabN];
+  __shared__ double s_u[F::NFRAG * 64];
+  for (int i = threadIdx.x; i < kLogTabN; i += blockDim.x) s_lt[i] = kLogTab[i];
+  for (int i = threadIdx.x; i < kAngTabN; i += blockDim.x) s_at[i] = kAngTab[i];
+  {
+    // U fragments in lane order: frag (ib, kb), lane l -> U[16 ib + (l & 15)][4 kb + (l >> 4)],
+    // zero below the diagonal (the oracle's chains start at j = i)
+    const double* __restrict__ U = a.lik + D + 1;
+    for (int e = threadIdx.x; e < F::NFRAG * 64; e += blockDim.x) {
+      const int f = e >> 6, l = e & 63;
+      int ib = 0, rem = f;
+      while (rem >= F::NKB - 4 * ib) { rem -= F::NKB - 4 * ib; ++ib; }
+      const int row = 16 * ib + (l & 15), col = 4 * (4 * ib + rem) + (l >> 4);
+      s_u[e] = col >= row ? U[row * D + col] : 0.0;
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int q = lane >> 4;                                // lane quadrant = sub
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t chain = wave * 16 + (lane & 15);
+  const bool active = chain < a.N;
+  const int64_t c = active ? chain : 0;
+  const int64_t N = a.N;
+  const Rng rng{a.k0, a.k1};
+  const uint32_t gid = a.chain_offset + (uint32_t)c;
+  auto dim = [&](int kb) { return 4 * kb + q; };
+
+  double x[NL], y[NL];
+#pragma unroll
+  for (int kb = 0; kb < NL; ++kb) x[kb] = a.x[(int64_t)dim(kb) * N + c];
+  double ll = a.ll[c], lp = a.lp[c];
+  unsigned long long na = 0;
+
+  const bool accum = (a.flags & RUNF_ACCUMULATE) != 0;
+  constexpr int P = 4, NH = 2;
+  double hcm[NH], hcs[NH];
+  double hm_pv = 0.0;
+  bool hm_pok = false;
+  double rmean[NL], rm2[NL];
+  if (accum) {
+#pragma unroll
+    for (int kb = 0; kb < NL; ++kb) {
+      rmean[kb] = a.mean[(int64_t)dim(kb) * N + c];
+      rm2[kb] = a.m2[(int64_t)dim(kb) * N + c];
+    }
+#pragma unroll
+    for (int l = 0; l < NH; ++l) {
+      hcm[l] = a.hm_m[(int64_t)(q + P * l) * N + c];
+      hcs[l] = a.hm_s[(int64_t)(q + P * l) * N + c];
+    }
+  }
+  auto hm_flush = [&](int64_t R0) {
+    const int li = (int)((R0 & 7) / P);
+    if (hm_pok) {
+#pragma unroll
+      for (int l = 0; l < NH; ++l)
+        if (l == li) hm_update(hcm[l], hcs[l], hm_pv);
+    }
+    hm_pok = false;
+  };
+
+  int64_t next_rec = a.next_rec, r = a.next_r;
+  auto record = [&](int64_t R) {
+    const int64_t s = R - a.rec_base;
+    if ((a.flags & RUNF_RECORD_X) && active) {
+#pragma unroll
+      for (int kb = 0; kb < NL; ++kb) a.rec_x[(s * D + dim(kb)) * N + c] = x[kb];
+    }
+    if ((a.flags & RUNF_RECORD_LLP) && active && q == 0) {
+      a.rec_ll[s * N + c] = ll;
+      a.rec_lp[s * N + c] = lp;
+    }
+    if (accum) {
+      const double inv = a.inv_n[R - a.next_r0];
+#pragma unroll
+      for (int kb = 0; kb < NL; ++kb) {
+        const double delta = x[kb] - rmean[kb];
+        const double mnew = fma(delta, inv, rmean[kb]);
+        rm2[kb] = fma(delta, x[kb] - mnew, rm2[kb]);
+        rmean[kb] = mnew;
+      }
+      const int jr = (int)(R & (P - 1));
+      if (q == jr) {
+        hm_pv = -ll;
+        hm_pok = true;
+      }
+      if (jr == P - 1) hm_flush(R - (P - 1));
+    }
+  };
+  if (a.flags & RUNF_RECORD_INITIAL) {
+    record(r);
+    ++r;
+  }
+
+  double lu_own = 0.0;
+  for (int64_t t = 0; t < a.nsteps; ++t) {
+    const uint64_t T = a.step_base + (uint64_t)t;
+    const uint32_t tlo = (uint32_t)T, thi = (uint32_t)(T >> 32);
+    const double* qlik = a.lik;
+    const double* qpri = a.pri;
+    const double* qprop = a.prop;
+    asm volatile("" : "+s"(qlik), "+s"(qpri), "+s"(qprop));
+    // ---- proposal: y = x + s z (mcmc.ml:41); calls 4m + q, transposed to the lane's dims ----
+    int inb = 1;
+#pragma unroll
+    for (int m = 0; m < F::NM; ++m) {
+      asm volatile("" ::: "memory");
+      const u32x4 w = rng(gid, tlo, (uint32_t)(4 * m + q), TAG_MH, thi);
+      double v[4];
+      normal_pair(w.x, w.y, v[0], v[1], s_lt, s_at);
+      normal_pair(w.z, w.w, v[2], v[3], s_lt, s_at);
+      transpose_quadrants(v);                 // v[k'] = z[16 m + 4 k' + q]
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2) {
+        const int kb = 4 * m + k2;
+        const int d = dim(kb);
+        const double yv = fma(qprop[d], v[k2], x[kb]);
+        y[kb] = yv;
+        inb &= (int)(yv >= qpri[d]) & (int)(yv <= qpri[D + d]);
+      }
+    }
+    // ---- log-likelihood: e = U (y - mu) on the matrix cores, S = sum e_i^2 ----
+    double A0 = 0.0, A1 = 0.0;     // accumulators k = q (even ib) and k = q + 4 (odd ib)
+#pragma unroll
+    for (int ib = 0; ib < F::NIB; ++ib) {
+      asm volatile("" ::: "memory");        // keep one row block's fragment reads in flight
+      dbl4 e = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kb = 4 * ib; kb < F::NKB; ++kb) {
+        const double rv = y[kb] - qlik[dim(kb)];
+        e = __builtin_amdgcn_mfma_f64_16x16x4f64(s_u[F::frag(ib, kb) * 64 + lane], rv, e, 0, 0, 0);
+      }
+#pragma unroll
+      for (int ri = 0; ri < 4; ++ri) {
+        if (ib & 1) A1 = fma(e[ri], e[ri], A1);
+        else A0 = fma(e[ri], e[ri], A0);
+      }
+    }
+    const double b = A0 + A1;
+    const double cs = b + __shfl_xor(b, 32, 64);
+    const double S = cs + __shfl_xor(cs, 16, 64);
+    const double lly = qlik[D] - 0.5 * S;
+    inb &= __shfl_xor(inb, 32, 64);
+    inb &= __shfl_xor(inb, 16, 64);
+    const double lpy = a.prior_kind == MCG_PRIOR_FLAT ? 0.0 : (inb ? qpri[2 * D] : -__builtin_inf());
+    // ---- Hastings ratio and accept test (mcmc.ml:42-56); staggered accept uniforms ----
+    const double ratio = (lly + lpy) - (ll + lp);
+    const int qq = (int)(t & (P - 1));
+    if (qq == 0) {
+      const uint64_t Tj = T + (uint64_t)q;
+      const u32x4 wa = rng(gid, (uint32_t)Tj, CALL_ACCEPT, TAG_MH, (uint32_t)(Tj >> 32));
+      lu_own = plog(u53(wa.x, wa.y), s_lt);
+    }
+    const double lu = __shfl(lu_own, (lane & 15) | (qq << 4), 64);
+    const bool acc = lu < ratio;
+    if (acc) {
+#pragma unroll
+      for (int kb = 0; kb < NL; ++kb) x[kb] = y[kb];
+      ll = lly;
+      lp = lpy;
+      ++na;
+    }
+    if (a.flags & RUNF_RECORD_ACCEPT) {
+      const uint64_t mb = (uint64_t)__ballot(acc && active) & 0xFFFFull;   // quadrant 0 = chains
+      if (lane == 0 && wave * 16 < N) {
+        uint8_t* row = a.bits + (a.t0 + t) * a.bits_row_bytes;
+        *(uint16_t*)(row + wave * 2) = (uint16_t)mb;
+      }
+    }
+    const int64_t tt1 = a.t0 + t + 1;
+    if (tt1 == next_rec && r < a.rec_end) {
+      record(r);
+      ++r;
+      next_rec += a.nskip;
+    }
+  }
+
+  if (!active) return;
+#pragma unroll
+  for (int kb = 0; kb < NL; ++kb) a.x[(int64_t)dim(kb) * N + c] = x[kb];
+  if (q == 0) {
+    a.ll[c] = ll;
+    a.lp[c] = lp;
+    a.nacc[c] += na;
+  }
+  if (accum) {
+#pragma unroll
+    for (int kb = 0; kb < NL; ++kb) {
+      a.mean[(int64_t)dim(kb) * N + c] = rmean[kb];
+      a.m2[(int64_t)dim(kb) * N + c] = rm2[kb];
+    }
+    hm_flush((r - 1) & ~(int64_t)(P - 1));
+#pragma unroll
+    for (int l = 0; l < NH; ++l) {
+      a.hm_m[(int64_t)(q + P * l) * N + c] = hcm[l];
+      a.hm_s[(int64_t)(q + P * l) * N + c] = hcs[l];
+    }
+  }
+}
+
+template <int D>
+hipError_t launch_mh_fullcov(const MhArgs& a, int64_t nthreads, hipStream_t s) {
+  const int64_t grid = (nthreads + 255) / 256;          // nthreads = 4 N: 64 chains per block
+  hipLaunchKernelGGL((mh_fullcov_kernel<D>), dim3((unsigned)grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace mcg

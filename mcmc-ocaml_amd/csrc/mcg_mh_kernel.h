@@ -165,7 +165,8 @@ __device__ __forceinline__ double eval_lik(const double* y, int sub, const MhArg
       double t = 0.0;
 #pragma unroll
       for (int j = i; j < D; ++j) t = fma(U[i * D + j], r[j], t);
-      A[(i >> 2) & 7] = fma(t, t, A[(i >> 2) & 7]);
+      const int k = (i & 3) | (((i >> 4) & 1) << 2);   // FULLCOV accumulator (mcg_fullcov_kernel.h)
+      A[k] = fma(t, t, A[k]);
     }
     return q[D] - 0.5 * canon8(A);
   } else {

@@ -399,11 +399,15 @@ int choose_lanes(mcg_ctx* ctx) {
   const char* env = std::getenv("MCG_LANES_PER_CHAIN");
   int want = ctx->opts.lanes_per_chain;
   if (env && *env) want = std::atoi(env);
+  // full covariance, Gaussian proposal, D in {16,32,48,64}: the matrix-core kernel (4 lanes/chain)
+  const bool fullcov_mfma = ctx->lik_kind == MCG_LIK_FULLCOV_GAUSS && ctx->prop_kind == MCG_PROP_GAUSS &&
+                            find_mh_kernel(D, 4, ctx->lik_kind, ctx->prop_kind) != nullptr;
   if (want > 0) {
     if (want == 1) return 1;
-    if (separable && D % (4 * want) == 0 && find_mh_kernel(D, want, ctx->lik_kind, ctx->prop_kind)) return want;
+    if ((separable || fullcov_mfma) && D % (4 * want) == 0 && find_mh_kernel(D, want, ctx->lik_kind, ctx->prop_kind)) return want;
     return 1;
   }
+  if (fullcov_mfma) return 4;
   if (!separable) return 1;
   const int64_t lanes_target = (int64_t)std::max(ctx->num_cus, 1) * 4 * 4 * 64;  // 4 waves/SIMD
   int best = 1;

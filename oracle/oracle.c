@@ -361,7 +361,10 @@ static double lik_eval(const prep_t* p, const double* x) {
       for (int i = 0; i < D; ++i) {
         double t = 0.0;
         for (int j = i; j < D; ++j) t = fma(p->U[i * D + j], r[j], t);
-        A[(i >> 2) & 7] = fma(t, t, A[(i >> 2) & 7]);
+        /* FULLCOV accumulator of row i: (i & 3) | ((i >> 4) & 1) << 2 -- the rows a lane
+           quadrant of the MFMA output holds (csrc/mcg_fullcov_kernel.h) */
+        int k = (i & 3) | (((i >> 4) & 1) << 2);
+        A[k] = fma(t, t, A[k]);
       }
       return p->C - 0.5 * canon8(A);
     }

@@ -117,6 +117,26 @@ def test_fullcov_bit_exact(oracle, T, D):
     assert_same(g, o)
 
 
+@pytest.mark.parametrize("D", [16, 32, 48, 64])
+def test_fullcov_matrix_core_bit_exact(oracle, T, D):
+    """C5 path: the MFMA full-covariance kernel (4 lanes per chain, mcg_fullcov_kernel.h) and the
+    one-lane VALU kernel both reproduce the oracle bit for bit (100 chains: a partial wave)."""
+    rng = np.random.default_rng(100 + D)
+    Q, _ = np.linalg.qr(rng.normal(size=(D, D)))
+    lam = np.exp(rng.uniform(math.log(0.1), math.log(10.0), D))
+    cov = (Q * lam) @ Q.T
+    cov = 0.5 * (cov + cov.T)
+    mu = rng.uniform(-1, 1, D)
+    lik = T.fullcov_gauss(mu, cov)
+    pri = T.box(-30 * np.ones(D), 30 * np.ones(D))
+    prop = T.gauss(2.38 / math.sqrt(D) * math.sqrt(lam.min()))
+    x0 = mu[:, None] + np.linalg.cholesky(cov) @ rng.normal(size=(D, 100))
+    o = run_oracle(oracle, lik, pri, prop, x0, 9, 3, 2, 40)
+    for lanes in (4, 1):
+        g = run_gpu(lik, pri, prop, x0, 9, nbin=3, nskip=2, n_rec=40, lanes=lanes)
+        assert_same(g, o)
+
+
 @pytest.mark.parametrize("cauchy", [False, True])
 def test_gaussian_cauchy_c1_bit_exact(oracle, T, cauchy):
     """C1: bin/gaussian_cauchy.ml data likelihoods, wrapping-uniform proposal
