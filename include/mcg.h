@@ -197,6 +197,21 @@ int mcg_nested_get(mcg_ctx* ctx, double* pts, double* ll, double* lp, double* lo
 /* Nested.log_total_error_estimate (nested.ml:148-150) */
 double mcg_log_total_error_estimate(double log_ev, double log_dev, int64_t nlive);
 
+/* ---- nested replicas: merge independent runs into one (multi-GPU C3) ----
+   Each of nruns independent runs (one per GPU) gives its points in nested_output order (dead in
+   retirement order, then the final live points ascending; nested.ml:143), concatenated run
+   after run in ll.  Run r retired its i-th dead point with nlive[r] - (i mod k[r]) live points
+   and its j-th final live point with nlive[r] - j (the final live points retired one by one).
+   The merged run visits every point in ascending ll (ties: run, then index) with the live
+   count n_p = the sum over runs of each run's count at level ll_p; volumes shrink by
+   log1p(-1/n_p) and the trapezoid rule of evidence_error_and_weights (nested.ml:81-120) gives
+   log Z, log dZ and the log weights.  order[p] = index into the concatenation of the p-th
+   merged point; log_wts is in merged order.  With equal runs of nlive/R points this is one run
+   of nlive points. */
+int mcg_nested_merge(int32_t nruns, const int64_t* n_total, const int64_t* nlive, const int64_t* k,
+                     const double* ll, int64_t* order, double* log_ev, double* log_dev,
+                     double* log_wts);
+
 /* ---- device timing of the dominant kernel (HIP events on the launch stream) ---- */
 typedef struct {
   int64_t launches;

@@ -294,6 +294,57 @@ int mcg_nested_get(mcg_ctx* ctx, double* pts, double* ll, double* lp, double* lo
   return MCG_OK;
 }
 
+// Run merging for nested replicas (one independent run per GPU).  A run with
+// constant live count n is n "threads"; merging runs adds their live counts at every likelihood
+// level, so R runs of n/R points each merge into one run of n points.  The volume and trapezoid
+// algebra is that of evidence_error_and_weights (nested.ml:81-120) with a per-point live count.
+int mcg_nested_merge(int32_t nruns, const int64_t* n_total, const int64_t* nlive, const int64_t* k,
+                     const double* ll, int64_t* order, double* log_ev, double* log_dev,
+                     double* log_wts) {
+  if (nruns <= 0 || !n_total || !nlive || !k || !ll || !order || !log_ev || !log_dev || !log_wts)
+    return MCG_EINVAL;
+  std::vector<int64_t> base((size_t)nruns + 1, 0);
+  for (int r = 0; r < nruns; ++r) {
+    if (nlive[r] <= 0 || k[r] <= 0 || k[r] > nlive[r] || n_total[r] < nlive[r]) return MCG_EINVAL;
+    base[(size_t)r + 1] = base[(size_t)r] + n_total[r];
+  }
+  const int64_t n = base[(size_t)nruns];
+  // live count of run r's point i
+  auto count = [&](int r, int64_t i) -> int64_t {
+    const int64_t ndead = n_total[r] - nlive[r];
+    return i < ndead ? nlive[r] - i % k[r] : nlive[r] - (i - ndead);
+  };
+  for (int64_t p = 0; p < n; ++p) order[p] = p;
+  // ascending ll; ties by concatenation index (= run, then position in the run)
+  std::stable_sort(order, order + n, [&](int64_t a, int64_t b) { return ll[a] < ll[b]; });
+  // pos[r] = first index of run r with ll >= the current level; ll is nondecreasing within a run
+  std::vector<int64_t> pos((size_t)nruns, 0);
+  const double log_half = -0.69314718055994530942;
+  double log_x = 0.0, low = -HUGE_VAL, high = -HUGE_VAL;
+  for (int64_t p = 0; p < n; ++p) log_wts[p] = -HUGE_VAL;
+  for (int64_t p = 0; p < n; ++p) {
+    const double L = ll[order[p]];
+    int64_t np = 0;
+    for (int r = 0; r < nruns; ++r) {
+      int64_t& i = pos[(size_t)r];
+      while (i < n_total[r] && ll[base[(size_t)r] + i] < L) ++i;
+      if (i < n_total[r]) np += count(r, i);
+    }
+    const double log_dv = log_x + std::log(1.0 / (double)np);
+    log_x += std::log1p(-1.0 / (double)np);
+    const int64_t q = p + 1 < n ? p + 1 : p;
+    const double dl = log_dv + L, dh = log_dv + ll[order[q]];
+    low = lse_host(low, dl);
+    high = lse_host(high, dh);
+    log_wts[p] = lse_host(log_wts[p], log_half + dl);
+    log_wts[q] = lse_host(log_wts[q], log_half + dh);
+  }
+  *log_ev = log_half + lse_host(low, high);
+  *log_dev = high + std::log1p(-std::exp(low - high));
+  for (int64_t p = 0; p < n; ++p) log_wts[p] -= *log_ev;
+  return MCG_OK;
+}
+
 }  // extern "C"
 
 void mcg_free_nested_bufs(mcg_nested_bufs_holder* h) { delete h; }

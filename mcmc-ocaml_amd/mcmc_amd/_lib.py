@@ -18,6 +18,7 @@ FLAG_NESTED_FIXED_STOP = 1
 
 _dp = C.POINTER(C.c_double)
 _u64p = C.POINTER(C.c_uint64)
+_i64p = C.POINTER(C.c_int64)
 _i32p = C.POINTER(C.c_int32)
 
 
@@ -78,6 +79,7 @@ SIGNATURES = {
                     C.c_void_p], C.c_int),
     "mcg_nested_get": ([C.c_void_p, _dp, _dp, _dp, _dp], C.c_int),
     "mcg_log_total_error_estimate": ([C.c_double, C.c_double, C.c_int64], C.c_double),
+    "mcg_nested_merge": ([C.c_int32, _i64p, _i64p, _i64p, _dp, _i64p, _dp, _dp, _dp], C.c_int),
     "mcg_get_kernel_timing": ([C.c_void_p, C.c_char_p, C.POINTER(McgKernelTiming)], C.c_int),
     "mcg_set_timing": ([C.c_void_p, C.c_int32], C.c_int),
     "mcg_sync": ([C.c_void_p], C.c_int),
@@ -133,6 +135,10 @@ def dptr(a):
 
 def u64ptr(a):
     return None if a is None else a.ctypes.data_as(_u64p)
+
+
+def i64ptr(a):
+    return None if a is None else a.ctypes.data_as(_i64p)
 
 
 def i32ptr(a):

@@ -45,6 +45,39 @@ class NestedOutput(tuple):
         return t
 
 
+def merge_runs(runs):
+    """Merge independent nested runs (replicas) into one run (include/mcg.h mcg_nested_merge).
+
+    runs = [(output, nlive, k)] with output a nested_output-like tuple carrying .ll/.lp (or a
+    (log_ev, log_dev, pts, log_wts, ll, lp) tuple).  Returns a NestedOutput over the union of the
+    points in ascending ll; n_dead counts every point that is not among the final live points of
+    the merged run's last run."""
+    n_total = np.array([len(_ll(o)) for o, _, _ in runs], np.int64)
+    nlive = np.array([nl for _, nl, _ in runs], np.int64)
+    kk = np.array([k for _, _, k in runs], np.int64)
+    ll = np.ascontiguousarray(np.concatenate([_ll(o) for o, _, _ in runs]), np.float64)
+    lp = np.concatenate([_lp(o) for o, _, _ in runs])
+    pts = np.concatenate([np.asarray(o[2]) for o, _, _ in runs])
+    n = len(ll)
+    order = np.zeros(n, np.int64)
+    w = np.zeros(n)
+    le, ld = C.c_double(), C.c_double()
+    L.check(L.lib().mcg_nested_merge(len(runs), L.i64ptr(n_total), L.i64ptr(nlive), L.i64ptr(kk),
+                                     L.dptr(ll), L.i64ptr(order), C.byref(le), C.byref(ld),
+                                     L.dptr(w)))
+    n_dead = int(n - nlive.sum())
+    n_gen = int(sum(getattr(o, "n_gen", 0) for o, _, _ in runs))
+    return NestedOutput(le.value, ld.value, pts[order], w, ll[order], lp[order], n_dead, n_gen)
+
+
+def _ll(o):
+    return np.asarray(o.ll if hasattr(o, "ll") else o[4], np.float64)
+
+
+def _lp(o):
+    return np.asarray(o.lp if hasattr(o, "lp") else o[5], np.float64)
+
+
 def log_total_error_estimate(log_ev, log_dev, nlive):
     """Nested.log_total_error_estimate (nested.ml:148-150)."""
     return L.lib().mcg_log_total_error_estimate(log_ev, log_dev, nlive)

@@ -10,7 +10,10 @@ number of GPUs.
 """
 import numpy as np
 
-from .context import combine_tiles
+from . import nested as _nested
+from .context import Context, combine_tiles
+
+GOLDEN64 = 0x9E3779B97F4A7C15
 
 
 def allgather_tiles(tiles, device=None, group=None):
@@ -30,3 +33,66 @@ def allgather_tiles(tiles, device=None, group=None):
 def reduce_stats(ndim, tiles, device=None, group=None):
     """Global Stats.multi_mean / multi_std and log Z_HM from this rank's tile partials."""
     return combine_tiles(ndim, allgather_tiles(tiles, device, group))
+
+
+def replica_seed(seed, rank):
+    """Philox key of nested replica `rank`: rank 0 keeps the caller's seed, so a one-GPU run is
+    the single-context run exactly."""
+    return (int(seed) + int(rank) * GOLDEN64) % (1 << 64)
+
+
+def _world(group):
+    import torch.distributed as dist
+    if not dist.is_available() or not dist.is_initialized():
+        return 0, 1
+    return dist.get_rank(group), dist.get_world_size(group)
+
+
+def allgather_runs(output, nlive, k, device=None, group=None):
+    """All-gather every rank's nested run: the point counts first, then the (pts | ll | lp) rows
+    padded to the longest run.  Returns [(output, nlive, k)] in rank order."""
+    rank, world = _world(group)
+    if world == 1:
+        return [(output, nlive, k)]
+    import torch
+    import torch.distributed as dist
+    pts = np.asarray(output[2], np.float64)
+    D = pts.shape[1]
+    rows = np.concatenate([pts, output.ll[:, None], output.lp[:, None]], axis=1)
+    meta = torch.tensor([rows.shape[0], nlive, k, output.n_gen], dtype=torch.int64, device=device)
+    metas = [torch.empty_like(meta) for _ in range(world)]
+    dist.all_gather(metas, meta, group=group)
+    metas = [m.cpu().numpy() for m in metas]
+    cap = int(max(m[0] for m in metas))
+    buf = np.zeros((cap, D + 2))
+    buf[:rows.shape[0]] = rows
+    t = torch.from_numpy(buf).to(device) if device is not None else torch.from_numpy(buf)
+    outs = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(outs, t, group=group)
+    runs = []
+    for m, o in zip(metas, outs):
+        r = o.cpu().numpy()[:int(m[0])]
+        run = _nested.NestedOutput(0.0, 0.0, r[:, :D].copy(), None, r[:, D].copy(), r[:, D + 1].copy(),
+                                   int(m[0] - m[1]), int(m[3]))
+        runs.append((run, int(m[1]), int(m[2])))
+    return runs
+
+
+def nested_evidence_replicas(log_likelihood, log_prior, epsrel=0.01, nmcmc=1000, nlive=1000,
+                             mode_hopping_frac=0.1, k=1, seed=0, device=0, group=None,
+                             comm_device=None):
+    """Nested.nested_evidence (nested.ml:122-146) as one replica per GPU: every
+    rank runs an independent nested run with nlive / world live points on its own Philox key,
+    the runs are all-gathered and merged (mcg_nested_merge) into one run of nlive points.  Every
+    rank returns the same merged NestedOutput."""
+    rank, world = _world(group)
+    if nlive % world:
+        raise ValueError("nlive (%d) must be a multiple of the number of ranks (%d)" % (nlive, world))
+    nl = nlive // world
+    kk = min(k, nl)
+    with Context(seed=replica_seed(seed, rank), device=device) as ctx:
+        out = _nested.nested_evidence(log_likelihood, log_prior, epsrel=epsrel, nmcmc=nmcmc,
+                                      nlive=nl, mode_hopping_frac=mode_hopping_frac, k=kk, ctx=ctx)
+    if world == 1:
+        return out
+    return _nested.merge_runs(allgather_runs(out, nl, kk, comm_device, group))

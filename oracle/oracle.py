@@ -277,3 +277,53 @@ def evidence_weights(ll, nlive, k=1):
     w = np.zeros(n); le = C.c_double(); ld = C.c_double()
     lib().or_evidence_weights(n, nlive, k, dptr(ll), C.byref(le), C.byref(ld), dptr(w))
     return le.value, ld.value, w
+
+
+def _lse(a, b):
+    """Stats.log_sum_logs (stats.ml:240-248)."""
+    if a == -np.inf and b == -np.inf:
+        return -np.inf
+    if b > a:
+        a, b = b, a
+    return a + np.log1p(np.exp(b - a))
+
+
+def nested_merge(runs):
+    """Restatement of run merging for nested replicas: runs = [(ll, nlive, k)],
+    each ll in nested_output order (nested.ml:143).  The live count at each merged point is the
+    sum over runs of the count of the run's first point at or above that level (dead point i:
+    nlive - i mod k; final live point j: nlive - j), and the trapezoid of
+    evidence_error_and_weights (nested.ml:81-120) runs with that per-point count.
+    Returns (order, log_ev, log_dev, log_wts in merged order)."""
+    lls, counts = [], []
+    for ll, nlive, k in runs:
+        ll = np.asarray(ll, np.float64)
+        ndead = len(ll) - nlive
+        i = np.arange(len(ll))
+        counts.append(np.where(i < ndead, nlive - i % k, nlive - (i - ndead)))
+        lls.append(ll)
+    cat = np.concatenate(lls)
+    order = np.argsort(cat, kind="stable")
+    L = cat[order]
+    nps = np.zeros(len(L), np.int64)
+    for ll, c in zip(lls, counts):
+        i = np.searchsorted(ll, L, side="left")
+        ok = i < len(ll)
+        nps[ok] += c[i[ok]]
+    half = -0.69314718055994530942
+    n = len(L)
+    w = np.full(n, -np.inf)
+    low = high = -np.inf
+    log_x = 0.0
+    for p in range(n):
+        log_dv = log_x + np.log(1.0 / nps[p])
+        with np.errstate(divide="ignore"):
+            log_x += np.log1p(-1.0 / nps[p])
+        q = min(p + 1, n - 1)
+        dl, dh = log_dv + L[p], log_dv + L[q]
+        low, high = _lse(low, dl), _lse(high, dh)
+        w[p] = _lse(w[p], half + dl)
+        w[q] = _lse(w[q], half + dh)
+    log_ev = half + _lse(low, high)
+    log_dev = high + np.log1p(-np.exp(low - high))
+    return order, log_ev, log_dev, w - log_ev

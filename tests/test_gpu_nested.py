@@ -145,3 +145,39 @@ def test_c3_shell_batched_reduced_size(T):
     sig = math.sqrt(H / 16384)
     truth = shell_log_z(D, 2.0, 0.1, 6.0)
     assert abs(log_ev - truth) < 3 * sig + 0.02, (log_ev, truth, sig)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [1, 8])
+def test_nested_replicas_merge_bit_exact(oracle, T, k):
+    """SURVEY.md §8e replicas on one GPU: replica r runs on Philox key replica_seed(seed, r); the
+    merged run of two GPU replicas equals the merge of the two oracle runs bit for bit, and a
+    one-rank replica run is the plain run."""
+    from mcmc_amd import nested
+    from mcmc_amd.parallel import nested_evidence_replicas, replica_seed
+    lik, pri = unit_square_gauss(T)
+    gs = [gpu_nested(lik, pri, replica_seed(7, r), nlive=100, nmcmc=20, k=k) for r in range(2)]
+    os_ = [oracle_nested(oracle, lik, pri, replica_seed(7, r), nlive=100, nmcmc=20, k=k) for r in range(2)]
+    for g, o in zip(gs, os_):
+        assert_nested_same(g, o)
+    mg = nested.merge_runs([(g, 100, k) for g in gs])
+    order, le, ld, w = oracle.nested_merge([(o["ll"], 100, k) for o in os_])
+    np.testing.assert_array_equal(mg.ll, np.concatenate([o["ll"] for o in os_])[order])
+    np.testing.assert_allclose(mg[3], w, rtol=1e-12, atol=1e-12)
+    one = nested_evidence_replicas(lik, pri, nlive=100, nmcmc=20, k=k, seed=7)
+    assert_nested_same(one, os_[0])
+
+
+@pytest.mark.gpu
+def test_nested_replicas_unit_evidence(T):
+    """nested_test.ml:23-39 on a merge of 4 GPU replicas of 250 live points (one run of 1000)."""
+    from mcmc_amd import nested
+    from mcmc_amd.parallel import replica_seed
+    lik, pri = unit_square_gauss(T)
+    runs = [(gpu_nested(lik, pri, replica_seed(31, r), nlive=250, nmcmc=100, k=1), 250, 1)
+            for r in range(4)]
+    mg = nested.merge_runs(runs)
+    ev = math.exp(mg[0])
+    err = math.exp(nested.log_total_error_estimate(mg[0], mg[1], 1000))
+    assert abs(ev - 1.0) < 2 * err and err < 0.1
+    assert abs(np.exp(mg[3]).sum() - 1.0) < 1e-8
