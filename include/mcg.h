@@ -71,8 +71,25 @@ enum { MCG_PRIOR_FLAT = 0, MCG_PRIOR_BOX = 1, MCG_PRIOR_OPEN_BOX = 2 };
    WRAP_UNIFORM : lo[D], hi[D], dx[D] Mcmc.uniform_wrapping per dim (mcmc.ml:187-196), symmetric
    KD_INTERP    : set with mcg_set_kd_proposal; independence proposal Interpolate_pdf.draw with
                   log_jump_prob _ y = log (jump_prob y)  (interpolate_pdf.ml:114-142)
-   DE           : used by nested sampling (mcmc.ml:198-218) */
-enum { MCG_PROP_GAUSS = 1, MCG_PROP_WRAP_UNIFORM = 2, MCG_PROP_KD_INTERP = 3, MCG_PROP_DE = 4 };
+   DE           : used by nested sampling (mcmc.ml:198-218)
+   MIXTURE      : Mcmc.combine_jump_proposals [(p_i, jp_i, ljp_i)] (mcmc.ml:165-185):
+                  ncomp, then per component: p, comp_kind, ljp_mode, comp params, where
+                    MCG_MIX_GAUSS         s[D]        y = x + s z, z ~ N(0, 1)
+                    MCG_MIX_SHIFT_UNIFORM a[D], b[D]  y = x + random_between a b per dim
+                                                     (the proposals of test/mcmc_test.ml)
+                    MCG_MIX_WRAP_UNIFORM  lo, hi, dx  Mcmc.uniform_wrapping per dim
+                    MCG_MIX_KD_INTERP     (none)      the context's kD tree (mcg_set_kd_proposal)
+                  ljp_mode 0: the component's log_jump_prob is the constant 0 (what callers pass
+                  for symmetric jumps); 1: its log density (GAUSS, SHIFT_UNIFORM; KD_INTERP is
+                  always its density log q(y)).  Weights are normalised by their sum; the mixture
+                  log_jump_prob folds log p_i + ljp_i with the reference's log(1 + exp) log-sum
+                  (mcmc.ml:155-163).  A KD_INTERP component requires mcg_set_kd_proposal first
+                  (which itself selects the plain KD proposal; set the MIXTURE after it). */
+enum { MCG_PROP_GAUSS = 1, MCG_PROP_WRAP_UNIFORM = 2, MCG_PROP_KD_INTERP = 3, MCG_PROP_DE = 4,
+       MCG_PROP_MIXTURE = 5 };
+enum { MCG_MIX_GAUSS = 1, MCG_MIX_SHIFT_UNIFORM = 2, MCG_MIX_WRAP_UNIFORM = 3,
+       MCG_MIX_KD_INTERP = 4 };
+#define MCG_MIX_MAX_COMPONENTS 8
 
 /* ---- context ---- */
 enum {

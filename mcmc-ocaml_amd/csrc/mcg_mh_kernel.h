@@ -120,6 +120,63 @@ __device__ __forceinline__ double wrap_uniform(double xmin, double xmax, double 
   return nx;
 }
 
+// ---- Mcmc.combine_jump_proposals (mcmc.ml:165-185), device layout from mcg_runtime.cpp
+// pack_mixture: [ncomp], then per component (stride 5 + 3D) p, log p, kind, ljp mode, C, params.
+template <int D>
+struct MixLayout {
+  static constexpr int kStride = 5 + 3 * D;
+  __device__ static __forceinline__ const double* comp(const double* q, int c) { return q + 1 + c * kStride; }
+};
+
+// the reference's private log-sum (mcmc.ml:155-163): log (1 + exp), not log1p
+__device__ __forceinline__ double lse_mix(double la, double lb, const double2* lt) {
+  if (la == -__builtin_inf() && lb == -__builtin_inf()) return -__builtin_inf();
+  if (la > lb) return la + plog(1.0 + pexp(lb - la), lt);
+  return lb + plog(1.0 + pexp(la - lb), lt);
+}
+
+// log_jump_prob of the mixture from `from` to `to`: fold over the components of
+// log p_i + ljp_i from to (mcmc.ml:175-182); lq_to = log q(to) of the kD tree (if any)
+template <int D>
+__device__ __forceinline__ double mix_log_jp(const double* __restrict__ q, const double* from,
+                                             const double* to, double lq_to, const double2* lt) {
+  using M = MixLayout<D>;
+  const int nc = (int)q[0];
+  double acc = -__builtin_inf();
+  for (int c = 0; c < nc; ++c) {
+    const double* m = M::comp(q, c);
+    const int kind = (int)m[2];
+    double lj = 0.0;
+    if (m[3] != 0.0) {
+      if (kind == MCG_MIX_GAUSS) {
+        double S = 0.0;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          const double e = (to[d] - from[d]) * m[5 + D + d];
+          S = fma(e, e, S);
+        }
+        lj = m[4] - 0.5 * S;
+      } else if (kind == MCG_MIX_SHIFT_UNIFORM) {
+        bool in = true;
+#pragma unroll
+        for (int d = 0; d < D; ++d) in = in && (to[d] >= from[d] + m[5 + d]) && (to[d] <= from[d] + m[5 + D + d]);
+        lj = in ? m[4] : -__builtin_inf();
+      } else {
+        lj = lq_to;                                      // KD_INTERP: log jump_prob to
+      }
+    }
+    acc = lse_mix(acc, m[1] + lj, lt);
+  }
+  return acc;
+}
+
+__device__ __forceinline__ bool mix_has_kd(const double* __restrict__ q, int stride) {
+  const int nc = (int)q[0];
+  bool kd = false;
+  for (int c = 0; c < nc; ++c) kd = kd || ((int)q[1 + c * stride + 2] == MCG_MIX_KD_INTERP);
+  return kd;
+}
+
 template <int D, int P, int LIK>
 __device__ __forceinline__ double eval_lik(const double* y, int sub, const MhArgs& a,
                                            const double* __restrict__ q) {
@@ -259,6 +316,11 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
   double ll = a.ll[c], lp = a.lp[c];
   double lq = 0.0;
   if constexpr (PROP == MCG_PROP_KD_INTERP) lq = a.kd_logq[kd_find_leaf<D>(a.kd_nodes, a.kd_root, x)];
+  bool mix_kd = false;
+  if constexpr (PROP == MCG_PROP_MIXTURE) {
+    mix_kd = mix_has_kd(a.prop, MixLayout<D>::kStride);
+    if (mix_kd) lq = a.kd_logq[kd_find_leaf<D>(a.kd_nodes, a.kd_root, x)];
+  }
   unsigned long long na = 0;
 
   const bool accum = (a.flags & RUNF_ACCUMULATE) != 0;
@@ -468,6 +530,70 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
         lqy = a.kd_logq[ly];
         lf = lqy;   // log_jump_prob start proposed = log q(proposed)
         lb = lq;    // log_jump_prob proposed start = log q(start)
+      }
+      else if constexpr (PROP == MCG_PROP_MIXTURE) {
+        static_assert(P == 1, "MIXTURE: one lane per chain");
+        // pick a component: Random.float 1.0 walked down the normalised weights (mcmc.ml:168-173);
+        // a u past the last weight (rounding of the normalised sum) takes the last component
+        using M = MixLayout<D>;
+        const int nc = (int)qprop[0];
+        const u32x4 ws = rng(gid, tlo, CALL_MIX, TAG_MH, thi);
+        double u = u53(ws.x, ws.y);
+        int pick = nc - 1;
+        for (int cc = 0; cc < nc; ++cc) {
+          const double p = M::comp(qprop, cc)[0];
+          if (u < p) { pick = cc; break; }
+          u = u - p;
+        }
+        const double* m = M::comp(qprop, pick);
+        const int kind = (int)m[2];
+        int leaf_y = -1;
+        if (kind == MCG_MIX_GAUSS) {
+#pragma unroll
+          for (int i = 0; i < L::NCL; ++i) {
+            if (4 * i >= D) continue;
+            const u32x4 w = rng(gid, tlo, (uint32_t)i, TAG_MH, thi);
+            double z[4];
+            normal_pair(w.x, w.y, z[0], z[1], s_lt, s_at);
+            normal_pair(w.z, w.w, z[2], z[3], s_lt, s_at);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              if (4 * i + k < D) y[4 * i + k] = fma(m[5 + 4 * i + k], z[k], x[4 * i + k]);
+          }
+        } else if (kind == MCG_MIX_KD_INTERP) {
+          const u32x4 w = rng(gid, tlo, CALL_KD_PICK, TAG_MH, thi);
+          const int leaf = a.kd_pt_leaf[randint(w.x, w.y, (uint32_t)a.kd_M)];
+          const double* __restrict__ bx = a.kd_box + (int64_t)leaf * 2 * D;
+          bool strict = true;
+#pragma unroll
+          for (int d = 0; d < D; d += 2) {
+            const u32x4 v = rng(gid, tlo, (uint32_t)(d >> 1), TAG_MH, thi);
+            y[d] = bx[d] + (bx[D + d] - bx[d]) * u53(v.x, v.y);
+            strict = strict && (y[d] > bx[d]) && (y[d] < bx[D + d]);
+            if (d + 1 < D) {
+              y[d + 1] = bx[d + 1] + (bx[D + d + 1] - bx[d + 1]) * u53(v.z, v.w);
+              strict = strict && (y[d + 1] > bx[d + 1]) && (y[d + 1] < bx[D + d + 1]);
+            }
+          }
+          if (strict) leaf_y = leaf;
+        } else {
+          // SHIFT_UNIFORM: x + random_between a b; WRAP_UNIFORM: Mcmc.uniform_wrapping
+#pragma unroll
+          for (int d = 0; d < D; d += 2) {
+            const u32x4 w = rng(gid, tlo, (uint32_t)(d >> 1), TAG_MH, thi);
+            const double u0 = u53(w.x, w.y), u1 = u53(w.z, w.w);
+            if (kind == MCG_MIX_SHIFT_UNIFORM) {
+              y[d] = x[d] + (m[5 + d] + m[5 + 2 * D + d] * u0);
+              if (d + 1 < D) y[d + 1] = x[d + 1] + (m[5 + d + 1] + m[5 + 2 * D + d + 1] * u1);
+            } else {
+              y[d] = wrap_uniform(m[5 + d], m[5 + D + d], m[5 + 2 * D + d], x[d], u0);
+              if (d + 1 < D) y[d + 1] = wrap_uniform(m[5 + d + 1], m[5 + D + d + 1], m[5 + 2 * D + d + 1], x[d + 1], u1);
+            }
+          }
+        }
+        if (mix_kd) lqy = a.kd_logq[leaf_y >= 0 ? leaf_y : kd_find_leaf<D>(a.kd_nodes, a.kd_root, y)];
+        lf = mix_log_jp<D>(qprop, x, y, lqy, s_lt);   // log_jump_prob start proposed
+        lb = mix_log_jp<D>(qprop, y, x, lq, s_lt);    // log_jump_prob proposed start
       }
       lly = eval_lik<D, P, LIK>(y, sub, a, qlik);
       lpy = eval_prior<D, P>(y, sub, a, qpri);

@@ -110,6 +110,80 @@ void timing_harvest(mcg_ctx* ctx) {
 
 static const double kNegHalfLog2Pi = -0.91893853320467274178;
 
+// Mcmc.combine_jump_proposals (mcmc.ml:165-185) -> device layout (mcg_mh_kernel.h MixLayout):
+// [ncomp] then per component (stride 5 + 3D): p / ptot, log(p / ptot), comp kind, ljp mode,
+// constant C of the component log density, then 3D parameters:
+//   GAUSS: s[D], 1/s[D]  (C = sum_d (-1/2 log 2pi - log s_d))
+//   SHIFT_UNIFORM: a[D], b[D], b - a[D]  (C = -sum_d log(b_d - a_d))
+//   WRAP_UNIFORM: lo[D], hi[D], dx[D]
+static int pack_mixture(mcg_ctx* ctx, const double* params, size_t n, std::vector<double>& dev) {
+  const int D = ctx->D;
+  if (!params || n < 1) return mcg::set_error(ctx, MCG_EINVAL, "MIXTURE: ncomp, components...");
+  const int nc = (int)params[0];
+  if (nc < 1 || nc > MCG_MIX_MAX_COMPONENTS || (double)nc != params[0])
+    return mcg::set_error(ctx, MCG_EINVAL, "MIXTURE: 1 <= ncomp <= %d", MCG_MIX_MAX_COMPONENTS);
+  const size_t stride = 5 + 3 * (size_t)D;
+  dev.assign(1 + nc * stride, 0.0);
+  dev[0] = nc;
+  double ptot = 0.0;
+  size_t o = 1;
+  for (int c = 0; c < nc; ++c) {               // first pass: validate, sum the weights
+    if (o + 3 > n) return mcg::set_error(ctx, MCG_EINVAL, "MIXTURE: component %d truncated", c);
+    const double p = params[o];
+    const int ck = (int)params[o + 1], mode = (int)params[o + 2];
+    size_t np = ck == MCG_MIX_GAUSS ? D : ck == MCG_MIX_SHIFT_UNIFORM ? 2 * D
+              : ck == MCG_MIX_WRAP_UNIFORM ? 3 * D : ck == MCG_MIX_KD_INTERP ? 0 : (size_t)-1;
+    if (np == (size_t)-1) return mcg::set_error(ctx, MCG_EINVAL, "MIXTURE: unknown component kind %d", ck);
+    if (!(p >= 0.0) || (mode != 0 && mode != 1))
+      return mcg::set_error(ctx, MCG_EINVAL, "MIXTURE: component %d needs p >= 0, ljp_mode 0/1", c);
+    if (ck == MCG_MIX_WRAP_UNIFORM && mode == 1)
+      return mcg::set_error(ctx, MCG_EINVAL, "MIXTURE: the wrapping-uniform density is symmetric; use ljp_mode 0");
+    if (ck == MCG_MIX_KD_INTERP && !ctx->kd.built)
+      return mcg::set_error(ctx, MCG_ESTATE, "MIXTURE: KD_INTERP component needs mcg_set_kd_proposal first");
+    if (o + 3 + np > n) return mcg::set_error(ctx, MCG_EINVAL, "MIXTURE: component %d truncated", c);
+    ptot = ptot + p;                            // List.fold_left (+.) 0.0 (mcmc.ml:166)
+    o += 3 + np;
+  }
+  if (o != n) return mcg::set_error(ctx, MCG_EINVAL, "MIXTURE: %zu trailing parameters", n - o);
+  if (!(ptot > 0.0)) return mcg::set_error(ctx, MCG_EINVAL, "MIXTURE: weights sum to zero");
+  o = 1;
+  for (int c = 0; c < nc; ++c) {
+    double* q = &dev[1 + c * stride];
+    const int ck = (int)params[o + 1], mode = (int)params[o + 2];
+    const double* u = params + o + 3;
+    q[0] = params[o] / ptot;                    // mcmc.ml:167
+    q[1] = std::log(q[0]);                      // log p, mcmc.ml:178
+    q[2] = ck;
+    q[3] = ck == MCG_MIX_KD_INTERP ? 1 : mode;
+    double C = 0.0;
+    if (ck == MCG_MIX_GAUSS) {
+      for (int d = 0; d < D; ++d) {
+        if (!(u[d] > 0.0)) return mcg::set_error(ctx, MCG_EINVAL, "MIXTURE: GAUSS scale must be > 0");
+        q[5 + d] = u[d];
+        q[5 + D + d] = 1.0 / u[d];
+        C = C + (kNegHalfLog2Pi - std::log(u[d]));
+      }
+      o += 3 + D;
+    } else if (ck == MCG_MIX_SHIFT_UNIFORM) {
+      for (int d = 0; d < D; ++d) {
+        if (!(u[D + d] > u[d])) return mcg::set_error(ctx, MCG_EINVAL, "MIXTURE: SHIFT_UNIFORM needs a < b");
+        q[5 + d] = u[d];
+        q[5 + D + d] = u[D + d];
+        q[5 + 2 * D + d] = u[D + d] - u[d];
+        C = C - std::log(u[D + d] - u[d]);
+      }
+      o += 3 + 2 * D;
+    } else if (ck == MCG_MIX_WRAP_UNIFORM) {
+      for (int j = 0; j < 3 * D; ++j) q[5 + j] = u[j];
+      o += 3 + 3 * D;
+    } else {
+      o += 3;
+    }
+    q[4] = C;
+  }
+  return MCG_OK;
+}
+
 extern "C" {
 
 int mcg_abi_version(void) { return MCG_ABI_VERSION; }
@@ -293,6 +367,9 @@ int mcg_set_proposal(mcg_ctx* ctx, int32_t kind, const double* params, size_t n)
   } else if (kind == MCG_PROP_KD_INTERP) {
     if (!ctx->kd.built) return set_error(ctx, MCG_ESTATE, "call mcg_set_kd_proposal first");
     dev.push_back(0.0);
+  } else if (kind == MCG_PROP_MIXTURE) {
+    int rc = pack_mixture(ctx, params, n, dev);
+    if (rc) return rc;
   } else {
     return set_error(ctx, MCG_EINVAL, "unsupported proposal kind %d for MH", kind);
   }

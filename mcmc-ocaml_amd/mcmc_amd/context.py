@@ -61,6 +61,10 @@ class Context:
                 self._check(L.lib().mcg_set_kd_proposal(self._p, L.dptr(jump.pts), M,
                                                         L.dptr(jump.low), L.dptr(jump.high)))
             else:
+                kd = getattr(jump, "kd", None)
+                if kd is not None:      # a mixture with a kD component: build the tree first
+                    self._check(L.lib().mcg_set_kd_proposal(self._p, L.dptr(kd.pts), kd.pts.shape[0],
+                                                            L.dptr(kd.low), L.dptr(kd.high)))
                 self._check(L.lib().mcg_set_proposal(self._p, jump.kind, L.dptr(jump.params),
                                                      len(jump.params)))
             self._keep.append(jump)

@@ -99,3 +99,52 @@ class KdInterp:
         self.pts = np.ascontiguousarray(np.asarray(pts, dtype=np.float64))
         self.low, self.high = _f64(low), _f64(high)
         self.kind = L.PROP_KD_INTERP
+
+
+def shift_uniform(a, b):
+    """y = x + random_between a b per dim (the uniform jumps of test/mcmc_test.ml:50,71-74,186-188);
+    only as a component of combine_jump_proposals."""
+    a, b = _f64(a), _f64(b)
+    p = Proposal(MIX_SHIFT_UNIFORM_KIND, np.concatenate([a, b]))
+    return p
+
+
+MIX_SHIFT_UNIFORM_KIND = -2     # Python-side tag; mapped to MCG_MIX_SHIFT_UNIFORM below
+
+
+class Mixture(Proposal):
+    """Mcmc.combine_jump_proposals [(p, jump, log_jump_prob)] (mcmc.ml:165-185).
+
+    components: (p, proposal) or (p, proposal, ljp) with proposal from gauss / shift_uniform /
+    uniform_wrapping / KdInterp and ljp = 1 for the component's log density (default for gauss,
+    shift_uniform, KdInterp) or 0 for the constant-zero log_jump_prob callers pass for symmetric
+    jumps (default, and the only choice, for uniform_wrapping)."""
+
+    def __init__(self, components, ndim):
+        parts = [float(len(components))]
+        self.kd = None
+        for comp in components:
+            p, prop = comp[0], comp[1]
+            if isinstance(prop, KdInterp):
+                if self.kd is not None:
+                    raise ValueError("combine_jump_proposals: one kD component at most")
+                self.kd = prop
+                kind, params, mode = L.MIX_KD_INTERP, [], 1
+            elif prop.kind == L.PROP_GAUSS:
+                s = prop.params
+                params = np.full(ndim, s[0]) if len(s) == 1 else s
+                kind, mode = L.MIX_GAUSS, 1
+            elif prop.kind == MIX_SHIFT_UNIFORM_KIND:
+                kind, params, mode = L.MIX_SHIFT_UNIFORM, prop.params, 1
+            elif prop.kind == L.PROP_WRAP_UNIFORM:
+                kind, params, mode = L.MIX_WRAP_UNIFORM, prop.params, 0
+            else:
+                raise ValueError("unsupported mixture component kind %r" % prop.kind)
+            if len(comp) > 2:
+                mode = int(comp[2])
+            parts += [float(p), float(kind), float(mode)] + list(np.asarray(params, np.float64))
+        super().__init__(L.PROP_MIXTURE, parts)
+
+
+def combine_jump_proposals(components, ndim):
+    return Mixture(components, ndim)

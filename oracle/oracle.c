@@ -52,6 +52,7 @@ void or_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
 #define CALL_DE_SCALE 0xFFFF0002u
 #define CALL_KD_PICK 0xFFFF0003u
 #define CALL_START 0xFFFF0004u
+#define CALL_MIX 0xFFFF0005u
 
 static inline void rng4(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t tag,
                         uint32_t hi16, uint32_t out[4]) {
@@ -277,10 +278,23 @@ typedef struct {
   double* s;                                   /* GAUSS proposal scales [D] */
   const double* wlo; const double* whi; const double* wdx;   /* WRAP_UNIFORM */
   const or_kd* kd;
+  int nmix; struct mix_comp* mix; int mix_kd;  /* MIXTURE (combine_jump_proposals) */
 } prep_t;
+
+/* one component of Mcmc.combine_jump_proposals (mcmc.ml:165-185): normalised weight p, log p,
+   kind (MCG_MIX_*), ljp mode (0: log_jump_prob = 0, 1: the component's log density) */
+struct mix_comp {
+  double p, logp, C;
+  int kind, mode;
+  const double* v0; const double* v1; const double* v2;   /* GAUSS: s; SHIFT: a, b; WRAP: lo, hi, dx */
+  double* inv_s;                                           /* GAUSS: 1/s */
+  double* width;                                           /* SHIFT: b - a */
+};
 
 static void prep_free(prep_t* p) {
   free(p->mu); free(p->isig); free(p->ctr); free(p->s);
+  for (int c = 0; c < p->nmix; ++c) { free(p->mix[c].inv_s); free(p->mix[c].width); }
+  free(p->mix);
 }
 
 static int prep_model(const or_model* m, prep_t* p) {
@@ -333,6 +347,59 @@ static int prep_model(const or_model* m, prep_t* p) {
     p->wlo = m->prop_params; p->whi = m->prop_params + D; p->wdx = m->prop_params + 2 * D;
   } else if (p->prop == MCG_PROP_KD_INTERP) {
     p->kd = (const or_kd*)m->kd;
+  } else if (p->prop == MCG_PROP_MIXTURE) {
+    /* parameters: ncomp, then per component p, kind, ljp_mode, params (include/mcg.h) */
+    const double* q = m->prop_params;
+    int nc = (int)q[0];
+    if (nc < 1 || nc > MCG_MIX_MAX_COMPONENTS) return -1;
+    p->nmix = nc;
+    p->mix = (struct mix_comp*)calloc((size_t)nc, sizeof(struct mix_comp));
+    p->kd = (const or_kd*)m->kd;
+    double ptot = 0.0;
+    int64_t o = 1;
+    for (int c = 0; c < nc; ++c) {
+      struct mix_comp* mc = &p->mix[c];
+      mc->p = q[o]; mc->kind = (int)q[o + 1]; mc->mode = (int)q[o + 2];
+      const double* u = q + o + 3;
+      ptot = ptot + mc->p;                                   /* mcmc.ml:166 */
+      switch (mc->kind) {
+        case MCG_MIX_GAUSS:
+          mc->v0 = u;
+          mc->inv_s = (double*)malloc(sizeof(double) * D);
+          mc->C = 0.0;
+          for (int d = 0; d < D; ++d) {
+            mc->inv_s[d] = 1.0 / u[d];
+            mc->C = mc->C + (NEG_HALF_LOG_2PI - log(u[d]));
+          }
+          o += 3 + D;
+          break;
+        case MCG_MIX_SHIFT_UNIFORM:
+          mc->v0 = u; mc->v1 = u + D;
+          mc->width = (double*)malloc(sizeof(double) * D);
+          mc->C = 0.0;
+          for (int d = 0; d < D; ++d) {
+            mc->width[d] = u[D + d] - u[d];
+            mc->C = mc->C - log(mc->width[d]);
+          }
+          o += 3 + 2 * D;
+          break;
+        case MCG_MIX_WRAP_UNIFORM:
+          mc->v0 = u; mc->v1 = u + D; mc->v2 = u + 2 * D;
+          o += 3 + 3 * D;
+          break;
+        case MCG_MIX_KD_INTERP:
+          mc->mode = 1;
+          p->mix_kd = 1;
+          if (!p->kd) return -1;
+          o += 3;
+          break;
+        default: return -1;
+      }
+    }
+    for (int c = 0; c < nc; ++c) {
+      p->mix[c].p = p->mix[c].p / ptot;                     /* mcmc.ml:167 */
+      p->mix[c].logp = log(p->mix[c].p);
+    }
   }
   return 0;
 }
@@ -453,6 +520,41 @@ typedef struct {
   double x[256]; double ll, lp; double lq;   /* lq: cached log q(x) for KD_INTERP */
 } chain_t;
 
+/* Mcmc.log_sum_logs, the private one of mcmc.ml:155-163: log (1 + exp lr) */
+static double mix_lse(double la, double lb) {
+  if (la == -INFINITY && lb == -INFINITY) return -INFINITY;
+  if (la > lb) return la + or_log(1.0 + or_exp(lb - la));
+  return lb + or_log(1.0 + or_exp(la - lb));
+}
+
+/* log_jp x y of combine_jump_proposals (mcmc.ml:175-182), lq_y = log q(y) of the kD tree */
+static double mix_log_jp(const prep_t* p, const double* x, const double* y, double lq_y) {
+  int D = p->D;
+  double acc = -INFINITY;
+  for (int c = 0; c < p->nmix; ++c) {
+    const struct mix_comp* mc = &p->mix[c];
+    double lj = 0.0;
+    if (mc->mode) {
+      if (mc->kind == MCG_MIX_GAUSS) {
+        double S = 0.0;
+        for (int d = 0; d < D; ++d) {
+          double e = (y[d] - x[d]) * mc->inv_s[d];
+          S = fma(e, e, S);
+        }
+        lj = mc->C - 0.5 * S;
+      } else if (mc->kind == MCG_MIX_SHIFT_UNIFORM) {
+        int in = 1;   /* test/mcmc_test.ml:188-197: y >= x + a && y <= x + b */
+        for (int d = 0; d < D; ++d) in = in && y[d] >= x[d] + mc->v0[d] && y[d] <= x[d] + mc->v1[d];
+        lj = in ? mc->C : -INFINITY;
+      } else if (mc->kind == MCG_MIX_KD_INTERP) {
+        lj = lq_y;
+      }
+    }
+    acc = mix_lse(acc, mc->logp + lj);
+  }
+  return acc;
+}
+
 static int mh_step(const prep_t* p, uint64_t seed, uint32_t gid, uint64_t T, chain_t* c) {
   int D = p->D;
   uint32_t lo = (uint32_t)T, hi = (uint32_t)(T >> 32);
@@ -495,6 +597,53 @@ static int mh_step(const prep_t* p, uint64_t seed, uint32_t gid, uint64_t T, cha
       lqy = t->llogq[kd_find_leaf_idx(t, y)];
       lf = lqy;         /* log_jump_prob start proposed = log q(proposed) */
       lb = c->lq;       /* log_jump_prob proposed start = log q(start) */
+      break;
+    }
+    case MCG_PROP_MIXTURE: {
+      /* propose: Random.float 1.0 walked down the normalised weights (mcmc.ml:168-173); the
+         reference raises Failure past the last weight -- here the last component is taken */
+      uint32_t w[4];
+      rng4(seed, gid, lo, CALL_MIX, TAG_MH, hi, w);
+      double u = or_u53(w[0], w[1]);
+      int pick = p->nmix - 1;
+      for (int k = 0; k < p->nmix; ++k) {
+        if (u < p->mix[k].p) { pick = k; break; }
+        u = u - p->mix[k].p;
+      }
+      const struct mix_comp* mc = &p->mix[pick];
+      if (mc->kind == MCG_MIX_GAUSS) {
+        double z[256];
+        normals_tagged(seed, gid, lo, TAG_MH, hi, D, z);
+        for (int d = 0; d < D; ++d) y[d] = fma(mc->v0[d], z[d], c->x[d]);
+      } else if (mc->kind == MCG_MIX_KD_INTERP) {
+        const or_kd* t = p->kd;
+        rng4(seed, gid, lo, CALL_KD_PICK, TAG_MH, hi, w);
+        uint32_t pk = or_randint(w[0], w[1], (uint32_t)t->M);
+        int64_t L = kd_find_leaf_idx(t, t->pts + (int64_t)pk * D);
+        const double* blo = t->lbox + L * 2 * D;
+        const double* bhi = blo + D;
+        for (int d = 0; d < D; d += 2) {
+          rng4(seed, gid, lo, (uint32_t)(d >> 1), TAG_MH, hi, w);
+          y[d] = blo[d] + (bhi[d] - blo[d]) * or_u53(w[0], w[1]);
+          if (d + 1 < D) y[d + 1] = blo[d + 1] + (bhi[d + 1] - blo[d + 1]) * or_u53(w[2], w[3]);
+        }
+      } else {
+        for (int d = 0; d < D; d += 2) {
+          rng4(seed, gid, lo, (uint32_t)(d >> 1), TAG_MH, hi, w);
+          double u0 = or_u53(w[0], w[1]), u1 = or_u53(w[2], w[3]);
+          for (int j = 0; j < 2 && d + j < D; ++j) {
+            int e = d + j;
+            double uu = j ? u1 : u0;
+            if (mc->kind == MCG_MIX_SHIFT_UNIFORM)   /* x + random_between a b (mcmc_test.ml:15-16) */
+              y[e] = c->x[e] + (mc->v0[e] + mc->width[e] * uu);
+            else
+              y[e] = wrap_uniform(mc->v0[e], mc->v1[e], mc->v2[e], c->x[e], uu);
+          }
+        }
+      }
+      if (p->mix_kd) lqy = p->kd->llogq[kd_find_leaf_idx(p->kd, y)];
+      lf = mix_log_jp(p, c->x, y, lqy);   /* log_jump_prob start proposed */
+      lb = mix_log_jp(p, y, c->x, c->lq); /* log_jump_prob proposed start */
       break;
     }
     default: return -1;
@@ -590,7 +739,7 @@ static void* mh_worker(void* arg) {
     for (int d = 0; d < D; ++d) c.x[d] = j->x[(int64_t)d * j->N + i];
     c.ll = j->ll[i]; c.lp = j->lp[i];
     c.lq = 0.0;
-    if (p->prop == MCG_PROP_KD_INTERP) c.lq = p->kd->llogq[kd_find_leaf_idx(p->kd, c.x)];
+    if (p->prop == MCG_PROP_KD_INTERP || p->mix_kd) c.lq = p->kd->llogq[kd_find_leaf_idx(p->kd, c.x)];
     uint32_t gid = j->chain_offset + (uint32_t)i;
     if (o->nbin == 0 && o->n_rec > 0) record_sample(j, i, 0, &c);
     uint64_t na = 0;

@@ -253,3 +253,42 @@ def test_c2_full_size_properties(T):
     np.testing.assert_allclose(mean, mu, atol=0.02)
     np.testing.assert_allclose(sd, sg, rtol=0.02)
     assert np.isfinite(log_z)
+
+
+@pytest.mark.parametrize("D", [1, 3, 16])
+def test_mixture_bit_exact(oracle, T, D):
+    """Mcmc.combine_jump_proposals (mcmc.ml:165-185): Gaussian, shift-uniform (density and
+    constant-zero log_jump_prob) and wrapping-uniform components; GPU == oracle bit for bit."""
+    rng = np.random.default_rng(40 + D)
+    mu, sg = rng.uniform(-1, 1, D), rng.uniform(0.5, 2, D)
+    lik, pri = T.diag_gauss(mu, sg), T.box(-8 * np.ones(D), 8 * np.ones(D))
+    mix = T.combine_jump_proposals([
+        (0.4, T.gauss(0.7 * sg)),
+        (1.0, T.shift_uniform(-0.5 * sg, 0.2 * sg)),
+        (0.6, T.shift_uniform(-sg, sg), 0),
+        (0.5, T.uniform_wrapping(-8 * np.ones(D), 8 * np.ones(D), sg))], D)
+    x0 = mu[:, None] + sg[:, None] * rng.normal(size=(D, 200))
+    o = run_oracle(oracle, lik, pri, mix, x0, 13, 4, 2, 30)
+    g = run_gpu(lik, pri, mix, x0, 13, nbin=4, nskip=2, n_rec=30)
+    assert_same(g, o)
+
+
+@pytest.mark.parametrize("D", [2, 5])
+def test_mixture_with_kd_component_bit_exact(oracle, T, D):
+    """kD interpolated jump (Interpolate_pdf) mixed with a local Gaussian jump."""
+    rng = np.random.default_rng(60 + D)
+    pts = rng.normal(size=(300, D))
+    lo, hi = -6 * np.ones(D), 6 * np.ones(D)
+    lik, pri = T.diag_gauss(np.zeros(D), np.ones(D)), T.box(lo, hi)
+    kdp = T.KdInterp(pts, lo, hi)
+    mix = T.combine_jump_proposals([(0.7, kdp), (0.3, T.gauss(0.4))], D)
+    x0 = rng.normal(size=(D, 150))
+    kd = oracle.KdTree(pts, lo, hi)
+    m = oracle.Model(D, lik.kind, lik.params, pri.kind, pri.params, mix.kind, mix.params, kd)
+    ll0 = np.array([m.loglik(x0[:, i]) for i in range(x0.shape[1])])
+    lp0 = np.array([m.logprior(x0[:, i]) for i in range(x0.shape[1])])
+    o = oracle.mh_run(m, 21, x0, ll0, lp0, nbin=3, nskip=1, n_rec=40, nthreads=8)
+    o["ll0"], o["lp0"] = ll0, lp0
+    o["tiles"] = oracle.tile_stats(D, x0.shape[1], 40, o)
+    g = run_gpu(lik, pri, mix, x0, 21, nbin=3, nskip=1, n_rec=40)
+    assert_same(g, o)
