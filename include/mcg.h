@@ -229,6 +229,23 @@ int mcg_nested_merge(int32_t nruns, const int64_t* n_total, const int64_t* nlive
                      const double* ll, int64_t* order, double* log_ev, double* log_dev,
                      double* log_wts);
 
+/* ---- Read_write text formats (read_write.ml:19-101) ----
+   A Read_write file is rows of doubles printed with OCaml Printf "%g" (C %g; nan prints as
+   "nan"), separated by single spaces, one row per line:
+     write / write_sample (read_write.ml:19-30): coords..., log_likelihood, log_prior
+     write_nested (read_write.ml:58-66): a "log_ev log_dev" first line, then
+                                         coords..., log_likelihood, log_prior, log_weight
+   mcg_write_rows writes `header` (may be NULL, e.g. the write_nested first line) and then
+   rows [nrows][ncols] (formatted in parallel, written in order); append != 0 appends.
+   mcg_read_rows_shape counts the non-blank lines after skip_lines and their common field count
+   (ragged rows -> MCG_EFAIL); mcg_read_rows parses them (Scanf " %g ", read_write.ml:33-56) into
+   rows [nrows][ncols] and, if header != NULL, the first nheader fields of line 0. */
+int mcg_write_rows(const char* path, int32_t append, const char* header, int64_t nrows, int32_t ncols,
+                   const double* rows);
+int mcg_read_rows_shape(const char* path, int64_t skip_lines, int64_t* nrows, int32_t* ncols);
+int mcg_read_rows(const char* path, int64_t skip_lines, int64_t nrows, int32_t ncols, double* rows,
+                  double* header, int32_t nheader);
+
 /* ---- device timing of the dominant kernel (HIP events on the launch stream) ---- */
 typedef struct {
   int64_t launches;
