@@ -160,6 +160,48 @@ int mcg_get_records(mcg_ctx* ctx, double* rec_x, double* rec_ll, double* rec_lp,
                     uint64_t* accept_bits);
 int64_t mcg_last_run_steps(const mcg_ctx* ctx);
 
+/* ---- reversible-jump MCMC between two models (Mcmc.make_rjmcmc_sampler / rjmcmc_array,
+   mcmc.ml:84-153) ----
+   Each chain carries a model tag (0 = A, 1 = B) and a point of that model's dimension (padded
+   with zeros to max(ndim_A, ndim_B) in the [Dmax][N] state).  A step draws u ~ U[0,1): with
+   probability p_tag an internal jump of the current model, else a transition into the other
+   model (mcmc.ml:93-103); log_jump_prob and the model log prior log p_m + lp_m follow
+   mcmc.ml:104-116.  Likelihood kinds: FLAT, DIAG_GAUSS, GAUSS_SHELL, FULLCOV_GAUSS; priors as
+   above.  Jump kinds (internal and into):
+     MCG_RJ_JUMP_GAUSS       s[1] or s[D]   random walk y = x + s z, log_jump_prob 0
+     MCG_RJ_JUMP_WRAP        lo, hi, dx     Mcmc.uniform_wrapping per dim, log_jump_prob 0
+     MCG_RJ_JUMP_INDEP_GAUSS mu[D], s[D]    independence draw N(mu, s); log_jump_prob _ y =
+                                            sum_d Stats.log_gaussian mu_d s_d y_d
+     MCG_RJ_JUMP_KD          (kd_pts...)    independence draw Interpolate_pdf.draw from a kD tree
+                                            over kd_pts; log_jump_prob _ y = log jump_prob y
+   Transition proposals (into_kind) must be independence kinds (INDEP_GAUSS or KD): the
+   reference's jintoa / jintob take the other model's point, which no descriptor kind uses. */
+enum { MCG_RJ_JUMP_GAUSS = 1, MCG_RJ_JUMP_WRAP = 2, MCG_RJ_JUMP_INDEP_GAUSS = 3, MCG_RJ_JUMP_KD = 4 };
+
+typedef struct {
+  int32_t ndim;
+  int32_t lik_kind;   const double* lik_params;   size_t n_lik;
+  int32_t prior_kind; const double* prior_params; size_t n_prior;
+  int32_t jump_kind;  const double* jump_params;  size_t n_jump;   /* internal jump (jpa, ljpa) */
+  int32_t into_kind;  const double* into_params;  size_t n_into;   /* jump into this model (jintoa, ljpintoa) */
+  const double* kd_pts; int64_t kd_M;              /* [M][ndim] tree points for the KD kinds */
+  const double* kd_low; const double* kd_high;     /* tree bounds (Interpolate_pdf.make) */
+  double model_prior;                              /* pa / pb (pa + pb = 1, mcmc.ml:91) */
+} mcg_rj_model;
+
+int mcg_set_rjmcmc(mcg_ctx* ctx, const mcg_rj_model* a, const mcg_rj_model* b);
+/* model[N] (0 = A, 1 = B) or NULL for rjmcmc_array's fair coin per chain (mcmc.ml:120);
+   xa [ndim_A][N], xb [ndim_B][N]: the start point of each chain in model A and in model B (the
+   (a, b) pair of rjmcmc_array, per chain); the chain starts from the one of its model.  ll / lp
+   are evaluated on the device (lp includes log p_model, mcmc.ml:122-124).  Then mcg_run runs
+   rjmcmc_array's schedule (mcmc.ml:125-132) over every chain; the state and records use the
+   padded [Dmax][N] layout (dims beyond the chain's model are 0). */
+int mcg_rj_init(mcg_ctx* ctx, int64_t nchains, const uint8_t* model, const double* xa, const double* xb);
+/* model tags: current state [N] and recorded samples [n_rec][N] of the last run (any may be
+   NULL); counts = rjmcmc_model_counts over every recorded sample of every chain (mcmc.ml:136-144) */
+int mcg_rj_get_models(mcg_ctx* ctx, uint8_t* state_model, uint8_t* rec_model);
+int mcg_rj_model_counts(mcg_ctx* ctx, uint64_t* na, uint64_t* nb);
+
 /* ---- counters (mcmc.ml:27-35) ---- */
 int mcg_get_counters(mcg_ctx* ctx, uint64_t* naccept, uint64_t* nreject);
 int mcg_reset_counters(mcg_ctx* ctx);

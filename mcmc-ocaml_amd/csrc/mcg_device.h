@@ -16,6 +16,16 @@ struct KdNode {
 enum : int32_t { RUNF_RECORD_X = 1, RUNF_RECORD_LLP = 2, RUNF_RECORD_ACCEPT = 4, RUNF_ACCUMULATE = 8,
                  RUNF_RECORD_INITIAL = 16 };
 
+// device view of one flattened kD tree (mcg_kdtree.cpp)
+struct KdView {
+  const KdNode* nodes;
+  const double* logq;
+  const double* box;
+  const double* root;
+  const int32_t* pt_leaf;
+  int64_t M;
+};
+
 // Arguments of one MH launch (a contiguous slice of the steps of one mcg_run).
 struct MhArgs {
   double* x;            // [D][N] chain state
@@ -58,6 +68,12 @@ struct MhArgs {
   int32_t prior_kind;
   int32_t flags;        // RUNF_*
   int32_t is_cauchy;
+  // reversible jump (mcg_rj_kernel.h): model descriptors, tags, recorded tags, B-record counts
+  const double* rj;
+  uint8_t* tag;                 // [N]
+  uint8_t* rec_tag;             // [n_rec][N]
+  unsigned long long* rj_nb;    // [N] recorded samples in model B
+  KdView rj_kd[2];
 };
 
 struct TileArgs {

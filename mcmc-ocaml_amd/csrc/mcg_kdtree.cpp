@@ -91,13 +91,13 @@ struct Builder {
 }  // namespace
 
 int kd_build(mcg_ctx* ctx, const double* pts, int64_t M, int D, const double* low,
-             const double* high) {
+             const double* high, KdState* dst) {
   Builder b{pts, D, M, {}, {}, {}, {}};
   std::vector<int64_t> idx((size_t)M);
   std::iota(idx.begin(), idx.end(), 0);
   std::vector<double> lo(low, low + D), hi(high, high + D);
   b.build(idx.data(), M, lo, hi);
-  KdState& k = ctx->kd;
+  KdState& k = dst ? *dst : ctx->kd;
   k.M = M;
   k.nnodes = (int64_t)b.nodes.size();
   k.nleaves = (int64_t)b.count.size();

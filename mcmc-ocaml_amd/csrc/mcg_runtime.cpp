@@ -236,12 +236,16 @@ void mcg_ctx_destroy(mcg_ctx* ctx) {
   delete ctx;
 }
 
-int mcg_set_likelihood(mcg_ctx* ctx, int32_t kind, int32_t ndim, const double* params, size_t n) {
-  if (!ctx) return MCG_EINVAL;
-  std::vector<double> dev;
-  int D = ndim;
+}  // extern "C"
+
+namespace mcg {
+
+// device layout of a likelihood descriptor (the layouts mcg_mh_kernel.h eval_lik reads)
+int pack_likelihood(mcg_ctx* ctx, int32_t kind, int D, const double* params, size_t n,
+                    std::vector<double>& dev, int32_t* is_cauchy_out, int64_t* data_n_out) {
   int32_t is_cauchy = 0;
   int64_t data_n = 0;
+  dev.clear();
   switch (kind) {
     case MCG_LIK_FLAT:
       if (D < 1) return set_error(ctx, MCG_EINVAL, "FLAT: ndim >= 1");
@@ -299,6 +303,24 @@ int mcg_set_likelihood(mcg_ctx* ctx, int32_t kind, int32_t ndim, const double* p
     default:
       return set_error(ctx, MCG_EINVAL, "unknown likelihood kind %d", kind);
   }
+  if (is_cauchy_out) *is_cauchy_out = is_cauchy;
+  if (data_n_out) *data_n_out = data_n;
+  return MCG_OK;
+}
+
+}  // namespace mcg
+
+extern "C" {
+
+int mcg_set_likelihood(mcg_ctx* ctx, int32_t kind, int32_t ndim, const double* params, size_t n) {
+  if (!ctx) return MCG_EINVAL;
+  std::vector<double> dev;
+  const int D = ndim;
+  int32_t is_cauchy = 0;
+  int64_t data_n = 0;
+  int prc = pack_likelihood(ctx, kind, D, params, n, dev, &is_cauchy, &data_n);
+  if (prc) return prc;
+  ctx->rj_active = false;
   if (ctx->D != 0 && ctx->D != D && ctx->N > 0)
     return set_error(ctx, MCG_ESTATE, "ndim changed after mcg_init");
   ctx->D = D;
@@ -319,13 +341,14 @@ int mcg_set_likelihood(mcg_ctx* ctx, int32_t kind, int32_t ndim, const double* p
   return MCG_OK;
 }
 
-int mcg_set_prior(mcg_ctx* ctx, int32_t kind, const double* params, size_t n) {
-  if (!ctx) return MCG_EINVAL;
-  int D = ctx->D;
-  if (D < 1) return set_error(ctx, MCG_ESTATE, "set the likelihood (ndim) first");
-  // device layout: [check_lo[D], check_hi[D], lp_in, lo[D], hi[D]]: the closed-form bounds used
-  // by the kernels' box test, then the caller's bounds (uniform draws of nested sampling)
-  std::vector<double> dev(4 * D + 1);
+}  // extern "C"
+
+namespace mcg {
+
+// device layout: [check_lo[D], check_hi[D], lp_in, lo[D], hi[D]]: the closed-form bounds used
+// by the kernels' box test, then the caller's bounds (uniform draws of nested sampling)
+int pack_prior(mcg_ctx* ctx, int32_t kind, int D, const double* params, size_t n, std::vector<double>& dev) {
+  dev.assign(4 * (size_t)D + 1, 0.0);
   if (kind == MCG_PRIOR_FLAT) {
     for (int d = 0; d < D; ++d) {
       dev[d] = dev[2 * D + 1 + d] = -HUGE_VAL;
@@ -345,6 +368,20 @@ int mcg_set_prior(mcg_ctx* ctx, int32_t kind, const double* params, size_t n) {
   } else {
     return set_error(ctx, MCG_EINVAL, "unknown prior kind %d", kind);
   }
+  return MCG_OK;
+}
+
+}  // namespace mcg
+
+extern "C" {
+
+int mcg_set_prior(mcg_ctx* ctx, int32_t kind, const double* params, size_t n) {
+  if (!ctx) return MCG_EINVAL;
+  int D = ctx->D;
+  if (D < 1) return set_error(ctx, MCG_ESTATE, "set the likelihood (ndim) first");
+  std::vector<double> dev;
+  int prc = pack_prior(ctx, kind, D, params, n, dev);
+  if (prc) return prc;
   ctx->prior_kind = kind;
   ctx->pri_host = dev;
   int rc = hip_check(ctx, ctx->d_pri.ensure(dev.size() * 8), "alloc prior");
@@ -464,6 +501,7 @@ MhArgs base_args(mcg_ctx* ctx) {
   a.kd_root = (const double*)ctx->kd.d_root.p;
   a.kd_pt_leaf = (const int32_t*)ctx->kd.d_pt_leaf.p;
   a.kd_M = ctx->kd.M;
+  if (ctx->rj_active) rj_args(ctx, a);
   return a;
 }
 
@@ -508,8 +546,8 @@ int mcg_run(mcg_ctx* ctx, const mcg_run_opts* o) {
   (void)hipSetDevice(ctx->opts.device);
   const int D = ctx->D;
   const int64_t N = ctx->N;
-  const int P = choose_lanes(ctx);
-  mh_launch_fn fn = find_mh_kernel(D, P, ctx->lik_kind, ctx->prop_kind);
+  const int P = ctx->rj_active ? 1 : choose_lanes(ctx);
+  mh_launch_fn fn = ctx->rj_active ? find_rj_kernel(D) : find_mh_kernel(D, P, ctx->lik_kind, ctx->prop_kind);
   if (!fn) return set_error(ctx, MCG_EINVAL, "no compiled MH kernel for D=%d likelihood=%d proposal=%d", D, ctx->lik_kind, ctx->prop_kind);
   ctx->lanes = P;
   // mcmc_array schedule: records at run-local step counts s_r = nbin + r*nskip (r < n_rec);
@@ -534,7 +572,12 @@ int mcg_run(mcg_ctx* ctx, const mcg_run_opts* o) {
     if ((rc = hip_check(ctx, ctx->d_bits.ensure((size_t)nsteps * row_bytes), "alloc accept bits"))) return rc;
     if ((rc = hip_check(ctx, hipMemsetAsync(ctx->d_bits.p, 0, (size_t)nsteps * row_bytes, ctx->stream), "zero bits"))) return rc;
   }
-  if (o->accumulate) {
+  if (ctx->rj_active) {
+    if (o->record_llp && n_rec > 0 &&
+        (rc = hip_check(ctx, ctx->d_rec_tag.ensure((size_t)n_rec * Nz), "alloc rec tags"))) return rc;
+    if (o->accumulate && !append &&
+        (rc = hip_check(ctx, hipMemsetAsync(ctx->d_rj_nb.p, 0, Nz * 8, ctx->stream), "zero rj counts"))) return rc;
+  } else if (o->accumulate) {
     if ((rc = hip_check(ctx, ctx->d_mean.ensure(Nz * D * 8), "alloc mean"))) return rc;
     if ((rc = hip_check(ctx, ctx->d_m2.ensure(Nz * D * 8), "alloc m2"))) return rc;
     if ((rc = hip_check(ctx, ctx->d_hm_m.ensure(8 * Nz * 8), "alloc hm"))) return rc;

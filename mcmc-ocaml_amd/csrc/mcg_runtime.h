@@ -75,6 +75,13 @@ struct mcg_ctx {
   int inv_slot = 0, inv_cur = 0;
   std::vector<double> inv_host[2];
   bool rec_x_valid = false, rec_llp_valid = false, last_record_accept = false;
+  // reversible jump (mcg_rj.cpp)
+  bool rj_active = false;
+  std::vector<double> rj_host;
+  mcg::DevBuf d_rj, d_tag, d_rec_tag, d_rj_nb;
+  mcg::KdState rj_kd[2];
+  std::vector<double> rj_root[2];
+  mcg::DevBuf d_rj_root[2];
   // nested sampling
   mcg::NestedState nested;
   mcg_nested_bufs_holder* nested_bufs = nullptr;
@@ -97,5 +104,13 @@ double host_pexp(double x);
 void timing_begin(mcg_ctx* ctx, hipEvent_t* a, hipEvent_t* b);
 void timing_end(mcg_ctx* ctx, hipEvent_t a, hipEvent_t b, int kind);
 void timing_harvest(mcg_ctx* ctx);
-int kd_build(mcg_ctx* ctx, const double* pts, int64_t M, int D, const double* low, const double* high);
+int kd_build(mcg_ctx* ctx, const double* pts, int64_t M, int D, const double* low, const double* high,
+             KdState* dst = nullptr);
+int pack_likelihood(mcg_ctx* ctx, int32_t kind, int D, const double* params, size_t n,
+                    std::vector<double>& dev, int32_t* is_cauchy, int64_t* data_n);
+int pack_prior(mcg_ctx* ctx, int32_t kind, int D, const double* params, size_t n, std::vector<double>& dev);
+typedef hipError_t (*rj_init_fn)(const MhArgs&, int draw_tags, const double* xa, const double* xb, hipStream_t);
+mh_launch_fn find_rj_kernel(int DM);
+rj_init_fn find_rj_init(int DM);
+void rj_args(mcg_ctx* ctx, MhArgs& a);
 }  // namespace mcg

@@ -15,6 +15,7 @@ LIK_FLAT, LIK_DIAG_GAUSS, LIK_FULLCOV_GAUSS, LIK_GAUSS_SHELL, LIK_GAUSS_DATA, LI
 PRIOR_FLAT, PRIOR_BOX, PRIOR_OPEN_BOX = 0, 1, 2
 PROP_GAUSS, PROP_WRAP_UNIFORM, PROP_KD_INTERP, PROP_DE, PROP_MIXTURE = 1, 2, 3, 4, 5
 MIX_GAUSS, MIX_SHIFT_UNIFORM, MIX_WRAP_UNIFORM, MIX_KD_INTERP = 1, 2, 3, 4
+RJ_JUMP_GAUSS, RJ_JUMP_WRAP, RJ_JUMP_INDEP_GAUSS, RJ_JUMP_KD = 1, 2, 3, 4
 FLAG_NESTED_FIXED_STOP = 1
 
 _dp = C.POINTER(C.c_double)
@@ -43,6 +44,16 @@ class McgNestedOpts(C.Structure):
 class McgNestedResult(C.Structure):
     _fields_ = [("log_ev", C.c_double), ("log_dev", C.c_double), ("n_dead", C.c_int64),
                 ("n_total", C.c_int64), ("n_gen", C.c_int64)]
+
+
+class McgRjModel(C.Structure):
+    _fields_ = [("ndim", C.c_int32),
+                ("lik_kind", C.c_int32), ("lik_params", _dp), ("n_lik", C.c_size_t),
+                ("prior_kind", C.c_int32), ("prior_params", _dp), ("n_prior", C.c_size_t),
+                ("jump_kind", C.c_int32), ("jump_params", _dp), ("n_jump", C.c_size_t),
+                ("into_kind", C.c_int32), ("into_params", _dp), ("n_into", C.c_size_t),
+                ("kd_pts", _dp), ("kd_M", C.c_int64), ("kd_low", _dp), ("kd_high", _dp),
+                ("model_prior", C.c_double)]
 
 
 class McgKernelTiming(C.Structure):
@@ -83,6 +94,10 @@ SIGNATURES = {
     "mcg_write_rows": ([C.c_char_p, C.c_int32, C.c_char_p, C.c_int64, C.c_int32, _dp], C.c_int),
     "mcg_read_rows_shape": ([C.c_char_p, C.c_int64, _i64p, _i32p], C.c_int),
     "mcg_read_rows": ([C.c_char_p, C.c_int64, C.c_int64, C.c_int32, _dp, _dp, C.c_int32], C.c_int),
+    "mcg_set_rjmcmc": ([C.c_void_p, C.POINTER(McgRjModel), C.POINTER(McgRjModel)], C.c_int),
+    "mcg_rj_init": ([C.c_void_p, C.c_int64, C.POINTER(C.c_uint8), _dp, _dp], C.c_int),
+    "mcg_rj_get_models": ([C.c_void_p, C.POINTER(C.c_uint8), C.POINTER(C.c_uint8)], C.c_int),
+    "mcg_rj_model_counts": ([C.c_void_p, _u64p, _u64p], C.c_int),
     "mcg_nested_merge": ([C.c_int32, _i64p, _i64p, _i64p, _dp, _i64p, _dp, _dp, _dp], C.c_int),
     "mcg_get_kernel_timing": ([C.c_void_p, C.c_char_p, C.POINTER(McgKernelTiming)], C.c_int),
     "mcg_set_timing": ([C.c_void_p, C.c_int32], C.c_int),
@@ -139,6 +154,10 @@ def dptr(a):
 
 def u64ptr(a):
     return None if a is None else a.ctypes.data_as(_u64p)
+
+
+def u8ptr(a):
+    return None if a is None else a.ctypes.data_as(C.POINTER(C.c_uint8))
 
 
 def i64ptr(a):

@@ -67,3 +67,58 @@ def make_mcmc_sampler(log_likelihood, log_prior, jump_proposal, ctx=None):
         return ctx.state()
 
     return step
+
+
+@dataclass
+class RjSamples:
+    """('a, 'b) rjmcmc_sample array (mcmc.ml:86-87) for N chains, structure-of-arrays: value is
+    padded to max(ndim_A, ndim_B) (dims beyond the sample's model are 0)."""
+    model: np.ndarray            # (n, N) uint8: 0 = A, 1 = B
+    value: np.ndarray            # (n, Dmax, N)
+    log_likelihood: np.ndarray   # (n, N)
+    log_prior: np.ndarray        # (n, N) includes log p_model (mcmc.ml:115-116)
+    counts: tuple = (0, 0)       # rjmcmc_model_counts over every recorded sample
+
+
+def rjmcmc_array(n, model_a, model_b, start, nchains=1, nbin=0, nskip=1, ctx=None, models=None,
+                 record_x=True):
+    """Mcmc.rjmcmc_array ?nbin ?nskip n lls lps jps ljps jintos ljpintos (pa, pb) (a, b)
+    (mcmc.ml:118-132) for `nchains` chains.  model_a / model_b are targets.RjModel descriptors
+    (likelihood, prior, internal jump, jump into the model, model prior); start = (a, b) start
+    points (a (D_A,) / (D_A, N) array, likewise b).  Each chain starts in A or B by a fair coin
+    (mcmc.ml:120) unless models (N,) gives the start models."""
+    import ctypes as C
+    from . import _lib as L
+    ctx = ctx or default_context()
+    sa, sb = model_a.c_struct(), model_b.c_struct()
+    ctx._keep = [model_a, model_b]
+    L.check(L.lib().mcg_set_rjmcmc(ctx.ptr, C.byref(sa), C.byref(sb)), ctx.ptr)
+    a, b = start
+    xa = np.ascontiguousarray(np.broadcast_to(np.reshape(a, (model_a.ndim, -1)), (model_a.ndim, nchains)), np.float64)
+    xb = np.ascontiguousarray(np.broadcast_to(np.reshape(b, (model_b.ndim, -1)), (model_b.ndim, nchains)), np.float64)
+    tags = None if models is None else np.ascontiguousarray(models, np.uint8)
+    L.check(L.lib().mcg_rj_init(ctx.ptr, nchains, L.u8ptr(tags), L.dptr(xa), L.dptr(xb)), ctx.ptr)
+    ctx.ndim = max(model_a.ndim, model_b.ndim)
+    ctx.nchains = nchains
+    ctx.run(nbin=nbin, nskip=nskip, n_rec=n, record_x=record_x, record_llp=True, accumulate=True)
+    x, ll, lp, _ = ctx.records(x=record_x, llp=True)
+    rec_model = np.zeros((n, nchains), np.uint8)
+    L.check(L.lib().mcg_rj_get_models(ctx.ptr, None, L.u8ptr(rec_model)), ctx.ptr)
+    return RjSamples(rec_model, x, ll, lp, rjmcmc_model_counts(ctx))
+
+
+def rjmcmc_model_counts(ctx_or_samples):
+    """Mcmc.rjmcmc_model_counts (mcmc.ml:134-142): (#A, #B) over the recorded samples."""
+    if isinstance(ctx_or_samples, RjSamples):
+        nb = int(ctx_or_samples.model.sum())
+        return ctx_or_samples.model.size - nb, nb
+    from . import _lib as L
+    na = np.zeros(1, np.uint64); nb = np.zeros(1, np.uint64)
+    L.check(L.lib().mcg_rj_model_counts(ctx_or_samples.ptr, L.u64ptr(na), L.u64ptr(nb)), ctx_or_samples.ptr)
+    return int(na[0]), int(nb[0])
+
+
+def rjmcmc_evidence_ratio(samples):
+    """Mcmc.rjmcmc_evidence_ratio (mcmc.ml:144-146): #A / #B."""
+    na, nb = samples.counts if isinstance(samples, RjSamples) else rjmcmc_model_counts(samples)
+    return float(na) / float(nb)

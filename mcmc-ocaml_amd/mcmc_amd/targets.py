@@ -148,3 +148,59 @@ class Mixture(Proposal):
 
 def combine_jump_proposals(components, ndim):
     return Mixture(components, ndim)
+
+
+# ---- reversible-jump descriptors (Mcmc.make_rjmcmc_sampler, mcmc.ml:89-116) ----
+class RjJump:
+    """A jump of one RJ model: kind MCG_RJ_JUMP_* with its parameters (include/mcg.h)."""
+
+    def __init__(self, kind, params=(), kd=None):
+        self.kind, self.params, self.kd = kind, _f64(params if len(params) else [0.0]), kd
+        self.n = len(params)
+
+
+def rj_gauss(scale):
+    """random-walk jump x + s z (log_jump_prob 0)."""
+    return RjJump(L.RJ_JUMP_GAUSS, np.atleast_1d(_f64(scale)))
+
+
+def rj_wrap(lo, hi, dx):
+    """Mcmc.uniform_wrapping per dim (log_jump_prob 0)."""
+    return RjJump(L.RJ_JUMP_WRAP, np.concatenate([_f64(lo), _f64(hi), _f64(dx)]))
+
+
+def rj_indep_gauss(mu, sigma):
+    """independence draw Stats.draw_gaussian mu sigma per dim; log_jump_prob _ y = log N(y)."""
+    return RjJump(L.RJ_JUMP_INDEP_GAUSS, np.concatenate([_f64(mu), _f64(sigma)]))
+
+
+def rj_kd(pts, low, high):
+    """independence draw Interpolate_pdf.draw; log_jump_prob _ y = log (jump_prob y)."""
+    return RjJump(L.RJ_JUMP_KD, [], KdInterp(pts, low, high))
+
+
+class RjModel:
+    """One model of a reversible-jump pair: likelihood, prior, internal jump, jump into it,
+    model prior probability."""
+
+    def __init__(self, log_likelihood, log_prior, jump, jump_into, model_prior):
+        self.lik, self.prior, self.jump, self.into = log_likelihood, log_prior, jump, jump_into
+        self.model_prior = float(model_prior)
+        kds = [j.kd for j in (jump, jump_into) if j.kd is not None]
+        if len(kds) == 2 and kds[0] is not kds[1]:
+            raise ValueError("one kD tree per RJ model: pass the same rj_kd to jump and jump_into")
+        self.kd = kds[0] if kds else None
+
+    @property
+    def ndim(self):
+        return self.lik.ndim
+
+    def c_struct(self):
+        kd = self.kd
+        return L.McgRjModel(self.ndim, self.lik.kind, L.dptr(self.lik.params), len(self.lik.params),
+                            self.prior.kind, L.dptr(self.prior.params), len(self.prior.params),
+                            self.jump.kind, L.dptr(self.jump.params), self.jump.n,
+                            self.into.kind, L.dptr(self.into.params), self.into.n,
+                            L.dptr(kd.pts) if kd else None, kd.pts.shape[0] if kd else 0,
+                            L.dptr(kd.low) if kd else None, L.dptr(kd.high) if kd else None,
+                            self.model_prior)

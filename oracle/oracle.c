@@ -797,6 +797,198 @@ int or_mh_run(const or_model* m, uint64_t seed, uint32_t chain_offset, int64_t N
 }
 
 /* ======================================================================================
+ * Reversible jump between two models (Mcmc.make_rjmcmc_sampler, mcmc.ml:89-116; rjmcmc_array's
+ * schedule mcmc.ml:118-132), RNG injected: selector call CALL_RJ, start coin CALL_RJ_START
+ * ====================================================================================== */
+#define CALL_RJ 0xFFFF0006u
+#define CALL_RJ_START 0xFFFF0007u
+
+typedef struct {
+  prep_t p[2];
+  const or_rj_model* m[2];
+  double logp[2];
+  int DM;
+} rj_prep;
+
+/* log_jump_prob _ to of an independence jump; 0 for the random walks */
+static double rj_ljp_to(const rj_prep* R, int k, int kind, const double* q, const double* to) {
+  int D = R->m[k]->ndim;
+  if (kind == MCG_RJ_JUMP_INDEP_GAUSS) {
+    /* sum_d Stats.log_gaussian mu_d s_d to_d as C - S/2, e = to/s - mu/s (stats.ml:98-101) */
+    double C = 0.0, S = 0.0;
+    for (int d = 0; d < D; ++d) {
+      double inv = 1.0 / q[D + d];
+      double e = fma(to[d], inv, -(q[d] * inv));
+      S = fma(e, e, S);
+      C = C + (NEG_HALF_LOG_2PI - log(q[D + d]));
+    }
+    return C - 0.5 * S;
+  } else if (kind == MCG_RJ_JUMP_KD) {
+    const or_kd* t = (const or_kd*)R->m[k]->kd;
+    return t->llogq[kd_find_leaf_idx(t, to)];
+  }
+  return 0.0;
+}
+
+static void rj_draw(const rj_prep* R, int k, int kind, const double* q, uint64_t seed, uint32_t gid,
+                    uint32_t lo, uint32_t hi, const double* x, double* y) {
+  int D = R->m[k]->ndim;
+  for (int d = 0; d < R->DM; ++d) y[d] = 0.0;
+  uint32_t w[4];
+  if (kind == MCG_RJ_JUMP_GAUSS || kind == MCG_RJ_JUMP_INDEP_GAUSS) {
+    double z[256];
+    normals_tagged(seed, gid, lo, TAG_MH, hi, D, z);
+    for (int d = 0; d < D; ++d) {
+      double s = (kind == MCG_RJ_JUMP_GAUSS) ? (R->m[k]->n_jump == 1 ? q[0] : q[d]) : q[D + d];
+      y[d] = (kind == MCG_RJ_JUMP_GAUSS) ? fma(s, z[d], x[d]) : fma(s, z[d], q[d]);
+    }
+  } else if (kind == MCG_RJ_JUMP_WRAP) {
+    for (int d = 0; d < D; d += 2) {
+      rng4(seed, gid, lo, (uint32_t)(d >> 1), TAG_MH, hi, w);
+      y[d] = wrap_uniform(q[d], q[D + d], q[2 * D + d], x[d], or_u53(w[0], w[1]));
+      if (d + 1 < D) y[d + 1] = wrap_uniform(q[d + 1], q[D + d + 1], q[2 * D + d + 1], x[d + 1], or_u53(w[2], w[3]));
+    }
+  } else {
+    /* Interpolate_pdf.draw (interpolate_pdf.ml:114-119) on model k's tree */
+    const or_kd* t = (const or_kd*)R->m[k]->kd;
+    rng4(seed, gid, lo, CALL_KD_PICK, TAG_MH, hi, w);
+    uint32_t pk = or_randint(w[0], w[1], (uint32_t)t->M);
+    int64_t L = kd_find_leaf_idx(t, t->pts + (int64_t)pk * D);
+    const double* blo = t->lbox + L * 2 * D;
+    const double* bhi = blo + D;
+    for (int d = 0; d < D; d += 2) {
+      rng4(seed, gid, lo, (uint32_t)(d >> 1), TAG_MH, hi, w);
+      y[d] = blo[d] + (bhi[d] - blo[d]) * or_u53(w[0], w[1]);
+      if (d + 1 < D) y[d + 1] = blo[d + 1] + (bhi[d + 1] - blo[d + 1]) * or_u53(w[2], w[3]);
+    }
+  }
+}
+
+typedef struct {
+  const rj_prep* R; uint64_t seed; int64_t N; const or_run_opts* o;
+  uint8_t* tag; double* x; double* ll; double* lp; int draw_tags; const double* xa; const double* xb;
+  double* rec_x; double* rec_ll; double* rec_lp; uint8_t* rec_tag; uint64_t* bits;
+  uint64_t* nacc; uint64_t* nb_rec; int64_t i0, i1;
+} rj_job;
+
+static void* rj_worker(void* arg) {
+  rj_job* j = (rj_job*)arg;
+  const rj_prep* R = j->R;
+  const or_run_opts* o = j->o;
+  int DM = R->DM;
+  int64_t N = j->N;
+  int64_t nsteps = o->nbin + (o->n_rec > 0 ? (o->n_rec - 1) * o->nskip : 0);
+  int64_t words = (N + 63) / 64;
+  double x[256], y[256];
+  for (int64_t i = j->i0; i < j->i1; ++i) {
+    uint32_t gid = (uint32_t)i;
+    int tag = j->tag[i];
+    if (j->draw_tags) {              /* rjmcmc_array: is_a = Random.float 1.0 < 0.5 (mcmc.ml:120) */
+      uint32_t w[4];
+      rng4(j->seed, gid, 0u, CALL_RJ_START, TAG_MH, 0u, w);
+      tag = or_u53(w[0], w[1]) < 0.5 ? 0 : 1;
+    }
+    int D0 = R->m[tag]->ndim;
+    const double* src = tag ? j->xb : j->xa;
+    for (int d = 0; d < DM; ++d) x[d] = d < D0 ? src[(int64_t)d * N + i] : 0.0;
+    /* start record: log_like and lpa a + log pa (mcmc.ml:121-124) */
+    double ll = lik_eval(&R->p[tag], x), lp = prior_eval(&R->p[tag], x) + R->logp[tag];
+    uint64_t na = 0, nb = 0;
+#define RJ_RECORD(r) do { \
+      if (o->record_x && j->rec_x) for (int d = 0; d < DM; ++d) j->rec_x[((r) * DM + d) * N + i] = x[d]; \
+      if (o->record_llp) { j->rec_ll[(r) * N + i] = ll; j->rec_lp[(r) * N + i] = lp; j->rec_tag[(r) * N + i] = (uint8_t)tag; } \
+      nb += (uint64_t)tag; } while (0)
+    if (o->nbin == 0 && o->n_rec > 0) RJ_RECORD(0);
+    for (int64_t t = 0; t < nsteps; ++t) {
+      uint64_t T = (uint64_t)t;
+      uint32_t lo = (uint32_t)T, hi = (uint32_t)(T >> 32);
+      uint32_t w[4];
+      rng4(j->seed, gid, lo, CALL_RJ, TAG_MH, hi, w);
+      const or_rj_model* mc = R->m[tag];
+      int internal = or_u53(w[0], w[1]) < mc->model_prior;          /* mcmc.ml:95,100 */
+      int ytag = internal ? tag : 1 - tag;
+      const or_rj_model* my = R->m[ytag];
+      int kind = internal ? my->jump_kind : my->into_kind;
+      const double* q = internal ? my->jump_params : my->into_params;
+      rj_draw(R, ytag, kind, q, j->seed, gid, lo, hi, x, y);
+      double lf = R->logp[ytag] + rj_ljp_to(R, ytag, kind, q, y);  /* log_jump_prob x y */
+      double lb = internal ? R->logp[ytag] + rj_ljp_to(R, ytag, kind, q, x)
+                           : R->logp[tag] + rj_ljp_to(R, tag, mc->into_kind, mc->into_params, x);
+      double lly = lik_eval(&R->p[ytag], y);
+      double lpy = R->logp[ytag] + prior_eval(&R->p[ytag], y);
+      double ratio = (((lly + lpy) - (ll + lp)) + lb) - lf;
+      rng4(j->seed, gid, lo, CALL_ACCEPT, TAG_MH, hi, w);
+      int a = or_log(or_u53(w[0], w[1])) < ratio;
+      if (a) {
+        for (int d = 0; d < DM; ++d) x[d] = y[d];
+        ll = lly; lp = lpy; tag = ytag; ++na;
+        if (o->record_accept && j->bits) j->bits[t * words + (i >> 6)] |= (1ull << (i & 63));
+      }
+      int64_t t1 = t + 1;
+      if (t1 >= o->nbin && ((t1 - o->nbin) % o->nskip) == 0) {
+        int64_t r = (t1 - o->nbin) / o->nskip;
+        if (r < o->n_rec) RJ_RECORD(r);
+      }
+    }
+#undef RJ_RECORD
+    for (int d = 0; d < DM; ++d) j->x[(int64_t)d * N + i] = x[d];
+    j->ll[i] = ll; j->lp[i] = lp; j->tag[i] = (uint8_t)tag;
+    j->nacc[i] += na;
+    if (o->accumulate) j->nb_rec[i] += nb;
+  }
+  return NULL;
+}
+
+int or_rj_run(const or_rj_model* a, const or_rj_model* b, uint64_t seed, int64_t N, uint8_t* tag,
+              int draw_tags, const double* xa, const double* xb, double* x, double* ll, double* lp, uint64_t* nacc, uint64_t* nb_rec,
+              const or_run_opts* o, double* rec_x, double* rec_ll, double* rec_lp, uint8_t* rec_tag,
+              uint64_t* accept_bits, int nthreads) {
+  rj_prep R;
+  memset(&R, 0, sizeof R);
+  R.m[0] = a; R.m[1] = b;
+  R.DM = a->ndim > b->ndim ? a->ndim : b->ndim;
+  if (a->ndim < 1 || b->ndim < 1 || R.DM > 256 || N < 1 || o->nskip < 1) return -1;
+  double one = 1.0;
+  for (int k = 0; k < 2; ++k) {
+    const or_rj_model* q = R.m[k];
+    or_model m = {q->ndim, q->lik_kind, q->lik_params, q->n_lik, q->prior_kind, q->prior_params,
+                  q->n_prior, MCG_PROP_GAUSS, &one, 1, NULL};
+    if (prep_model(&m, &R.p[k]) != 0) return -1;
+    R.logp[k] = log(q->model_prior);
+  }
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > N) nthreads = (int)N;
+  rj_job* jobs = (rj_job*)calloc((size_t)nthreads, sizeof(rj_job));
+  pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+  int64_t per = (N + nthreads - 1) / nthreads;
+  for (int t = 0; t < nthreads; ++t) {
+    rj_job* j = &jobs[t];
+    j->R = &R; j->seed = seed; j->N = N; j->o = o; j->tag = tag; j->x = x; j->ll = ll; j->lp = lp;
+    j->draw_tags = draw_tags; j->xa = xa; j->xb = xb; j->rec_x = rec_x; j->rec_ll = rec_ll; j->rec_lp = rec_lp;
+    j->rec_tag = rec_tag; j->bits = accept_bits; j->nacc = nacc; j->nb_rec = nb_rec;
+    j->i0 = t * per; j->i1 = (t + 1) * per;
+    if (j->i0 > N) j->i0 = N;
+    if (j->i1 > N) j->i1 = N;
+  }
+  /* accept bits of one 64-chain word must come from one thread: split on 64-chain blocks */
+  if (nthreads > 1) {
+    int64_t blocks = (N + 63) / 64, bper = (blocks + nthreads - 1) / nthreads;
+    for (int t = 0; t < nthreads; ++t) {
+      jobs[t].i0 = t * bper * 64; jobs[t].i1 = (t + 1) * bper * 64;
+      if (jobs[t].i0 > N) jobs[t].i0 = N;
+      if (jobs[t].i1 > N) jobs[t].i1 = N;
+    }
+    for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, rj_worker, &jobs[t]);
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+  } else {
+    rj_worker(&jobs[0]);
+  }
+  free(jobs); free(th);
+  prep_free(&R.p[0]); prep_free(&R.p[1]);
+  return 0;
+}
+
+/* ======================================================================================
  * Tile statistics: Chan/Welford pairwise combine + log-space harmonic-mean partials
  * ====================================================================================== */
 static void comb(int D, double* a, const double* b) {

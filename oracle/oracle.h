@@ -83,6 +83,25 @@ typedef struct {
    x [D][N] in/out, ll/lp [N] in/out, nacc [N] in/out (incremented).
    rec_x [n_rec][D][N], rec_ll/rec_lp [n_rec][N], accept_bits [nsteps][ceil(N/64)] u64.
    nthreads: chains are split into contiguous blocks, one per thread. */
+/* ---- reversible jump between two models (Mcmc.make_rjmcmc_sampler, mcmc.ml:89-153) ----
+   jump / into kinds and parameter layouts as MCG_RJ_JUMP_* in include/mcg.h; kd = or_kd tree */
+typedef struct {
+  int32_t ndim;
+  int32_t lik_kind; const double* lik_params; int64_t n_lik;
+  int32_t prior_kind; const double* prior_params; int64_t n_prior;
+  int32_t jump_kind; const double* jump_params; int64_t n_jump;
+  int32_t into_kind; const double* into_params; int64_t n_into;
+  const void* kd;
+  double model_prior;
+} or_rj_model;
+/* xa [D_A][N], xb [D_B][N] start points; x [Dmax][N] out (final states); tag [N] (in: start
+   models unless draw_tags; out: final); rec_* [n_rec][..][N]; nb_rec [N] += recorded samples in
+   model B when o->accumulate */
+int or_rj_run(const or_rj_model* a, const or_rj_model* b, uint64_t seed, int64_t N, uint8_t* tag,
+              int draw_tags, const double* xa, const double* xb, double* x, double* ll, double* lp, uint64_t* nacc, uint64_t* nb_rec,
+              const or_run_opts* o, double* rec_x, double* rec_ll, double* rec_lp,
+              uint8_t* rec_tag, uint64_t* accept_bits, int nthreads);
+
 int or_mh_run(const or_model* m, uint64_t seed, uint32_t chain_offset, int64_t N, uint64_t step0,
               double* x, double* ll, double* lp, uint64_t* nacc, const or_run_opts* o,
               double* rec_x, double* rec_ll, double* rec_lp, uint64_t* accept_bits,

@@ -327,3 +327,54 @@ def nested_merge(runs):
     log_ev = half + _lse(low, high)
     log_dev = high + np.log1p(-np.exp(low - high))
     return order, log_ev, log_dev, w - log_ev
+
+
+class OrRjModel(C.Structure):
+    _fields_ = [("ndim", C.c_int32),
+                ("lik_kind", C.c_int32), ("lik_params", _dp), ("n_lik", C.c_int64),
+                ("prior_kind", C.c_int32), ("prior_params", _dp), ("n_prior", C.c_int64),
+                ("jump_kind", C.c_int32), ("jump_params", _dp), ("n_jump", C.c_int64),
+                ("into_kind", C.c_int32), ("into_params", _dp), ("n_into", C.c_int64),
+                ("kd", C.c_void_p), ("model_prior", C.c_double)]
+
+
+def rj_run(model_a, model_b, seed, xa, xb, nbin=0, nskip=1, n_rec=1, tags=None, nthreads=8):
+    """Restated Mcmc.rjmcmc_array over N chains.  model_x: dicts with ndim, lik (kind, params),
+    prior (kind, params), jump (kind, params), into (kind, params), kd (KdTree or None), p."""
+    keep = []
+
+    def mk(m):
+        arrs = [f64(m[k][1] if len(m[k][1]) else [0.0]) for k in ("lik", "prior", "jump", "into")]
+        keep.extend(arrs)
+        kd = m.get("kd")
+        return OrRjModel(m["ndim"], m["lik"][0], dptr(arrs[0]), len(m["lik"][1]), m["prior"][0],
+                         dptr(arrs[1]), len(m["prior"][1]), m["jump"][0], dptr(arrs[2]),
+                         len(m["jump"][1]), m["into"][0], dptr(arrs[3]), len(m["into"][1]),
+                         kd.ptr if kd is not None else None, m["p"])
+
+    a, b = mk(model_a), mk(model_b)
+    xa, xb = f64(xa), f64(xb)
+    N = xa.shape[1]
+    DM = max(model_a["ndim"], model_b["ndim"])
+    draw = tags is None
+    tag = np.zeros(N, np.uint8) if draw else np.ascontiguousarray(tags, np.uint8)
+    x = np.zeros((DM, N)); ll = np.zeros(N); lp = np.zeros(N)
+    nacc = np.zeros(N, np.uint64); nb = np.zeros(N, np.uint64)
+    nsteps = nbin + max(0, n_rec - 1) * nskip
+    rec_x = np.zeros((n_rec, DM, N)); rec_ll = np.zeros((n_rec, N)); rec_lp = np.zeros((n_rec, N))
+    rec_tag = np.zeros((n_rec, N), np.uint8)
+    bits = np.zeros((max(nsteps, 1), (N + 63) // 64), np.uint64)
+    o = OrRunOpts(nbin, nskip, n_rec, 1, 1, 1, 1)
+    u8 = lambda v: v.ctypes.data_as(C.POINTER(C.c_uint8))
+    L = lib()
+    L.or_rj_run.argtypes = [C.POINTER(OrRjModel), C.POINTER(OrRjModel), C.c_uint64, C.c_int64,
+                            C.POINTER(C.c_uint8), C.c_int, _dp, _dp, _dp, _dp, _dp, _u64p, _u64p,
+                            C.POINTER(OrRunOpts), _dp, _dp, _dp, C.POINTER(C.c_uint8), _u64p, C.c_int]
+    L.or_rj_run.restype = C.c_int
+    rc = L.or_rj_run(C.byref(a), C.byref(b), seed, N, u8(tag), int(draw), dptr(xa), dptr(xb), dptr(x),
+                     dptr(ll), dptr(lp), u64ptr(nacc), u64ptr(nb), C.byref(o), dptr(rec_x),
+                     dptr(rec_ll), dptr(rec_lp), u8(rec_tag), u64ptr(bits), nthreads)
+    if rc != 0:
+        raise RuntimeError("or_rj_run failed: %d" % rc)
+    return dict(x=x, ll=ll, lp=lp, tag=tag, nacc=nacc, nb=nb, rec_x=rec_x, rec_ll=rec_ll,
+                rec_lp=rec_lp, rec_tag=rec_tag, bits=bits[:nsteps])
