@@ -271,6 +271,17 @@ int mcg_nested_merge(int32_t nruns, const int64_t* n_total, const int64_t* nlive
                      const double* ll, int64_t* order, double* log_ev, double* log_dev,
                      double* log_wts);
 
+/* ---- kD-tree evidence integrals over samples (Evidence.Make(MO), evidence.ml:66-221) ----
+   pts [n][ndim] row-major, ll, lp [n]: one sample array (several chains: concatenated).
+   evidence_direct ?n (evidence.ml:145-156): duplicates removed, kD tree of the samples
+   (kd_tree.ml:155-175), cells with fewer than nbox samples, sum of cell volume x mean posterior.
+   evidence_lebesgue ?n ?eps (evidence.ml:194-221): samples up to the first gap > eps in 1/L,
+   prior mass of their cells (median prior) / mean 1/L.  Host computation; deterministic. */
+int mcg_evidence_direct(int32_t ndim, int64_t n, const double* pts, const double* ll, const double* lp,
+                        int64_t nbox, double* out);
+int mcg_evidence_lebesgue(int32_t ndim, int64_t n, const double* pts, const double* ll, const double* lp,
+                          int64_t nbox, double eps, double* out);
+
 /* ---- Read_write text formats (read_write.ml:19-101) ----
    A Read_write file is rows of doubles printed with OCaml Printf "%g" (C %g; nan prints as
    "nan"), separated by single spaces, one row per line:

@@ -122,3 +122,13 @@ def rjmcmc_evidence_ratio(samples):
     """Mcmc.rjmcmc_evidence_ratio (mcmc.ml:144-146): #A / #B."""
     na, nb = samples.counts if isinstance(samples, RjSamples) else rjmcmc_model_counts(samples)
     return float(na) / float(nb)
+
+
+def remove_repeat_samples(samples, chain=0):
+    """Mcmc.remove_repeat_samples (=) (mcmc.ml:74-82) on one chain of a Samples: keeps record 0
+    and every record whose value differs from the previous one.  Returns (pts (m, D), ll, lp)."""
+    x = np.asarray(samples.value)[:, :, chain]
+    keep = np.ones(len(x), bool)
+    keep[1:] = np.any(x[1:] != x[:-1], axis=1)
+    return (x[keep].copy(), np.asarray(samples.log_likelihood)[keep, chain].copy(),
+            np.asarray(samples.log_prior)[keep, chain].copy())
