@@ -7,8 +7,12 @@
 // generation after the stopping one into no-ops, so the host only synchronises once per batch.
 // evidence_error_and_weights (nested.ml:81-120) runs once on the host over the final points.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -44,42 +48,83 @@ double lse_host(double a, double b) {            // Stats.log_sum_logs (stats.ml
   return a + std::log1p(std::exp(b - a));
 }
 
-// nested.ml:81-120; dead point i was retired with n - (i mod k) live points
+// nested.ml:81-120; dead point i was retired with n - (i mod k) live points.
+// The reference is one loop of four log-sums per point: two running sums (low, high) and two
+// weight updates.  The running sums fold blocks of iterations in parallel (below); each weight
+// receives at most two contributions, from the neighbouring iterations, so the weights are
+// computed per index in parallel by replaying exactly those contributions in loop order.
 void evidence_weights(int64_t n, int64_t nlive, int64_t k, const double* ll, double* log_ev,
                       double* log_dev, double* wts) {
   const double log_half = -0.69314718055994530942;
   const int64_t ilive = n - nlive;
   std::vector<double> prefix((size_t)k + 1, 0.0);
   for (int64_t j = 0; j < k; ++j) prefix[j + 1] = prefix[j] + std::log1p(-1.0 / (double)(nlive - j));
-  for (int64_t i = 0; i < n; ++i) wts[i] = -HUGE_VAL;
-  double low = -HUGE_VAL, high = -HUGE_VAL;
-  for (int64_t i = 0; i < ilive; ++i) {
+  auto ldv_dead = [&](int64_t i) {
+    if (k == 1) return std::log(1.0 / (double)nlive) + (double)i * std::log1p(-1.0 / (double)nlive);
     const int64_t j = i % k, g = i / k;
-    double log_dv = std::log(1.0 / (double)(nlive - j)) + ((double)g * prefix[k] + prefix[j]);
-    if (k == 1) log_dv = std::log(1.0 / (double)nlive) + (double)i * std::log1p(-1.0 / (double)nlive);
-    const double dl = log_dv + ll[i], dh = log_dv + ll[i + 1];
-    low = lse_host(low, dl);
-    high = lse_host(high, dh);
-    wts[i] = lse_host(wts[i], log_half + dl);
-    wts[i + 1] = lse_host(wts[i + 1], log_half + dh);
-  }
-  double log_dv;
+    return std::log(1.0 / (double)(nlive - j)) + ((double)g * prefix[k] + prefix[j]);
+  };
+  double ldv_live;
   if (k == 1) {
-    log_dv = std::log(1.0 / (double)nlive) + (double)(ilive - 1) * std::log1p(-1.0 / (double)nlive);
+    ldv_live = std::log(1.0 / (double)nlive) + (double)(ilive - 1) * std::log1p(-1.0 / (double)nlive);
   } else {
     const int64_t g = ilive / k, j = ilive % k;
-    log_dv = ((double)g * prefix[k] + prefix[j]) + std::log(1.0 / (double)nlive);
+    ldv_live = ((double)g * prefix[k] + prefix[j]) + std::log(1.0 / (double)nlive);
   }
-  for (int64_t i = ilive; i < n; ++i) {
-    const double dl = log_dv + ll[i - 1], dh = log_dv + ll[i];
-    low = lse_host(low, dl);
-    high = lse_host(high, dh);
-    wts[i - 1] = lse_host(wts[i - 1], log_half + dl);
-    wts[i] = lse_host(wts[i], log_half + dh);
+  // iteration i's (dl, dh): first loop i < ilive, second loop i >= ilive (nested.ml:90-113)
+  auto dl = [&](int64_t i) { return i < ilive ? ldv_dead(i) + ll[i] : ldv_live + ll[i - 1]; };
+  auto dh = [&](int64_t i) { return i < ilive ? ldv_dead(i) + ll[i + 1] : ldv_live + ll[i]; };
+  // running sums: sequential log-sums over blocks of kEvBlock iterations (in parallel), then a
+  // sequential log-sum of the block results -- the reference's fold exactly for n <= kEvBlock,
+  // within rounding beyond (the oracle folds the same blocks, oracle.c or_evidence_weights)
+  constexpr int64_t kEvBlock = 65536;
+  const int64_t nb = (n + kEvBlock - 1) / kEvBlock;
+  std::vector<double> blow((size_t)nb, -HUGE_VAL), bhigh((size_t)nb, -HUGE_VAL);
+  std::vector<std::thread> tb;
+  const int TB = (int)std::max<int64_t>(1, std::min<int64_t>(nb, 8));
+  for (int t = 0; t < TB; ++t)
+    tb.emplace_back([&, t] {
+      for (int64_t b = t; b < nb; b += TB) {
+        double lo = -HUGE_VAL, hi = -HUGE_VAL;
+        for (int64_t i = b * kEvBlock; i < std::min(n, (b + 1) * kEvBlock); ++i) {
+          lo = lse_host(lo, dl(i));
+          hi = lse_host(hi, dh(i));
+        }
+        blow[(size_t)b] = lo;
+        bhigh[(size_t)b] = hi;
+      }
+    });
+  // weight m: first loop dh(m-1) then dl(m); second loop dh(m) then dl(m+1)
+  auto weight = [&](int64_t m) {
+    double w = -HUGE_VAL;
+    if (m >= 1 && m - 1 < ilive) w = lse_host(w, log_half + dh(m - 1));
+    if (m < ilive) w = lse_host(w, log_half + dl(m));
+    if (m >= ilive) w = lse_host(w, log_half + dh(m));
+    if (m + 1 >= ilive && m + 1 < n) w = lse_host(w, log_half + dl(m + 1));
+    return w;
+  };
+  const int T = (int)std::max<unsigned>(1, std::min<unsigned>(14, std::thread::hardware_concurrency()));
+  std::vector<std::thread> tw;
+  for (int t = 0; t < T; ++t)
+    tw.emplace_back([&, t] {
+      for (int64_t m = t * n / T; m < (t + 1) * n / T; ++m) wts[m] = weight(m);
+    });
+  for (auto& x : tw) x.join();
+  for (auto& x : tb) x.join();
+  double low = -HUGE_VAL, high = -HUGE_VAL;
+  for (int64_t b = 0; b < nb; ++b) {
+    low = lse_host(low, blow[(size_t)b]);
+    high = lse_host(high, bhigh[(size_t)b]);
   }
   *log_ev = log_half + lse_host(low, high);
   *log_dev = high + std::log1p(-std::exp(low - high));
-  for (int64_t i = 0; i < n; ++i) wts[i] = wts[i] - *log_ev;
+  const double le = *log_ev;
+  tw.clear();
+  for (int t = 0; t < T; ++t)
+    tw.emplace_back([&, t] {
+      for (int64_t m = t * n / T; m < (t + 1) * n / T; ++m) wts[m] = wts[m] - le;
+    });
+  for (auto& x : tw) x.join();
 }
 
 }  // namespace
@@ -167,6 +212,12 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   a.k1 = (uint32_t)(ctx->opts.seed >> 32);
 
   // initial live set: prior draws, evaluated, stably sorted by likelihood (nested.ml:126-132)
+  const bool prof = std::getenv("MCG_NESTED_PROFILE") != nullptr;
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+    return std::chrono::duration<double, std::milli>(b - a).count();
+  };
+  const auto t_start = now();
   HC(init(a, B.keys[0].l(), B.keys[0].t(), B.keys[0].s(), s), "nested init");
   bool in_tmp = false;
   HC(launch_sort_keys(B.keys[0].l(), B.keys[0].t(), B.keys[0].s(), B.keys[1].l(), B.keys[1].t(),
@@ -217,8 +268,13 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
       HC(launch_retire(a, D, s), "nested retire");
       HC(launch_estimate(a, s), "nested estimate");
       bool nk_tmp = false;
-      HC(launch_sort_keys(B.newk.l(), B.newk.t(), B.newk.s(), B.newk_tmp.l(), B.newk_tmp.t(),
-                          B.newk_tmp.s(), k, &nk_tmp, s, a.st), "sort new keys");
+      if (k <= 4096) {
+        HC(launch_sort_new_small(a, B.newk_tmp.l(), B.newk_tmp.t(), B.newk_tmp.s(), s), "sort new keys");
+        nk_tmp = true;
+      } else {
+        HC(launch_sort_keys(B.newk.l(), B.newk.t(), B.newk.s(), B.newk_tmp.l(), B.newk_tmp.t(),
+                            B.newk_tmp.s(), k, &nk_tmp, s, a.st), "sort new keys");
+      }
       KeyBuf& nk = nk_tmp ? B.newk_tmp : B.newk;
       HC(launch_merge_new(a, nxt.l(), nxt.t(), nxt.s(), nk.l(), nk.t(), nk.s(), s), "merge keys");
       HC(launch_stop(a, nxt.l(), s), "stop test");
@@ -241,17 +297,19 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
     if (st.stopped) break;
     batch = std::min<int64_t>(batch * 2, 64);
   }
+  const auto t_gen = now();
   // final: dead points in retirement order, then the live set ascending (nested.ml:143)
   const int64_t ndead = st.gen_done * k;
   const int64_t ntot = ndead + n;
   KeyBuf& fin = B.keys[(base + st.gen_done) % 2];
   NestedState& R = ctx->nested;
-  R.pts.assign((size_t)ntot * D, 0.0);
-  R.ll.assign((size_t)ntot, 0.0);
-  R.lp.assign((size_t)ntot, 0.0);
-  R.wts.assign((size_t)ntot, 0.0);
+  // the dead rows stay on the device (B.dead_x) until mcg_nested_get copies them straight into
+  // the caller's buffer; the host keeps ll / lp (for the weights) and the final live rows
+  R.pts.assign((size_t)n * D, 0.0);
+  R.ll.resize((size_t)ntot);
+  R.lp.resize((size_t)ntot);
+  R.wts.resize((size_t)ntot);
   if (ndead > 0) {
-    HC(hipMemcpy(R.pts.data(), B.dead_x.p, ndead * D * 8, hipMemcpyDeviceToHost), "copy dead");
     HC(hipMemcpy(R.ll.data(), B.dead_ll.p, ndead * 8, hipMemcpyDeviceToHost), "copy dead");
     HC(hipMemcpy(R.lp.data(), B.dead_lp.p, ndead * 8, hipMemcpyDeviceToHost), "copy dead");
   }
@@ -263,11 +321,15 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   HC(hipMemcpy(llp.data(), B.lp.p, n * 8, hipMemcpyDeviceToHost), "copy live");
   for (int64_t j = 0; j < n; ++j) {
     const int sl = slots[(size_t)j];
-    std::memcpy(&R.pts[(size_t)(ndead + j) * D], &lx[(size_t)sl * D], sizeof(double) * D);
+    std::memcpy(&R.pts[(size_t)j * D], &lx[(size_t)sl * D], sizeof(double) * D);
     R.ll[(size_t)(ndead + j)] = lll[(size_t)sl];
     R.lp[(size_t)(ndead + j)] = llp[(size_t)sl];
   }
+  const auto t_copy = now();
   evidence_weights(ntot, n, k, R.ll.data(), &R.log_ev, &R.log_dev, R.wts.data());
+  if (prof)
+    std::fprintf(stderr, "mcg_nested: generations %.1f ms, final copies %.1f ms, weights %.1f ms\n",
+                 ms(t_start, t_gen), ms(t_gen, t_copy), ms(t_copy, now()));
   R.n_total = ntot;
   R.n_dead = ndead;
   R.n_gen = st.gen_done;
@@ -287,7 +349,15 @@ int mcg_nested_get(mcg_ctx* ctx, double* pts, double* ll, double* lp, double* lo
   if (!ctx) return MCG_EINVAL;
   const NestedState& R = ctx->nested;
   if (R.n_total == 0) return set_error(ctx, MCG_ESTATE, "no nested run");
-  if (pts) std::copy(R.pts.begin(), R.pts.end(), pts);
+  if (pts) {
+    const int64_t D = (int64_t)(R.pts.size() / (size_t)R.nlive);
+    if (R.n_dead > 0) {
+      int rc = hip_check(ctx, hipMemcpy(pts, ctx->nested_bufs->b.dead_x.p, (size_t)(R.n_dead * D) * 8,
+                                        hipMemcpyDeviceToHost), "copy dead points");
+      if (rc) return rc;
+    }
+    std::copy(R.pts.begin(), R.pts.end(), pts + R.n_dead * D);
+  }
   if (ll) std::copy(R.ll.begin(), R.ll.end(), ll);
   if (lp) std::copy(R.lp.begin(), R.lp.end(), lp);
   if (log_wts) std::copy(R.wts.begin(), R.wts.end(), log_wts);

@@ -52,19 +52,30 @@ struct NestArgs {
   uint64_t seed_unused;
 };
 
-// ---- one constrained DE-MCMC walker per lane (draw_new_live_point, nested.ml:50-74) ----
-template <int D, int LIK>
+// ---- constrained DE-MCMC walkers (draw_new_live_point, nested.ml:50-74) ----
+// P lanes per walker (P in {1, 2, 4}; the MH kernel's layout: lane `sub` owns the 4-dim blocks
+// c = sub, sub + P, ...).  Every lane of a walker draws the same Philox words, so the DE indices,
+// scale, accept decision and start point agree without communication; the log-target is the
+// canonical sum reduced across the P lanes (reduce_canon).  The DE partner rows of step s + 1
+// depend only on the RNG, so they are loaded while step s computes (one step of prefetch).
+template <int D, int LIK, int P>
 __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
+  using Lay = Layout<D, P>;
+  constexpr int NL = Lay::NL;
   __shared__ double2 s_lt[kLogTabN];                 // math tables staged in LDS (gathers)
   __shared__ double2 s_at[kAngTabN];
   for (int i = threadIdx.x; i < kLogTabN; i += blockDim.x) s_lt[i] = kLogTab[i];
   for (int i = threadIdx.x; i < kAngTabN; i += blockDim.x) s_at[i] = kAngTab[i];
   __syncthreads();
   if (a.st->stopped) return;
-  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= a.k) return;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int sub = (int)(tid & (P - 1));
+  const int64_t w = tid / P;
+  const bool active = w < a.k;
+  // inactive lanes of a partial wave run walker 0's arithmetic (shuffle partners) but store nothing
+  const int64_t wc = active ? w : 0;
   const Rng rng{a.k0, a.k1};
-  const uint32_t wid = (uint32_t)(a.mrep + w);
+  const uint32_t wid = (uint32_t)(a.mrep + wc);
   const double thr = a.key_ll[a.k - 1];
   const uint32_t n = (uint32_t)a.n;
   // start: a uniformly random live point satisfying the constraint (nested.ml:63); with k = 1
@@ -79,16 +90,38 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
     }
   }
   if (start < 0) start = a.key_slot[a.k - 1];
-  double cur[D], y[D];
+  double cur[NL], y[NL], bi[NL], bj[NL];
+  auto load_row = [&](double* dst, int64_t row) {
+    const double* __restrict__ src = a.x + row * D;
 #pragma unroll
-  for (int d = 0; d < D; ++d) cur[d] = a.x[start * D + d];
-  double cur_l = (a.ll[start] >= thr) ? a.lp[start] : -__builtin_inf();   // mcmc_logl, :54-59
-  for (int64_t s = 0; s < a.nmcmc; ++s) {
-    // differential_evolution_proposal (mcmc.ml:198-218)
+    for (int i = 0; i < Lay::NCL; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        dst[4 * i + q] = Lay::valid(sub, i, q) ? src[Lay::dim(sub, i, q)] : 0.0;
+  };
+  // differential_evolution_proposal's pick_samples (mcmc.ml:199-203): i, then j != i
+  auto pick = [&](int64_t s, uint32_t& i, uint32_t& j) {
     const u32x4 ri = rng(wid, (uint32_t)s, CALL_DE_IDX, TAG_NEST_WALK, 0u);
-    const uint32_t i = randint(ri.x, ri.y, n);
+    i = randint(ri.x, ri.y, n);
     const uint32_t jj = randint(ri.z, ri.w, n - 1);
-    const uint32_t j = jj + (jj >= i ? 1u : 0u);
+    j = jj + (jj >= i ? 1u : 0u);
+  };
+  load_row(cur, start);
+  double cur_l = (a.ll[start] >= thr) ? a.lp[start] : -__builtin_inf();   // mcmc_logl, :54-59
+  if (a.nmcmc > 0) {
+    uint32_t i0, j0;
+    pick(0, i0, j0);
+    load_row(bi, i0);
+    load_row(bj, j0);
+  }
+  for (int64_t s = 0; s < a.nmcmc; ++s) {
+    double ni[NL], nj[NL];
+    if (s + 1 < a.nmcmc) {                             // prefetch step s + 1's partner rows
+      uint32_t i1, j1;
+      pick(s + 1, i1, j1);
+      load_row(ni, i1);
+      load_row(nj, j1);
+    }
     const u32x4 rs = rng(wid, (uint32_t)s, CALL_DE_SCALE, TAG_NEST_WALK, 0u);
     double dsc;
     if (a.mode_hop != 0.0 && u53(rs.x, rs.y) < a.mode_hop) {
@@ -98,27 +131,39 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
       normal_pair(rs.z, rs.w, z0, z1, s_lt, s_at);
       dsc = a.sigma_de * z0;
     }
-    const double* __restrict__ xi = a.x + (int64_t)i * D;
-    const double* __restrict__ xj = a.x + (int64_t)j * D;
 #pragma unroll
-    for (int d = 0; d < D; ++d) y[d] = cur[d] + dsc * (xj[d] - xi[d]);
-    const double lly = eval_lik<D, 1, LIK>(y, 0, a.m, a.m.lik);
-    const double ml = (lly >= thr) ? eval_prior<D, 1>(y, 0, a.m, a.m.pri) : -__builtin_inf();
+    for (int d = 0; d < NL; ++d) y[d] = cur[d] + dsc * (bj[d] - bi[d]);
+    const double lly = eval_lik<D, P, LIK>(y, sub, a.m, a.m.lik);
+    const double lpy = eval_prior<D, P>(y, sub, a.m, a.m.pri);
+    const double ml = (lly >= thr) ? lpy : -__builtin_inf();
     const double ratio = (((ml + 0.0) - (cur_l + 0.0)) + 0.0) - 0.0;   // mcmc.ml:47-48
     const u32x4 ra = rng(wid, (uint32_t)s, CALL_ACCEPT, TAG_NEST_WALK, 0u);
     if (plog(u53(ra.x, ra.y), s_lt) < ratio) {
 #pragma unroll
-      for (int d = 0; d < D; ++d) cur[d] = y[d];
+      for (int d = 0; d < NL; ++d) cur[d] = y[d];
       cur_l = ml;
     }
-  }
-  const double nl = eval_lik<D, 1, LIK>(cur, 0, a.m, a.m.lik);
-  const double np = eval_prior<D, 1>(cur, 0, a.m, a.m.pri);
+    if (s + 1 < a.nmcmc) {
 #pragma unroll
-  for (int d = 0; d < D; ++d) a.nx[w * D + d] = cur[d];
-  a.nll[w] = nl;
-  a.nlp[w] = np;
-  if (!(nl >= thr)) a.st->error = 1;                 // nested.ml:70-72 -> Failure
+      for (int d = 0; d < NL; ++d) {
+        bi[d] = ni[d];
+        bj[d] = nj[d];
+      }
+    }
+  }
+  const double nl = eval_lik<D, P, LIK>(cur, sub, a.m, a.m.lik);
+  const double np = eval_prior<D, P>(cur, sub, a.m, a.m.pri);
+  if (!active) return;
+#pragma unroll
+  for (int i = 0; i < Lay::NCL; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (Lay::valid(sub, i, q)) a.nx[w * D + Lay::dim(sub, i, q)] = cur[4 * i + q];
+  if (sub == 0) {
+    a.nll[w] = nl;
+    a.nlp[w] = np;
+    if (!(nl >= thr)) a.st->error = 1;               // nested.ml:70-72 -> Failure
+  }
 }
 
 // ---- prior draws of the initial live set (nested.ml:126-129, Stats.draw_uniform) ----
@@ -149,8 +194,12 @@ __global__ void __launch_bounds__(256) nest_init_kernel(const NestArgs a, double
 
 template <int D, int LIK>
 hipError_t launch_nest_walk(const NestArgs& a, hipStream_t st) {
-  const int64_t grid = (a.k + 255) / 256;
-  hipLaunchKernelGGL((nest_walk_kernel<D, LIK>), dim3((unsigned)grid), dim3(256), 0, st, a);
+  // lanes per walker: the separable likelihoods split the dims over 4 (or 2) lanes when D is a
+  // multiple of 16 (8), which gives the few-thousand-walker generations 4x (2x) the lanes
+  constexpr bool sep = LIK == MCG_LIK_DIAG_GAUSS || LIK == MCG_LIK_GAUSS_SHELL || LIK == MCG_LIK_FLAT;
+  constexpr int P = (sep && D % 16 == 0) ? 4 : (sep && D % 8 == 0) ? 2 : 1;
+  const int64_t grid = (a.k * P + 255) / 256;
+  hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P>), dim3((unsigned)grid), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
@@ -169,6 +218,7 @@ hipError_t launch_merge_new(const NestArgs& a, double* out_ll, long long* out_ti
                             const double* new_ll, const long long* new_tie, const int* new_slot,
                             hipStream_t st);
 hipError_t launch_retire(const NestArgs& a, int D, hipStream_t st);
+hipError_t launch_sort_new_small(const NestArgs& a, double* oll, long long* otie, int* oslot, hipStream_t st);
 hipError_t launch_estimate(const NestArgs& a, hipStream_t st);
 hipError_t launch_stop(const NestArgs& a, const double* final_ll, hipStream_t st);
 

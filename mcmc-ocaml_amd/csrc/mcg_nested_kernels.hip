@@ -46,7 +46,7 @@ __global__ void __launch_bounds__(256) sort_chunks_kernel(double* ll, long long*
   for (int size = 2; size <= kChunk; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       for (int p = threadIdx.x; p < kChunk / 2; p += blockDim.x) {
-        const int i = 2 * stride * (p / stride) + (p % stride);
+        const int i = ((p & ~(stride - 1)) << 1) | (p & (stride - 1));   // stride is a power of 2
         const int j = i + stride;
         const bool up = (i & size) == 0;
         const bool gt = key_less(sl[j], st[j], sl[i], st[i]);
@@ -109,6 +109,55 @@ hipError_t launch_sort_keys(double* ll, long long* tie, int* slot, double* tll, 
   }
   *result_in_tmp = in_tmp;
   return hipSuccess;
+}
+
+// Sort this generation's k <= 4096 new keys in one workgroup (bitonic, 1024 threads, LDS).  The
+// new keys' ties are -(mrep + j + 1), decreasing in j, so the key order is (ll ascending, j
+// descending) and only (ll, j) enter LDS (48 KiB); tie and slot are rebuilt from j on the way out.
+constexpr int kSmallSort = 4096;
+
+__global__ void __launch_bounds__(1024) sort_new_small_kernel(const NestArgs a, double* oll,
+                                                              long long* otie, int* oslot) {
+  if (a.st->stopped) return;
+  __shared__ double sl[kSmallSort];
+  __shared__ int sj[kSmallSort];
+  const int k = (int)a.k;
+  int L = 2;
+  while (L < k) L <<= 1;
+  for (int i = threadIdx.x; i < L; i += blockDim.x) {
+    sl[i] = i < k ? a.newk_ll[i] : __builtin_inf();
+    sj[i] = i < k ? i : -1;
+  }
+  __syncthreads();
+  for (int size = 2; size <= L; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int p = threadIdx.x; p < L / 2; p += blockDim.x) {
+        const int i = ((p & ~(stride - 1)) << 1) | (p & (stride - 1));   // stride is a power of 2
+        const int j = i + stride;
+        const bool up = (i & size) == 0;
+        const double li = sl[i], lj = sl[j];
+        const int ji = sj[i], jj = sj[j];
+        const bool j_less = lj < li || (lj == li && jj > ji);      // key j < key i
+        if (j_less == up) {
+          sl[i] = lj; sl[j] = li;
+          sj[i] = jj; sj[j] = ji;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = threadIdx.x; i < k; i += blockDim.x) {
+    const int j = sj[i];
+    oll[i] = sl[i];
+    otie[i] = -(long long)(a.mrep + j + 1);
+    oslot[i] = a.newk_slot[j];
+  }
+}
+
+hipError_t launch_sort_new_small(const NestArgs& a, double* oll, long long* otie, int* oslot, hipStream_t s) {
+  if (a.k > kSmallSort) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(sort_new_small_kernel, dim3(1), dim3(1024), 0, s, a, oll, otie, oslot);
+  return hipGetLastError();
 }
 
 // survivors keys[k..n) + k sorted new keys -> out[0..n)

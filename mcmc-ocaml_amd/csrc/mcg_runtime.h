@@ -34,7 +34,8 @@ struct KdState {
 };
 
 struct NestedState {
-  // last run, host copies (dead points in retirement order, then live ascending)
+  // last run: ll, lp, wts of every point (dead in retirement order, then live ascending); pts
+  // holds the final live rows only (the dead rows stay in the device dead buffer)
   std::vector<double> pts, ll, lp, wts;
   int64_t n_total = 0, n_dead = 0, n_gen = 0, nlive = 0;
   double log_ev = 0.0, log_dev = 0.0;

@@ -89,10 +89,17 @@ type prior =
   | Box of float array * float array * float
   | Open_box of float array * float array * float
 
+type mix_component =
+  | Mix_gauss of float array
+  | Mix_shift_uniform of float array * float array
+  | Mix_wrap of float array * float array * float array
+  | Mix_interp
+
 type proposal =
   | Gauss of float array
   | Uniform_wrapping of float array * float array * float array
   | Interp of float array array * float array * float array
+  | Mixture of (float * mix_component * bool) list * (float array array * float array * float array) option
 
 let dims = Hashtbl.create 8
 
@@ -139,6 +146,21 @@ let set_model ctx lik pri prop =
     check ctx (c_set_proposal ctx 2l (carr p) (Unsigned.Size_t.of_int (Array.length p)))
   | Some (Interp (pts, lo, hi)) ->
     check ctx (c_set_kd ctx (carr (flatten pts)) (Int64.of_int (Array.length pts)) (carr lo) (carr hi))
+  | Some (Mixture (comps, tree)) ->
+    (* Mcmc.combine_jump_proposals (mcmc.ml:165-185): ncomp, then p, kind, ljp mode, params *)
+    (match tree with
+     | Some (pts, lo, hi) ->
+       check ctx (c_set_kd ctx (carr (flatten pts)) (Int64.of_int (Array.length pts)) (carr lo) (carr hi))
+     | None -> ());
+    let comp (p, c, density) =
+      let m = if density then 1.0 else 0.0 in
+      match c with
+      | Mix_gauss s -> Array.append [| p; 1.0; m |] s
+      | Mix_shift_uniform (a, b) -> Array.concat [ [| p; 2.0; m |]; a; b ]
+      | Mix_wrap (lo, hi, dx) -> Array.concat [ [| p; 3.0; 0.0 |]; lo; hi; dx ]
+      | Mix_interp -> [| p; 4.0; 1.0 |] in
+    let params = Array.concat ([| float (List.length comps) |] :: List.map comp comps) in
+    check ctx (c_set_proposal ctx 5l (carr params) (Unsigned.Size_t.of_int (Array.length params)))
 
 let reset_counters ctx = check ctx (c_reset_counters ctx)
 
@@ -188,3 +210,189 @@ let nested_evidence ?(epsrel = 0.01) ?(nmcmc = 1000) ?(nlive = 1000) ?(mode_hopp
 
 let log_total_error_estimate log_ev log_dev nlive =
   c_log_total_error log_ev log_dev (Int64.of_int nlive)
+
+(* ---- reversible jump (Mcmc.rjmcmc_array, mcmc.ml:118-132) ---- *)
+type rj_jump =
+  | Rj_gauss of float array
+  | Rj_wrap of float array * float array * float array
+  | Rj_indep_gauss of float array * float array
+  | Rj_interp
+
+type rj_model = {
+  rj_lik : likelihood; rj_prior : prior; rj_jump : rj_jump; rj_into : rj_jump;
+  rj_tree : (float array array * float array * float array) option; rj_model_prior : float }
+
+type rj_model_s
+let rj_model_s : rj_model_s structure typ = structure "mcg_rj_model"
+let m_ndim = field rj_model_s "ndim" int32_t
+let m_lik_kind = field rj_model_s "lik_kind" int32_t
+let m_lik = field rj_model_s "lik_params" (ptr double)
+let m_nlik = field rj_model_s "n_lik" size_t
+let m_pri_kind = field rj_model_s "prior_kind" int32_t
+let m_pri = field rj_model_s "prior_params" (ptr double)
+let m_npri = field rj_model_s "n_prior" size_t
+let m_jump_kind = field rj_model_s "jump_kind" int32_t
+let m_jump = field rj_model_s "jump_params" (ptr double)
+let m_njump = field rj_model_s "n_jump" size_t
+let m_into_kind = field rj_model_s "into_kind" int32_t
+let m_into = field rj_model_s "into_params" (ptr double)
+let m_ninto = field rj_model_s "n_into" size_t
+let m_kd_pts = field rj_model_s "kd_pts" (ptr double)
+let m_kd_m = field rj_model_s "kd_M" int64_t
+let m_kd_low = field rj_model_s "kd_low" (ptr double)
+let m_kd_high = field rj_model_s "kd_high" (ptr double)
+let m_p = field rj_model_s "model_prior" double
+let () = seal rj_model_s
+
+let c_set_rjmcmc = fn "mcg_set_rjmcmc" (ptr void @-> ptr rj_model_s @-> ptr rj_model_s @-> returning int)
+let c_rj_init = fn "mcg_rj_init" (ptr void @-> int64_t @-> ptr uint8_t @-> ptr double @-> ptr double @-> returning int)
+let c_rj_get_models = fn "mcg_rj_get_models" (ptr void @-> ptr uint8_t @-> ptr uint8_t @-> returning int)
+let c_rj_counts = fn "mcg_rj_model_counts" (ptr void @-> ptr uint64_t @-> ptr uint64_t @-> returning int)
+
+let lik_params = function
+  | Flat d -> 0, d, [| 0.0 |]
+  | Diag_gauss (mu, s) -> 1, Array.length mu, Array.append mu s
+  | Fullcov_gauss (mu, u) -> 2, Array.length mu, Array.append mu (flatten u)
+  | Gauss_shell (c, r, w) -> 3, Array.length c, Array.append c [| r; w |]
+  | Gauss_data _ | Cauchy_data _ -> raise (Invalid_argument "rjmcmc: data likelihoods are not supported")
+
+let rj_struct m =
+  let s = make rj_model_s in
+  let kind, nd, lp = lik_params m.rj_lik in
+  let pk, pp = match m.rj_prior with
+    | Flat_prior -> 0, [||]
+    | Box (lo, hi, l) -> 1, Array.concat [ lo; hi; [| l |] ]
+    | Open_box (lo, hi, l) -> 2, Array.concat [ lo; hi; [| l |] ] in
+  let jump = function
+    | Rj_gauss sc -> 1, sc
+    | Rj_wrap (lo, hi, dx) -> 2, Array.concat [ lo; hi; dx ]
+    | Rj_indep_gauss (mu, sg) -> 3, Array.append mu sg
+    | Rj_interp -> 4, [||] in
+  let jk, jp = jump m.rj_jump and ik, ip = jump m.rj_into in
+  let sz a = Unsigned.Size_t.of_int (Array.length a) in
+  let arr a = if Array.length a = 0 then carr [| 0.0 |] else carr a in
+  setf s m_ndim (Int32.of_int nd);
+  setf s m_lik_kind (Int32.of_int kind); setf s m_lik (carr lp); setf s m_nlik (sz lp);
+  setf s m_pri_kind (Int32.of_int pk); setf s m_pri (arr pp); setf s m_npri (sz pp);
+  setf s m_jump_kind (Int32.of_int jk); setf s m_jump (arr jp); setf s m_njump (sz jp);
+  setf s m_into_kind (Int32.of_int ik); setf s m_into (arr ip); setf s m_ninto (sz ip);
+  (match m.rj_tree with
+   | Some (pts, lo, hi) ->
+     setf s m_kd_pts (carr (flatten pts)); setf s m_kd_m (Int64.of_int (Array.length pts));
+     setf s m_kd_low (carr lo); setf s m_kd_high (carr hi)
+   | None ->
+     setf s m_kd_pts (from_voidp double null); setf s m_kd_m 0L;
+     setf s m_kd_low (from_voidp double null); setf s m_kd_high (from_voidp double null));
+  setf s m_p m.rj_model_prior;
+  (s, nd)
+
+let rjmcmc_array ?(nbin = 0) ?(nskip = 1) ctx n (ma : rj_model) (mb : rj_model) (a : mat) (b : mat) =
+  let sa, da = rj_struct ma and sb, db = rj_struct mb in
+  check ctx (c_set_rjmcmc ctx (addr sa) (addr sb));
+  let nch = Bigarray.Array2.dim2 a in
+  check ctx (c_rj_init ctx (Int64.of_int nch) (from_voidp uint8_t null) (bigarray_start array2 a)
+               (bigarray_start array2 b));
+  let dm = max da db in
+  Hashtbl.replace dims ctx dm;
+  let o = make run_opts in
+  setf o r_nbin (Int64.of_int nbin); setf o r_nskip (Int64.of_int nskip); setf o r_nrec (Int64.of_int n);
+  setf o r_rx 1l; setf o r_rllp 1l; setf o r_racc 0l; setf o r_accum 1l; setf o r_append 0l;
+  check ctx (c_run ctx (addr o));
+  let open Bigarray in
+  let xs = Genarray.create float64 c_layout [| n; dm; nch |] in
+  let ll = Array2.create float64 c_layout n nch and lp = Array2.create float64 c_layout n nch in
+  let models = Array2.create int8_unsigned c_layout n nch in
+  check ctx (c_get_records ctx (bptr xs) (bigarray_start array2 ll) (bigarray_start array2 lp)
+               (from_voidp uint64_t null));
+  check ctx (c_rj_get_models ctx (from_voidp uint8_t null) (bigarray_start array2 models));
+  (models, xs, ll, lp)
+
+(* Mcmc.rjmcmc_model_counts / rjmcmc_evidence_ratio (mcmc.ml:134-146) over the last run *)
+let rjmcmc_model_counts ctx =
+  let a = allocate uint64_t Unsigned.UInt64.zero and b = allocate uint64_t Unsigned.UInt64.zero in
+  check ctx (c_rj_counts ctx a b);
+  (Unsigned.UInt64.to_int !@a, Unsigned.UInt64.to_int !@b)
+
+let rjmcmc_evidence_ratio ctx =
+  let na, nb = rjmcmc_model_counts ctx in
+  float na /. float nb
+
+(* ---- Evidence.evidence_direct / evidence_lebesgue (evidence.ml:145-221) ---- *)
+let c_ev_direct = fn "mcg_evidence_direct" (int32_t @-> int64_t @-> ptr double @-> ptr double @-> ptr double @-> int64_t @-> ptr double @-> returning int)
+let c_ev_lebesgue = fn "mcg_evidence_lebesgue" (int32_t @-> int64_t @-> ptr double @-> ptr double @-> ptr double @-> int64_t @-> double @-> ptr double @-> returning int)
+
+let sample_arrays (samples : (float array * float * float) array) =
+  let n = Array.length samples in
+  let d = let (v, _, _) = samples.(0) in Array.length v in
+  let pts = carr (Array.concat (Array.to_list (Array.map (fun (v, _, _) -> v) samples))) in
+  (n, d, pts, carr (Array.map (fun (_, l, _) -> l) samples), carr (Array.map (fun (_, _, p) -> p) samples))
+
+let raise_rc rc = if rc = -1 then raise (Invalid_argument "evidence") else if rc <> 0 then raise (Failure "evidence")
+
+let evidence_direct ?(n = 64) samples =
+  let ns, d, pts, ll, lp = sample_arrays samples in
+  let out = allocate double 0.0 in
+  raise_rc (c_ev_direct (Int32.of_int d) (Int64.of_int ns) pts ll lp (Int64.of_int n) out);
+  !@out
+
+let evidence_lebesgue ?(n = 64) ?(eps = 0.1) samples =
+  let ns, d, pts, ll, lp = sample_arrays samples in
+  let out = allocate double 0.0 in
+  raise_rc (c_ev_lebesgue (Int32.of_int d) (Int64.of_int ns) pts ll lp (Int64.of_int n) eps out);
+  !@out
+
+(* ---- nested replicas: merge runs (mcg_nested_merge) ---- *)
+let c_nested_merge = fn "mcg_nested_merge" (int32_t @-> ptr int64_t @-> ptr int64_t @-> ptr int64_t @-> ptr double @-> ptr int64_t @-> ptr double @-> ptr double @-> ptr double @-> returning int)
+
+(* runs: (log-likelihoods in nested_output order, nlive, k); returns (order, log Z, log dZ, log weights) *)
+let nested_merge (runs : (float array * int * int) list) =
+  let i64 l = CArray.start (CArray.of_list int64_t (List.map Int64.of_int l)) in
+  let lls = Array.concat (List.map (fun (l, _, _) -> l) runs) in
+  let n = Array.length lls in
+  let order = CArray.make int64_t n and w = CArray.make double n in
+  let le = allocate double 0.0 and ld = allocate double 0.0 in
+  raise_rc (c_nested_merge (Int32.of_int (List.length runs))
+              (i64 (List.map (fun (l, _, _) -> Array.length l) runs))
+              (i64 (List.map (fun (_, nl, _) -> nl) runs)) (i64 (List.map (fun (_, _, k) -> k) runs))
+              (carr lls) (CArray.start order) le ld (CArray.start w));
+  (Array.of_list (List.map Int64.to_int (CArray.to_list order)), !@le, !@ld, Array.of_list (CArray.to_list w))
+
+(* ---- Read_write text formats (read_write.ml:19-101) ---- *)
+let c_write_rows = fn "mcg_write_rows" (string @-> int32_t @-> string_opt @-> int64_t @-> int32_t @-> ptr double @-> returning int)
+let c_read_shape = fn "mcg_read_rows_shape" (string @-> int64_t @-> ptr int64_t @-> ptr int32_t @-> returning int)
+let c_read_rows = fn "mcg_read_rows" (string @-> int64_t @-> int64_t @-> int32_t @-> ptr double @-> ptr double @-> int32_t @-> returning int)
+
+let write_rows ?(append = false) ?header path (rows : float array array) =
+  let nr = Array.length rows in
+  let nc = if nr = 0 then 1 else Array.length rows.(0) in
+  raise_rc (c_write_rows path (if append then 1l else 0l) header (Int64.of_int nr) (Int32.of_int nc)
+              (carr (flatten rows)))
+
+let read_rows ?(skip = 0) ?(nheader = 0) path =
+  let nr = allocate int64_t 0L and nc = allocate int32_t 0l in
+  raise_rc (c_read_shape path (Int64.of_int skip) nr nc);
+  let nr = Int64.to_int !@nr and nc = Int32.to_int !@nc in
+  let buf = CArray.make double (max 1 (nr * nc)) and hdr = CArray.make double (max 1 nheader) in
+  raise_rc (c_read_rows path (Int64.of_int skip) (Int64.of_int nr) (Int32.of_int nc) (CArray.start buf)
+              (if nheader > 0 then CArray.start hdr else from_voidp double null) (Int32.of_int nheader));
+  (Array.init nr (fun i -> Array.init nc (fun j -> CArray.get buf (i * nc + j))),
+   Array.init nheader (fun j -> CArray.get hdr j))
+
+(* Read_write.write / read on (coords, log_likelihood, log_prior) samples *)
+let write_samples path samples =
+  write_rows path (Array.map (fun (v, l, p) -> Array.append v [| l; p |]) samples)
+
+let read_samples path =
+  let rows, _ = read_rows path in
+  Array.map (fun r -> let d = Array.length r - 2 in (Array.sub r 0 d, r.(d), r.(d + 1))) rows
+
+(* Read_write.write_nested / read_nested *)
+let write_nested path (log_ev, log_dev, pts, wts) (ll : float array) (lp : float array) =
+  let rows = Array.mapi (fun i v -> Array.append v [| ll.(i); lp.(i); wts.(i) |]) pts in
+  write_rows ~header:(Printf.sprintf "%g %g\n" log_ev log_dev) path rows
+
+let read_nested path =
+  let rows, hdr = read_rows ~skip:1 ~nheader:2 path in
+  let d = if Array.length rows = 0 then 0 else Array.length rows.(0) - 3 in
+  (hdr.(0), hdr.(1), Array.map (fun r -> (Array.sub r 0 d, r.(d), r.(d + 1))) rows,
+   Array.map (fun r -> r.(d + 2)) rows)

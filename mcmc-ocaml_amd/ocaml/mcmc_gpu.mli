@@ -33,10 +33,21 @@ type prior =
   | Box of float array * float array * float     (** lo, hi, log density inside (inclusive) *)
   | Open_box of float array * float array * float
 
+(** components of Mcmc.combine_jump_proposals (mcmc.ml:165-185) *)
+type mix_component =
+  | Mix_gauss of float array                     (** x + s N(0,1) *)
+  | Mix_shift_uniform of float array * float array   (** x + random_between a b (test/mcmc_test.ml) *)
+  | Mix_wrap of float array * float array * float array   (** Mcmc.uniform_wrapping *)
+  | Mix_interp                                   (** the mixture's kD tree (Interpolate_pdf.draw) *)
+
 type proposal =
   | Gauss of float array                         (** y = x + s N(0,1), symmetric *)
   | Uniform_wrapping of float array * float array * float array   (** Mcmc.uniform_wrapping *)
   | Interp of float array array * float array * float array        (** Interpolate_pdf.make *)
+  | Mixture of (float * mix_component * bool) list * (float array array * float array * float array) option
+  (** combine_jump_proposals [(p, jump, density?)]: [density] = the component's log_jump_prob is
+      its log density (else the constant 0 of a symmetric jump); the optional kD tree serves
+      Mix_interp *)
 
 val set_model : ctx -> likelihood -> prior -> proposal option -> unit
 
@@ -63,3 +74,40 @@ val nested_evidence :
 
 (** Nested.log_total_error_estimate (nested.mli:69). *)
 val log_total_error_estimate : float -> float -> int -> float
+
+(** {2 Reversible jump (Mcmc.make_rjmcmc_sampler / rjmcmc_array, mcmc.ml:89-153)} *)
+type rj_jump =
+  | Rj_gauss of float array                      (** random walk, log_jump_prob 0 *)
+  | Rj_wrap of float array * float array * float array
+  | Rj_indep_gauss of float array * float array  (** independence draw N(mu, s) *)
+  | Rj_interp                                    (** independence draw from the model's kD tree *)
+
+type rj_model = {
+  rj_lik : likelihood; rj_prior : prior; rj_jump : rj_jump; rj_into : rj_jump;
+  rj_tree : (float array array * float array * float array) option; rj_model_prior : float }
+
+(** [rjmcmc_array ctx n a b start_a start_b]: start_a is D_A x N, start_b D_B x N (the (a, b)
+    pair per chain); each chain starts by a fair coin (mcmc.ml:120).  Returns the record model
+    tags (n x N), values (n x Dmax x N, zero-padded), log-likelihoods and log-priors. *)
+val rjmcmc_array :
+  ?nbin:int -> ?nskip:int -> ctx -> int -> rj_model -> rj_model -> mat -> mat ->
+  (int, Bigarray.int8_unsigned_elt, Bigarray.c_layout) Bigarray.Array2.t *
+  (float, Bigarray.float64_elt, Bigarray.c_layout) Bigarray.Genarray.t * mat * mat
+
+val rjmcmc_model_counts : ctx -> int * int
+val rjmcmc_evidence_ratio : ctx -> float
+
+(** {2 Evidence.evidence_direct / evidence_lebesgue (evidence.ml:145-221)} on samples
+    (coordinates, log_likelihood, log_prior) *)
+val evidence_direct : ?n:int -> (float array * float * float) array -> float
+val evidence_lebesgue : ?n:int -> ?eps:float -> (float array * float * float) array -> float
+
+(** {2 Nested replicas} merge runs [(ll in nested_output order, nlive, k)] into one run:
+    (merged order, log Z, log dZ, log weights) *)
+val nested_merge : (float array * int * int) list -> int array * float * float * float array
+
+(** {2 Read_write (read_write.ml:19-101)} *)
+val write_samples : string -> (float array * float * float) array -> unit
+val read_samples : string -> (float array * float * float) array
+val write_nested : string -> float * float * float array array * float array -> float array -> float array -> unit
+val read_nested : string -> float * float * (float array * float * float) array * float array

@@ -1227,6 +1227,7 @@ int or_nested(const or_model* m, uint64_t seed, const or_nested_opts* o, double*
 /* nested.ml:81-120.  Dead point i was retired with n_i = nlive - (i mod k) live points; its
    remaining volume is logX_i = (i div k) * L_k + prefix[i mod k].  With k = 1 this is exactly
    log_vol_fraction + i * log_reduction_frac of nested.ml:96. */
+#define OR_EV_BLOCK 65536
 void or_evidence_weights(int64_t n, int64_t nlive, int64_t k, const double* ll,
                          double* log_ev, double* log_dev, double* wts) {
   const double log_half = -0.69314718055994530942;
@@ -1235,7 +1236,17 @@ void or_evidence_weights(int64_t n, int64_t nlive, int64_t k, const double* ll,
   prefix[0] = 0.0;
   for (int64_t j = 0; j < k; ++j) prefix[j + 1] = prefix[j] + log1p(-1.0 / (double)(nlive - j));
   for (int64_t i = 0; i < n; ++i) wts[i] = -INFINITY;
-  double low = -INFINITY, high = -INFINITY;
+  /* the running sums low / high fold the iterations in blocks of OR_EV_BLOCK: a sequential
+     log-sum inside each block from -inf, then a sequential log-sum of the block results -- the
+     reference's sequential fold exactly when n <= OR_EV_BLOCK (a single block), and within
+     rounding of it otherwise (the blocks run in parallel on the host) */
+  double low = -INFINITY, high = -INFINITY, blow = -INFINITY, bhigh = -INFINITY;
+  int64_t it = 0;
+#define OR_EV_FOLD(dl_, dh_) do { \
+    blow = or_log_sum_logs(blow, (dl_)); bhigh = or_log_sum_logs(bhigh, (dh_)); \
+    if (++it % OR_EV_BLOCK == 0 || it == n) { \
+      low = or_log_sum_logs(low, blow); high = or_log_sum_logs(high, bhigh); \
+      blow = -INFINITY; bhigh = -INFINITY; } } while (0)
   double last_dv = 0.0;
   for (int64_t i = 0; i < ilive; ++i) {
     int64_t j = i % k, g = i / k;
@@ -1243,8 +1254,7 @@ void or_evidence_weights(int64_t n, int64_t nlive, int64_t k, const double* ll,
     double log_dv = log(1.0 / (double)(nlive - j)) + logx;
     if (k == 1) log_dv = log(1.0 / (double)nlive) + (double)i * log1p(-1.0 / (double)nlive);
     double dlow = log_dv + ll[i], dhigh = log_dv + ll[i + 1];
-    low = or_log_sum_logs(low, dlow);
-    high = or_log_sum_logs(high, dhigh);
+    OR_EV_FOLD(dlow, dhigh);
     wts[i] = or_log_sum_logs(wts[i], log_half + dlow);
     wts[i + 1] = or_log_sum_logs(wts[i + 1], log_half + dhigh);
     last_dv = log_dv;
@@ -1259,11 +1269,11 @@ void or_evidence_weights(int64_t n, int64_t nlive, int64_t k, const double* ll,
   }
   for (int64_t i = ilive; i < n; ++i) {
     double dlow = log_dv + ll[i - 1], dhigh = log_dv + ll[i];
-    low = or_log_sum_logs(low, dlow);
-    high = or_log_sum_logs(high, dhigh);
+    OR_EV_FOLD(dlow, dhigh);
     wts[i - 1] = or_log_sum_logs(wts[i - 1], log_half + dlow);
     wts[i] = or_log_sum_logs(wts[i], log_half + dhigh);
   }
+#undef OR_EV_FOLD
   *log_ev = log_half + or_log_sum_logs(low, high);
   *log_dev = high + log1p(-exp(low - high));
   for (int64_t i = 0; i < n; ++i) wts[i] = wts[i] - *log_ev;

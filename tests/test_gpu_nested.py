@@ -181,3 +181,15 @@ def test_nested_replicas_unit_evidence(T):
     err = math.exp(nested.log_total_error_estimate(mg[0], mg[1], 1000))
     assert abs(ev - 1.0) < 2 * err and err < 0.1
     assert abs(np.exp(mg[3]).sum() - 1.0) < 1e-8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D,k", [(8, 16), (16, 100), (32, 7)])
+def test_nested_multilane_walkers_bit_exact(oracle, T, D, k):
+    """Walkers on 2 (D % 8 == 0) or 4 (D % 16 == 0) lanes with prefetched DE rows, and the
+    one-workgroup sort of the new keys: still the oracle's dead-point sequence bit for bit."""
+    lik = T.gauss_shell(np.zeros(D), 1.0, 0.2)
+    pri = T.box(-2 * np.ones(D), 2 * np.ones(D))
+    g = gpu_nested(lik, pri, 6, nlive=300, nmcmc=15, mode_hopping_frac=0.1, k=k, max_dead=k * 40)
+    o = oracle_nested(oracle, lik, pri, 6, nlive=300, nmcmc=15, mode_hop=0.1, k=k, max_iter=k * 40)
+    assert_nested_same(g, o)

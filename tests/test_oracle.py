@@ -319,3 +319,32 @@ def test_kd_interp_mean_of_linear_pdf(oracle):
     p = np.array([t.jump_prob([x]) for x in xs])
     mean = (p * xs).sum() / p.sum()
     assert abs(mean - 2 / 3) < 0.05 * 2 / 3
+
+
+def test_evidence_weights_blocked_fold_close_to_sequential(oracle):
+    """Beyond 65,536 iterations the running sums fold in blocks; the result
+    stays within 1e-13 relative of the reference's sequential fold (nested.ml:90-113)."""
+    rng = np.random.default_rng(8)
+    nlive, n = 1000, 150000
+    ll = np.sort(rng.normal(size=n)) * 5.0
+    le, ld, _ = oracle.evidence_weights(ll, nlive, 1)
+
+    def lse(a, b):
+        if a == -math.inf and b == -math.inf:
+            return -math.inf
+        if b > a:
+            a, b = b, a
+        return a + math.log1p(math.exp(b - a))
+
+    lvf, lrf = math.log(1.0 / nlive), math.log1p(-1.0 / nlive)
+    ilive = n - nlive
+    low = high = -math.inf
+    for i in range(ilive):
+        ldv = lvf + i * lrf
+        low, high = lse(low, ldv + ll[i]), lse(high, ldv + ll[i + 1])
+    ldv = lvf + (ilive - 1) * lrf
+    for i in range(ilive, n):
+        low, high = lse(low, ldv + ll[i - 1]), lse(high, ldv + ll[i])
+    lev = -0.69314718055994530942 + lse(low, high)
+    assert abs(le - lev) <= 1e-13 * abs(lev)
+    assert abs(ld - (high + math.log1p(-math.exp(low - high)))) <= 1e-12 * abs(ld)
