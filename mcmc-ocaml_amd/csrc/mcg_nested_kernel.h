@@ -52,6 +52,106 @@ struct NestArgs {
   uint64_t seed_unused;
 };
 
+#ifndef MCG_NEST_PREFETCH
+#define MCG_NEST_PREFETCH 4
+#endif
+constexpr int kNestPrefetch = MCG_NEST_PREFETCH;    // DE steps whose partner rows are in flight
+
+// broadcast lane K of each lane quad to the quad (DPP quad_perm, no LDS)
+template <int K>
+__device__ __forceinline__ uint32_t quad_bcast_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, K * 0x55, 0xF, 0xF, false);
+}
+template <int K>
+__device__ __forceinline__ double quad_bcast_f64(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), K * 0x55, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), K * 0x55, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// The log-target constants of one walker lane (its dims of mu/sigma or the shell centre, the box
+// bounds), loaded into registers once per launch.  Loaded per step through the parameter
+// pointers they would queue behind the prefetched DE rows in the in-order vector-memory counter
+// and expose the full load latency every step.  Same operations as eval_lik / eval_prior.
+template <int D, int P, int LIK>
+struct WalkTarget {
+  using Lay = Layout<D, P>;
+  static constexpr int NL = Lay::NL;
+  static constexpr bool kReg =
+      (LIK == MCG_LIK_DIAG_GAUSS || LIK == MCG_LIK_GAUSS_SHELL || LIK == MCG_LIK_FLAT) && NL <= 8;
+  static constexpr int NR = kReg ? NL : 1;
+  double m0[NR], m1[NR], lo[NR], hi[NR];
+  double c0 = 0.0, c1 = 0.0, c2 = 0.0, lp_in = 0.0;
+  bool box = false;
+
+  __device__ __forceinline__ void load(const MhArgs& a, int sub) {
+    if constexpr (kReg) {
+      const double* __restrict__ q = a.lik;
+      const double* __restrict__ pr = a.pri;
+      box = a.prior_kind != MCG_PRIOR_FLAT;
+#pragma unroll
+      for (int i = 0; i < Lay::NCL; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int j = 4 * i + k;
+          const bool v = Lay::valid(sub, i, k);
+          const int d = v ? Lay::dim(sub, i, k) : 0;
+          m0[j] = (v && LIK != MCG_LIK_FLAT) ? q[d] : 0.0;
+          m1[j] = (v && LIK == MCG_LIK_DIAG_GAUSS) ? q[D + d] : 0.0;
+          lo[j] = v ? pr[d] : -__builtin_inf();
+          hi[j] = v ? pr[D + d] : __builtin_inf();
+        }
+      if constexpr (LIK == MCG_LIK_DIAG_GAUSS) c0 = q[2 * D];
+      if constexpr (LIK == MCG_LIK_GAUSS_SHELL) { c0 = q[D]; c1 = q[D + 1]; c2 = q[D + 2]; }
+      lp_in = pr[2 * D];
+    }
+  }
+
+  __device__ __forceinline__ double lik(const double* y, int sub, const MhArgs& a) const {
+    if constexpr (!kReg) {
+      return eval_lik<D, P, LIK>(y, sub, a, a.lik);
+    } else if constexpr (LIK == MCG_LIK_FLAT) {
+      return 0.0;
+    } else {
+      double A[Lay::NA];
+#pragma unroll
+      for (int j = 0; j < Lay::NA; ++j) A[j] = 0.0;
+#pragma unroll
+      for (int i = 0; i < Lay::NCL; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (!Lay::valid(sub, i, k)) continue;
+          const int j = 4 * i + k;
+          double e;
+          if constexpr (LIK == MCG_LIK_DIAG_GAUSS) e = fma(y[j], m1[j], -m0[j]);
+          else e = y[j] - m0[j];
+          A[i % Lay::NA] = fma(e, e, A[i % Lay::NA]);
+        }
+      const double S = reduce_canon<P>(A);
+      if constexpr (LIK == MCG_LIK_DIAG_GAUSS) {
+        return c0 - 0.5 * S;
+      } else {
+        const double r = psqrt(S);
+        const double qq = (r - c0) * c1;
+        return c2 - 0.5 * qq * qq;
+      }
+    }
+  }
+
+  __device__ __forceinline__ double prior(const double* y, int sub, const MhArgs& a) const {
+    if constexpr (!kReg) {
+      return eval_prior<D, P>(y, sub, a, a.pri);
+    } else {
+      if (!box) return 0.0;
+      int inb = 1;
+#pragma unroll
+      for (int j = 0; j < NL; ++j) inb &= (int)(y[j] >= lo[j]) & (int)(y[j] <= hi[j]);
+      inb = and_lanes<P>(inb);
+      return inb ? lp_in : -__builtin_inf();
+    }
+  }
+};
+
 // ---- constrained DE-MCMC walkers (draw_new_live_point, nested.ml:50-74) ----
 // P lanes per walker (P in {1, 2, 4}; the MH kernel's layout: lane `sub` owns the 4-dim blocks
 // c = sub, sub + P, ...).  Every lane of a walker draws the same Philox words, so the DE indices,
@@ -90,7 +190,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
     }
   }
   if (start < 0) start = a.key_slot[a.k - 1];
-  double cur[NL], y[NL], bi[NL], bj[NL];
+  double cur[NL], y[NL];
   auto load_row = [&](double* dst, int64_t row) {
     const double* __restrict__ src = a.x + row * D;
 #pragma unroll
@@ -106,53 +206,79 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
     const uint32_t jj = randint(ri.z, ri.w, n - 1);
     j = jj + (jj >= i ? 1u : 0u);
   };
+  WalkTarget<D, P, LIK> tgt;
+  tgt.load(a.m, sub);
   load_row(cur, start);
   double cur_l = (a.ll[start] >= thr) ? a.lp[start] : -__builtin_inf();   // mcmc_logl, :54-59
-  if (a.nmcmc > 0) {
+  // partner rows of steps s .. s + PD - 1 in flight: ring slot u holds step s0 + u
+  constexpr int PD = kNestPrefetch;
+  double bi[PD][NL], bj[PD][NL];
+#pragma unroll
+  for (int u = 0; u < PD; ++u) {
     uint32_t i0, j0;
-    pick(0, i0, j0);
-    load_row(bi, i0);
-    load_row(bj, j0);
+    pick(u, i0, j0);
+    load_row(bi[u], i0);
+    load_row(bj[u], j0);
   }
-  for (int64_t s = 0; s < a.nmcmc; ++s) {
-    double ni[NL], nj[NL];
-    if (s + 1 < a.nmcmc) {                             // prefetch step s + 1's partner rows
-      uint32_t i1, j1;
-      pick(s + 1, i1, j1);
-      load_row(ni, i1);
-      load_row(nj, j1);
-    }
-    const u32x4 rs = rng(wid, (uint32_t)s, CALL_DE_SCALE, TAG_NEST_WALK, 0u);
-    double dsc;
-    if (a.mode_hop != 0.0 && u53(rs.x, rs.y) < a.mode_hop) {
-      dsc = 1.0;
-    } else {
-      double z0, z1;
-      normal_pair(rs.z, rs.w, z0, z1, s_lt, s_at);
-      dsc = a.sigma_de * z0;
-    }
+  // whole groups of PD steps with no data-dependent branches around the loads, so the compiler
+  // can count the in-flight loads (vmcnt) across iterations; steps past nmcmc only compute
+  for (int64_t s0 = 0; s0 < a.nmcmc; s0 += PD) {
 #pragma unroll
-    for (int d = 0; d < NL; ++d) y[d] = cur[d] + dsc * (bj[d] - bi[d]);
-    const double lly = eval_lik<D, P, LIK>(y, sub, a.m, a.m.lik);
-    const double lpy = eval_prior<D, P>(y, sub, a.m, a.m.pri);
-    const double ml = (lly >= thr) ? lpy : -__builtin_inf();
-    const double ratio = (((ml + 0.0) - (cur_l + 0.0)) + 0.0) - 0.0;   // mcmc.ml:47-48
-    const u32x4 ra = rng(wid, (uint32_t)s, CALL_ACCEPT, TAG_NEST_WALK, 0u);
-    if (plog(u53(ra.x, ra.y), s_lt) < ratio) {
+    for (int u = 0; u < PD; ++u) {
+      const int64_t s = s0 + u;
+      const bool live = s < a.nmcmc;
+      const int64_t sp = s + PD;                       // the step whose rows go into slot u next
+      double dsc, lu;
+      uint32_t ip = 0, jp = 0;
+      if constexpr (P == 4) {
+        // the step's three Philox calls on three lanes of the walker's quad, one call per lane:
+        // lane 0 the DE indices of step s + PD (prefetch), lane 1 the DE scale, lane 2 the accept
+        // uniform; every lane finishes all three words (same instructions, own data) and the
+        // quad broadcasts (DPP) take each value from its lane
+        const uint32_t call = sub == 0 ? CALL_DE_IDX : sub == 1 ? CALL_DE_SCALE : CALL_ACCEPT;
+        const u32x4 r = rng(wid, (uint32_t)(sub == 0 ? sp : s), call, TAG_NEST_WALK, 0u);
+        const uint32_t pi = randint(r.x, r.y, n);
+        const uint32_t pjj = randint(r.z, r.w, n - 1);
+        double z0, z1;
+        normal_pair(r.z, r.w, z0, z1, s_lt, s_at);
+        const double hop_u = u53(r.x, r.y);
+        const double dloc = (a.mode_hop != 0.0 && hop_u < a.mode_hop) ? 1.0 : a.sigma_de * z0;
+        const double lloc = plog(hop_u, s_lt);
+        ip = quad_bcast_u32<0>(pi);
+        jp = quad_bcast_u32<0>(pjj);
+        jp = jp + (jp >= ip ? 1u : 0u);
+        dsc = quad_bcast_f64<1>(dloc);
+        lu = quad_bcast_f64<2>(lloc);
+      } else {
+        pick(sp, ip, jp);
+        const u32x4 rs = rng(wid, (uint32_t)s, CALL_DE_SCALE, TAG_NEST_WALK, 0u);
+        if (a.mode_hop != 0.0 && u53(rs.x, rs.y) < a.mode_hop) {
+          dsc = 1.0;
+        } else {
+          double z0, z1;
+          normal_pair(rs.z, rs.w, z0, z1, s_lt, s_at);
+          dsc = a.sigma_de * z0;
+        }
+        const u32x4 ra = rng(wid, (uint32_t)s, CALL_ACCEPT, TAG_NEST_WALK, 0u);
+        lu = plog(u53(ra.x, ra.y), s_lt);
+      }
 #pragma unroll
-      for (int d = 0; d < NL; ++d) cur[d] = y[d];
-      cur_l = ml;
-    }
-    if (s + 1 < a.nmcmc) {
+      for (int d = 0; d < NL; ++d) y[d] = cur[d] + dsc * (bj[u][d] - bi[u][d]);
+      load_row(bi[u], ip);                             // refill slot u with step s + PD's rows
+      load_row(bj[u], jp);
+      const double lly = tgt.lik(y, sub, a.m);
+      const double lpy = tgt.prior(y, sub, a.m);
+      const double ml = (lly >= thr) ? lpy : -__builtin_inf();
+      const double ratio = (((ml + 0.0) - (cur_l + 0.0)) + 0.0) - 0.0;   // mcmc.ml:47-48
+      if (live && lu < ratio) {
 #pragma unroll
-      for (int d = 0; d < NL; ++d) {
-        bi[d] = ni[d];
-        bj[d] = nj[d];
+        for (int d = 0; d < NL; ++d) cur[d] = y[d];
+        cur_l = ml;
       }
     }
   }
-  const double nl = eval_lik<D, P, LIK>(cur, sub, a.m, a.m.lik);
-  const double np = eval_prior<D, P>(cur, sub, a.m, a.m.pri);
+  const double nl = tgt.lik(cur, sub, a.m);
+  const double np = tgt.prior(cur, sub, a.m);
   if (!active) return;
 #pragma unroll
   for (int i = 0; i < Lay::NCL; ++i)
