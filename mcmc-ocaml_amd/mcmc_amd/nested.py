@@ -57,7 +57,7 @@ def merge_runs(runs):
     kk = np.array([k for _, _, k in runs], np.int64)
     ll = np.ascontiguousarray(np.concatenate([_ll(o) for o, _, _ in runs]), np.float64)
     lp = np.concatenate([_lp(o) for o, _, _ in runs])
-    pts = np.concatenate([np.asarray(o[2]) for o, _, _ in runs])
+    pts = None if any(o[2] is None for o, _, _ in runs) else np.concatenate([np.asarray(o[2]) for o, _, _ in runs])
     n = len(ll)
     order = np.zeros(n, np.int64)
     w = np.zeros(n)
@@ -67,7 +67,8 @@ def merge_runs(runs):
                                      L.dptr(w)))
     n_dead = int(n - nlive.sum())
     n_gen = int(sum(getattr(o, "n_gen", 0) for o, _, _ in runs))
-    return NestedOutput(le.value, ld.value, pts[order], w, ll[order], lp[order], n_dead, n_gen)
+    return NestedOutput(le.value, ld.value, None if pts is None else pts[order], w, ll[order], lp[order],
+                        n_dead, n_gen)
 
 
 def _ll(o):

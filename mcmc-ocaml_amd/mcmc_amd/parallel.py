@@ -48,15 +48,16 @@ def _world(group):
     return dist.get_rank(group), dist.get_world_size(group)
 
 
-def allgather_runs(output, nlive, k, device=None, group=None):
+def allgather_runs(output, nlive, k, device=None, group=None, points=True):
     """All-gather every rank's nested run: the point counts first, then the (pts | ll | lp) rows
-    padded to the longest run.  Returns [(output, nlive, k)] in rank order."""
+    padded to the longest run (points=False: ll | lp only, enough for log Z).  Returns
+    [(output, nlive, k)] in rank order."""
     rank, world = _world(group)
     if world == 1:
         return [(output, nlive, k)]
     import torch
     import torch.distributed as dist
-    pts = np.asarray(output[2], np.float64)
+    pts = np.asarray(output[2], np.float64) if points else np.zeros((len(output.ll), 0))
     D = pts.shape[1]
     rows = np.concatenate([pts, output.ll[:, None], output.lp[:, None]], axis=1)
     meta = torch.tensor([rows.shape[0], nlive, k, output.n_gen], dtype=torch.int64, device=device)
@@ -72,19 +73,20 @@ def allgather_runs(output, nlive, k, device=None, group=None):
     runs = []
     for m, o in zip(metas, outs):
         r = o.cpu().numpy()[:int(m[0])]
-        run = _nested.NestedOutput(0.0, 0.0, r[:, :D].copy(), None, r[:, D].copy(), r[:, D + 1].copy(),
-                                   int(m[0] - m[1]), int(m[3]))
+        run = _nested.NestedOutput(0.0, 0.0, r[:, :D].copy() if points else None, None, r[:, D].copy(),
+                                   r[:, D + 1].copy(), int(m[0] - m[1]), int(m[3]))
         runs.append((run, int(m[1]), int(m[2])))
     return runs
 
 
 def nested_evidence_replicas(log_likelihood, log_prior, epsrel=0.01, nmcmc=1000, nlive=1000,
                              mode_hopping_frac=0.1, k=1, seed=0, device=0, group=None,
-                             comm_device=None):
+                             comm_device=None, points=True):
     """Nested.nested_evidence (nested.ml:122-146) as one replica per GPU: every
     rank runs an independent nested run with nlive / world live points on its own Philox key,
     the runs are all-gathered and merged (mcg_nested_merge) into one run of nlive points.  Every
-    rank returns the same merged NestedOutput."""
+    rank returns the same merged NestedOutput (points=False: gather ll / lp only; the merged
+    output then has no points)."""
     rank, world = _world(group)
     if nlive % world:
         raise ValueError("nlive (%d) must be a multiple of the number of ranks (%d)" % (nlive, world))
@@ -95,4 +97,4 @@ def nested_evidence_replicas(log_likelihood, log_prior, epsrel=0.01, nmcmc=1000,
                                       nlive=nl, mode_hopping_frac=mode_hopping_frac, k=kk, ctx=ctx)
     if world == 1:
         return out
-    return _nested.merge_runs(allgather_runs(out, nl, kk, comm_device, group))
+    return _nested.merge_runs(allgather_runs(out, nl, kk, comm_device, group, points=points))

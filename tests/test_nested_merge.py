@@ -95,6 +95,9 @@ def _worker(rank, world, port, q):
     out = nested.NestedOutput(r["log_ev"], r["log_dev"], r["pts"], r["log_wts"], r["ll"], r["lp"],
                               r["n_dead"], r["n_gen"])
     merged = nested.merge_runs(allgather_runs(out, 40, 1))
+    light = nested.merge_runs(allgather_runs(out, 40, 1, points=False))   # ll / lp only
+    assert light[2] is None and light[0] == merged[0]
+    np.testing.assert_array_equal(light[3], merged[3])
     q.put((rank, merged[0], merged[1], merged.ll, merged[2], merged[3]))
     dist.barrier()
     dist.destroy_process_group()
