@@ -62,7 +62,10 @@ __device__ __forceinline__ void transpose_quadrants(double* v) {
 }
 
 template <int D>
-__global__ void __launch_bounds__(256) mh_fullcov_kernel(const MhArgs a) {
+#ifndef MCG_FC_MIN_WAVES
+#define MCG_FC_MIN_WAVES 2   // occupancy 2 with a few spills beats occupancy 1 (+50%, C5)
+#endif
+__global__ void __launch_bounds__(256, MCG_FC_MIN_WAVES) mh_fullcov_kernel(const MhArgs a) {
   using F = FcLayout<D>;
   constexpr int NL = F::NKB;
   __shared__ double2 s_lt[kLogTabN];
