@@ -177,20 +177,21 @@ __device__ __forceinline__ void normal_pair(uint32_t a, uint32_t b, double& z0, 
 
 // log1p(r), r in [0,1] (Goldberg: r * log(1+r) / ((1+r)-1)); log-sum-exp on the portable
 // exp/log.  Drives the running nested-sampling estimate (nested.ml:139-142).
-__device__ __forceinline__ double plog1p(double r) {
+__device__ __forceinline__ double plog1p(double r, const double2* tab = kLogTab) {
   double u = 1.0 + r;
   if (u == 1.0) return r;
-  return plog(u) * (r / (u - 1.0));
+  return plog(u, tab) * (r / (u - 1.0));
 }
 
-__device__ __forceinline__ double plse(double a, double b) {
+// `tab`: kLogTab or a copy staged in LDS
+__device__ __forceinline__ double plse(double a, double b, const double2* tab = kLogTab) {
   if (a == -__builtin_inf() && b == -__builtin_inf()) return -__builtin_inf();
   if (b > a) {
     double t = a;
     a = b;
     b = t;
   }
-  return a + plog1p(pexp(b - a));
+  return a + plog1p(pexp(b - a), tab);
 }
 
 // log-space harmonic-mean partial (m, s) += v = -ll (evidence.ml:101-107 in log space);

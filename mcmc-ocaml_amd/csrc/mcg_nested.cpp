@@ -2,7 +2,7 @@
 //
 // One generation = walk (k constrained DE-MCMC walkers, one lane each) -> retire (k lowest to the
 // dead buffer, new points into their slots) -> estimate (running evidence + log volume) -> sort
-// the k new keys -> merge them into the n-k survivors -> stop test.  All of it is enqueued
+// the k new keys -> merge them into the n-k survivors (+ stop test).  All of it is enqueued
 // asynchronously in batches of generations; the device-side stop flag turns the kernels of any
 // generation after the stopping one into no-ops, so the host only synchronises once per batch.
 // evidence_error_and_weights (nested.ml:81-120) runs once on the host over the final points.
@@ -37,7 +37,7 @@ struct KeyBuf {
 };
 
 struct NestedBufs {
-  DevBuf x, ll, lp, nx, nll, nlp, tv, prefix, qadd, st, dead_x, dead_ll, dead_lp;
+  DevBuf x, ll, lp, nx, nll, nlp, tv, prefix, qadd, st, dead_x, dead_ll, dead_lp, runl, runj;
   KeyBuf keys[2], newk, newk_tmp;
   int64_t dead_cap = 0;
 };
@@ -170,6 +170,8 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   HC(B.nlp.ensure(k * 8), "alloc new");
   HC(B.newk.ensure(k), "alloc new keys");
   HC(B.newk_tmp.ensure(k), "alloc new keys");
+  HC(B.runl.ensure(((k + 255) / 256) * 256 * 8), "alloc sort runs");
+  HC(B.runj.ensure(((k + 255) / 256) * 256 * 4), "alloc sort runs");
   HC(B.tv.ensure(p2 * 8), "alloc tv");
   HC(B.prefix.ensure((k + 1) * 8), "alloc prefix");
   HC(B.qadd.ensure(k * 8), "alloc qadd");
@@ -269,7 +271,9 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
       HC(launch_estimate(a, s), "nested estimate");
       bool nk_tmp = false;
       if (k <= 4096) {
-        HC(launch_sort_new_small(a, B.newk_tmp.l(), B.newk_tmp.t(), B.newk_tmp.s(), s), "sort new keys");
+        // run-sorted (ll, j) scratch of ceil(k/256)*256 entries
+        HC(launch_sort_new_small(a, (double*)B.runl.p, (int*)B.runj.p, B.newk_tmp.l(), B.newk_tmp.t(),
+                                 B.newk_tmp.s(), s), "sort new keys");
         nk_tmp = true;
       } else {
         HC(launch_sort_keys(B.newk.l(), B.newk.t(), B.newk.s(), B.newk_tmp.l(), B.newk_tmp.t(),
@@ -277,7 +281,6 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
       }
       KeyBuf& nk = nk_tmp ? B.newk_tmp : B.newk;
       HC(launch_merge_new(a, nxt.l(), nxt.t(), nxt.s(), nk.l(), nk.t(), nk.s(), s), "merge keys");
-      HC(launch_stop(a, nxt.l(), s), "stop test");
     }
     gen += G;
     HC(hipMemcpyAsync(&st, B.st.p, sizeof st, hipMemcpyDeviceToHost, s), "read state");

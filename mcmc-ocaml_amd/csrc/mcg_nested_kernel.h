@@ -344,9 +344,10 @@ hipError_t launch_merge_new(const NestArgs& a, double* out_ll, long long* out_ti
                             const double* new_ll, const long long* new_tie, const int* new_slot,
                             hipStream_t st);
 hipError_t launch_retire(const NestArgs& a, int D, hipStream_t st);
-hipError_t launch_sort_new_small(const NestArgs& a, double* oll, long long* otie, int* oslot, hipStream_t st);
+// k <= 4096: run-sorted (ll, j) scratch rl[ceil(k/256)*256], rj[...] then a rank merge into o*
+hipError_t launch_sort_new_small(const NestArgs& a, double* rl, int* rj, double* oll, long long* otie,
+                                 int* oslot, hipStream_t st);
 hipError_t launch_estimate(const NestArgs& a, hipStream_t st);
-hipError_t launch_stop(const NestArgs& a, const double* final_ll, hipStream_t st);
 
 typedef hipError_t (*nest_walk_fn)(const NestArgs&, hipStream_t);
 typedef hipError_t (*nest_init_fn)(const NestArgs&, double*, long long*, int*, hipStream_t);
