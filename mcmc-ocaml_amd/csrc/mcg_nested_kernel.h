@@ -56,6 +56,10 @@ struct NestArgs {
 #define MCG_NEST_PREFETCH 4
 #endif
 constexpr int kNestPrefetch = MCG_NEST_PREFETCH;    // DE steps whose partner rows are in flight
+#ifndef MCG_NEST_WALK_BLOCK
+#define MCG_NEST_WALK_BLOCK 64
+#endif
+constexpr int kNestWalkBlock = MCG_NEST_WALK_BLOCK;
 
 // broadcast lane K of each lane quad to the quad (DPP quad_perm, no LDS)
 template <int K>
@@ -324,8 +328,11 @@ hipError_t launch_nest_walk(const NestArgs& a, hipStream_t st) {
   // multiple of 16 (8), which gives the few-thousand-walker generations 4x (2x) the lanes
   constexpr bool sep = LIK == MCG_LIK_DIAG_GAUSS || LIK == MCG_LIK_GAUSS_SHELL || LIK == MCG_LIK_FLAT;
   constexpr int P = (sep && D % 16 == 0) ? 4 : (sep && D % 8 == 0) ? 2 : 1;
-  const int64_t grid = (a.k * P + 255) / 256;
-  hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P>), dim3((unsigned)grid), dim3(256), 0, st, a);
+  // small workgroups: a generation has only k * P lanes, so one wave per workgroup spreads them
+  // over all CUs (their LDS tables, L1 and scalar units) instead of packing four per CU
+  const int block = kNestWalkBlock;
+  const int64_t grid = (a.k * P + block - 1) / block;
+  hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P>), dim3((unsigned)grid), dim3(block), 0, st, a);
   return hipGetLastError();
 }
 

@@ -92,10 +92,56 @@ def reductions():
                         log_ev=le, log_dev=ld, log_wts=w)
 
 
+def next_mini():
+    """SURVEY §8(f) components: a combine_jump_proposals MH run (mcmc.ml:165-185), a
+    reversible-jump run (mcmc.ml:89-153), the kD evidence integrals (evidence.ml:145-221) of its
+    model-A samples, and the merge of two nested runs."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import evidence_ref as R
+    # mixture: Gaussian + shift-uniform (density) + symmetric shift-uniform (ljp 0), D = 3
+    D, N = 3, 96
+    mix = np.array([3.0, 0.5, 1, 1, 0.6, 0.8, 1.0,
+                    1.0, 2, 1, -0.4, -0.4, -0.4, 0.2, 0.2, 0.2,
+                    0.7, 2, 0, -1.0, -1.0, -1.0, 1.0, 1.0, 1.0])
+    lik = np.array([0.3, -0.5, 1.0, 0.5, 1.0, 2.0])
+    pri = np.array([-8, -8, -8, 8, 8, 8, -3 * math.log(16.0)])
+    m = O.Model(D, LIK_DIAG, lik, PRIOR_BOX, pri, 5, mix)
+    x0 = np.random.default_rng(12).normal(size=(D, N))
+    ll0 = np.array([m.loglik(x0[:, i]) for i in range(N)])
+    lp0 = np.array([m.logprior(x0[:, i]) for i in range(N)])
+    r = O.mh_run(m, 14, x0, ll0, lp0, nbin=3, nskip=2, n_rec=40, record_x=True, record_llp=True)
+    # reversible jump: 1-D model A (Gaussian), 2-D model B (shell), independence transitions
+    a = dict(ndim=1, lik=(LIK_DIAG, [0.3, 0.6]), prior=(0, []), jump=(1, [0.5]), into=(3, [0.3, 0.6]), p=0.4)
+    b = dict(ndim=2, lik=(LIK_SHELL, [0.0, 0.0, 1.0, 0.2]), prior=(PRIOR_BOX, [-3, -3, 3, 3, 0.0]),
+             jump=(1, [0.3]), into=(3, [0.0, 0.0, 1.0, 1.0]), p=0.6)
+    NR = 80
+    xa = np.full((1, NR), 0.3)
+    xb = np.tile(np.array([[1.0], [0.0]]), (1, NR))
+    rj = O.rj_run(a, b, 21, xa, xb, nbin=5, nskip=2, n_rec=50)
+    # evidence integrals over the model-A records of the RJ run (1-D samples with repeats)
+    inA = rj["rec_tag"].T.reshape(-1) == 0
+    pts = rj["rec_x"][:, 0, :].T.reshape(-1)[inA][:, None]
+    ll = rj["rec_ll"].T.reshape(-1)[inA]
+    lp = rj["rec_lp"].T.reshape(-1)[inA]
+    direct = R.evidence_direct(pts, ll, lp, n=16)
+    lebesgue = R.evidence_lebesgue(pts, ll, lp, n=16, eps=0.5)
+    # run merge of two nested runs of the nested_test.ml Gaussian
+    mn = O.Model(2, LIK_DIAG, [0.5, 0.5, 0.1, 0.1], PRIOR_OPEN, [0, 0, 1, 1, 0.0], PROP_GAUSS, [1.0])
+    runs = [O.nested(mn, sd, nlive=40, nmcmc=20, k=2) for sd in (31, 32)]
+    order, mle, mld, mw = O.nested_merge([(q["ll"], 40, 2) for q in runs])
+    np.savez_compressed(os.path.join(HERE, "next_mini.npz"), mix=mix, mix_lik=lik, mix_pri=pri, mix_x0=x0,
+                        mix_bits=r["bits"], mix_rec_x=r["rec_x"], mix_x=r["x"],
+                        rj_tag=rj["rec_tag"], rj_rec_x=rj["rec_x"], rj_rec_ll=rj["rec_ll"], rj_nb=rj["nb"],
+                        ev_pts=pts, ev_ll=ll, ev_lp=lp, ev_direct=direct, ev_lebesgue=lebesgue,
+                        merge_ll0=runs[0]["ll"], merge_ll1=runs[1]["ll"], merge_order=order,
+                        merge_log_ev=mle, merge_log_dev=mld, merge_wts=mw)
+
+
 if __name__ == "__main__":
     O.build()
     c2_mini()
     c3_mini()
     c4_mini()
     reductions()
+    next_mini()
     print("golden fixtures written to", HERE)
