@@ -248,69 +248,34 @@ hipError_t launch_sort_new_small(const NestArgs& a, double* rl, int* rj, double*
 
 __device__ __forceinline__ void stop_test(const NestArgs& a, double max_ll);
 
-// Number of keys of the sorted run A[0, len) strictly below (kl, kt), in two levels: a binary
-// search over every W-th key staged in LDS (sl, st: ceil(len / W) samples), then the W - 1 keys
-// between the two bracketing samples loaded at once (independent loads: one memory latency,
-// where a plain binary search pays one per level).
-__device__ __forceinline__ int64_t count_less_2l(const double* al, const long long* at, int64_t len,
-                                                 int W, const double* sl, const long long* st,
-                                                 int nsamp, double kl, long long kt) {
-  int lo = 0, hi = nsamp;                          // samples [0, lo) are below the key
-  while (lo < hi) {
-    const int m = (lo + hi) >> 1;
-    if (key_less(sl[m], st[m], kl, kt)) lo = m + 1;
-    else hi = m;
-  }
-  if (lo == 0) return 0;                           // A[0] is not below the key
-  // A[(lo-1) W] is below, A[lo W] (if any) is not: count A[(lo-1) W + 1 .. lo W - 1]
-  const int64_t b = (int64_t)(lo - 1) * W + 1;
-  const int64_t e = (int64_t)lo * W < len ? (int64_t)lo * W : len;
-  int64_t c = b;
-  for (int64_t i = b; i < e; ++i) c += key_less(al[i], at[i], kl, kt) ? 1 : 0;
-  return c;
-}
-
-constexpr int kMergeSamples = 2048;                // LDS samples per run (32 KiB)
-
-// survivors keys[k..n) + k sorted new keys -> out[0..n).  Blocks [0, nbs) place survivors (their
-// rank among the new keys), blocks [nbs, ..) place new keys (their rank among the survivors); the
-// thread placing the largest key also runs the stop test of the generation.
+// survivors keys[k..n) + k sorted new keys -> out[0..n) by rank scatter; the thread placing the
+// largest key also runs the stop test of the generation.  (A two-level search with LDS-staged
+// samples measured slower: 29 vs 12 us at C3 -- the per-block sample loads cost more than the
+// L2-resident binary searches they save.)
 __global__ void __launch_bounds__(256) merge_new_kernel(const NestArgs a, double* oll,
                                                         long long* otie, int* oslot,
                                                         const double* nl, const long long* nt,
-                                                        const int* ns, int64_t nbs, int wn, int ws) {
+                                                        const int* ns) {
   if (a.st->stopped) return;
-  __shared__ double sl[kMergeSamples];
-  __shared__ long long stt[kMergeSamples];
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t n = a.n, k = a.k, ns_ = n - k;
-  const bool surv = blockIdx.x < nbs;
-  // the run this block searches: the new keys (for survivors) or the survivors (for new keys)
-  const double* rl = surv ? nl : a.key_ll + k;
-  const long long* rt = surv ? nt : a.key_tie + k;
-  const int64_t rlen = surv ? k : ns_;
-  const int W = surv ? wn : ws;
-  const int nsamp = (int)((rlen + W - 1) / W);
-  for (int i = threadIdx.x; i < nsamp; i += blockDim.x) {
-    sl[i] = rl[(int64_t)i * W];
-    stt[i] = rt[(int64_t)i * W];
-  }
-  __syncthreads();
-  const int64_t e = surv ? (int64_t)blockIdx.x * blockDim.x + threadIdx.x
-                         : (int64_t)(blockIdx.x - nbs) * blockDim.x + threadIdx.x;
-  if (e >= (surv ? ns_ : k)) return;
+  if (e >= n) return;
   double kl;
   long long kt;
   int ks;
-  if (surv) {
+  int64_t pos;
+  if (e < ns_) {
     kl = a.key_ll[k + e];
     kt = a.key_tie[k + e];
     ks = a.key_slot[k + e];
+    pos = e + count_less(nl, nt, 0, k, kl, kt);
   } else {
-    kl = nl[e];
-    kt = nt[e];
-    ks = ns[e];
+    const int64_t b = e - ns_;
+    kl = nl[b];
+    kt = nt[b];
+    ks = ns[b];
+    pos = b + count_less(a.key_ll + k, a.key_tie + k, 0, ns_, kl, kt);
   }
-  const int64_t pos = e + count_less_2l(rl, rt, rlen, W, sl, stt, nsamp, kl, kt);
   oll[pos] = kl;
   otie[pos] = kt;
   oslot[pos] = ks;
@@ -320,15 +285,9 @@ __global__ void __launch_bounds__(256) merge_new_kernel(const NestArgs a, double
 hipError_t launch_merge_new(const NestArgs& a, double* out_ll, long long* out_tie, int* out_slot,
                             const double* new_ll, const long long* new_tie, const int* new_slot,
                             hipStream_t s) {
-  const int64_t ns_ = a.n - a.k;
-  auto stride = [](int64_t len) {                  // sample stride: a power of two, >= 8
-    int W = 8;
-    while ((len + W - 1) / W > kMergeSamples) W <<= 1;
-    return W;
-  };
-  const int64_t nbs = (ns_ + 255) / 256, nbn = (a.k + 255) / 256;
-  hipLaunchKernelGGL(merge_new_kernel, dim3((unsigned)(nbs + nbn)), dim3(256), 0, s, a, out_ll, out_tie,
-                     out_slot, new_ll, new_tie, new_slot, nbs, stride(a.k), stride(ns_));
+  const unsigned grid = (unsigned)((a.n + 255) / 256);
+  hipLaunchKernelGGL(merge_new_kernel, dim3(grid), dim3(256), 0, s, a, out_ll, out_tie, out_slot,
+                     new_ll, new_tie, new_slot);
   return hipGetLastError();
 }
 
