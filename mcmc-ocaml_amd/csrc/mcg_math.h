@@ -221,4 +221,37 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) {
   return __shfl_xor(v, m, 64);
 }
 
+// value of lane ^ M.  M = 1, 2 stay inside a lane quad: a DPP quad_perm move (VALU, a few cycles)
+// instead of ds_bpermute (an LDS round trip on the serial chain of every MH / walker step).
+#ifndef MCG_DPP_XLANE
+#define MCG_DPP_XLANE 1
+#endif
+template <int M>
+__device__ __forceinline__ int xor_lane_i(int v) {
+  if constexpr (!MCG_DPP_XLANE) return __shfl_xor(v, M, 64);
+  else if constexpr (M == 1) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);   // [1,0,3,2]
+  else if constexpr (M == 2) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+  else return __shfl_xor(v, M, 64);
+}
+template <int M>
+__device__ __forceinline__ double xor_lane_d(double v) {
+  if constexpr (MCG_DPP_XLANE && (M == 1 || M == 2)) {
+    return __hiloint2double(xor_lane_i<M>(__double2hiint(v)), xor_lane_i<M>(__double2loint(v)));
+  } else {
+    return __shfl_xor(v, M, 64);
+  }
+}
+
+// broadcast lane K of each lane quad to the quad (DPP quad_perm, no LDS)
+template <int K>
+__device__ __forceinline__ uint32_t quad_bcast_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, K * 0x55, 0xF, 0xF, false);
+}
+template <int K>
+__device__ __forceinline__ double quad_bcast_f64(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), K * 0x55, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), K * 0x55, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
 }  // namespace mcg

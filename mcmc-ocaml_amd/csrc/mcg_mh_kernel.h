@@ -39,23 +39,23 @@ __device__ __forceinline__ double reduce_canon(const double* a) {
     return canon8(a);
   } else if constexpr (P == 2) {
     double c = (a[0] + a[2]) + (a[1] + a[3]);
-    return c + shfl_xor_d(c, 1);
+    return c + xor_lane_d<1>(c);
   } else if constexpr (P == 4) {
     double b = a[0] + a[1];
-    double c = b + shfl_xor_d(b, 2);
-    return c + shfl_xor_d(c, 1);
+    double c = b + xor_lane_d<2>(b);
+    return c + xor_lane_d<1>(c);
   } else {
-    double b = a[0] + shfl_xor_d(a[0], 4);
-    double c = b + shfl_xor_d(b, 2);
-    return c + shfl_xor_d(c, 1);
+    double b = a[0] + xor_lane_d<4>(a[0]);
+    double c = b + xor_lane_d<2>(b);
+    return c + xor_lane_d<1>(c);
   }
 }
 
 template <int P>
 __device__ __forceinline__ int and_lanes(int v) {
-  if constexpr (P >= 8) v &= __shfl_xor(v, 4, 64);
-  if constexpr (P >= 4) v &= __shfl_xor(v, 2, 64);
-  if constexpr (P >= 2) v &= __shfl_xor(v, 1, 64);
+  if constexpr (P >= 8) v &= xor_lane_i<4>(v);
+  if constexpr (P >= 4) v &= xor_lane_i<2>(v);
+  if constexpr (P >= 2) v &= xor_lane_i<1>(v);
   return v;
 }
 
@@ -615,7 +615,12 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
         const u32x4 wa = rng(gid, (uint32_t)Tj, CALL_ACCEPT, TAG_MH, (uint32_t)(Tj >> 32));
         lu_own = plog(u53(wa.x, wa.y), s_lt);
       }
-      lu = __shfl(lu_own, (lane & ~(P - 1)) | q, 64);
+      if constexpr (P == 4 && MCG_DPP_XLANE) {    // quad broadcast of lane q (DPP)
+        lu = q == 0 ? quad_bcast_f64<0>(lu_own) : q == 1 ? quad_bcast_f64<1>(lu_own)
+           : q == 2 ? quad_bcast_f64<2>(lu_own) : quad_bcast_f64<3>(lu_own);
+      } else {
+        lu = __shfl(lu_own, (lane & ~(P - 1)) | q, 64);
+      }
     }
     const bool acc = lu < ratio;
     if (acc) {

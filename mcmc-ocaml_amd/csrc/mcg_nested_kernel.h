@@ -61,18 +61,6 @@ constexpr int kNestPrefetch = MCG_NEST_PREFETCH;    // DE steps whose partner ro
 #endif
 constexpr int kNestWalkBlock = MCG_NEST_WALK_BLOCK;
 
-// broadcast lane K of each lane quad to the quad (DPP quad_perm, no LDS)
-template <int K>
-__device__ __forceinline__ uint32_t quad_bcast_u32(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, K * 0x55, 0xF, 0xF, false);
-}
-template <int K>
-__device__ __forceinline__ double quad_bcast_f64(double v) {
-  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), K * 0x55, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), K * 0x55, 0xF, 0xF, false);
-  return __hiloint2double(hi, lo);
-}
-
 // The log-target constants of one walker lane (its dims of mu/sigma or the shell centre, the box
 // bounds), loaded into registers once per launch.  Loaded per step through the parameter
 // pointers they would queue behind the prefetched DE rows in the in-order vector-memory counter
@@ -227,13 +215,14 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   // whole groups of PD steps with no data-dependent branches around the loads, so the compiler
   // can count the in-flight loads (vmcnt) across iterations; steps past nmcmc only compute
   for (int64_t s0 = 0; s0 < a.nmcmc; s0 += PD) {
+    // phase 1: the random numbers of the group's PD steps -- independent of the walker state, so
+    // the PD Philox / Box-Muller / log chains overlap instead of sitting in the serial chain
+    double dsc_g[PD], lu_g[PD];
+    uint32_t ip_g[PD], jp_g[PD];
 #pragma unroll
     for (int u = 0; u < PD; ++u) {
       const int64_t s = s0 + u;
-      const bool live = s < a.nmcmc;
       const int64_t sp = s + PD;                       // the step whose rows go into slot u next
-      double dsc, lu;
-      uint32_t ip = 0, jp = 0;
       if constexpr (P == 4) {
         // the step's three Philox calls on three lanes of the walker's quad, one call per lane:
         // lane 0 the DE indices of step s + PD (prefetch), lane 1 the DE scale, lane 2 the accept
@@ -248,33 +237,38 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
         const double hop_u = u53(r.x, r.y);
         const double dloc = (a.mode_hop != 0.0 && hop_u < a.mode_hop) ? 1.0 : a.sigma_de * z0;
         const double lloc = plog(hop_u, s_lt);
-        ip = quad_bcast_u32<0>(pi);
-        jp = quad_bcast_u32<0>(pjj);
-        jp = jp + (jp >= ip ? 1u : 0u);
-        dsc = quad_bcast_f64<1>(dloc);
-        lu = quad_bcast_f64<2>(lloc);
+        ip_g[u] = quad_bcast_u32<0>(pi);
+        const uint32_t jq = quad_bcast_u32<0>(pjj);
+        jp_g[u] = jq + (jq >= ip_g[u] ? 1u : 0u);
+        dsc_g[u] = quad_bcast_f64<1>(dloc);
+        lu_g[u] = quad_bcast_f64<2>(lloc);
       } else {
-        pick(sp, ip, jp);
+        pick(sp, ip_g[u], jp_g[u]);
         const u32x4 rs = rng(wid, (uint32_t)s, CALL_DE_SCALE, TAG_NEST_WALK, 0u);
         if (a.mode_hop != 0.0 && u53(rs.x, rs.y) < a.mode_hop) {
-          dsc = 1.0;
+          dsc_g[u] = 1.0;
         } else {
           double z0, z1;
           normal_pair(rs.z, rs.w, z0, z1, s_lt, s_at);
-          dsc = a.sigma_de * z0;
+          dsc_g[u] = a.sigma_de * z0;
         }
         const u32x4 ra = rng(wid, (uint32_t)s, CALL_ACCEPT, TAG_NEST_WALK, 0u);
-        lu = plog(u53(ra.x, ra.y), s_lt);
+        lu_g[u] = plog(u53(ra.x, ra.y), s_lt);
       }
+    }
+    // phase 2: the serial constrained steps
 #pragma unroll
-      for (int d = 0; d < NL; ++d) y[d] = cur[d] + dsc * (bj[u][d] - bi[u][d]);
-      load_row(bi[u], ip);                             // refill slot u with step s + PD's rows
-      load_row(bj[u], jp);
+    for (int u = 0; u < PD; ++u) {
+      const bool live = s0 + u < a.nmcmc;
+#pragma unroll
+      for (int d = 0; d < NL; ++d) y[d] = cur[d] + dsc_g[u] * (bj[u][d] - bi[u][d]);
+      load_row(bi[u], ip_g[u]);                        // refill slot u with step s + PD's rows
+      load_row(bj[u], jp_g[u]);
       const double lly = tgt.lik(y, sub, a.m);
       const double lpy = tgt.prior(y, sub, a.m);
       const double ml = (lly >= thr) ? lpy : -__builtin_inf();
       const double ratio = (((ml + 0.0) - (cur_l + 0.0)) + 0.0) - 0.0;   // mcmc.ml:47-48
-      if (live && lu < ratio) {
+      if (live && lu_g[u] < ratio) {
 #pragma unroll
         for (int d = 0; d < NL; ++d) cur[d] = y[d];
         cur_l = ml;
