@@ -113,11 +113,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    # MCG_BENCH_BACKEND=gloo rehearses the multi-rank flow with CPU collectives (e.g. several ranks
+    # sharing one GPU: MCG_BENCH_DEVICE=0); the driver's runs use RCCL ("nccl"), one GPU per rank
+    backend = os.environ.get("MCG_BENCH_BACKEND", "nccl")
+    if os.environ.get("MCG_BENCH_DEVICE"):
+        local = int(os.environ["MCG_BENCH_DEVICE"])
     if dist:
         import torch.distributed as tdist
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl")
+        tdist.init_process_group(backend)
     dev = torch.device("cuda", local)
+    comm = dev if backend == "nccl" else None      # device of the collectives' tensors
 
     from mcmc_amd import Context, targets as T
     from mcmc_amd.parallel import reduce_stats
@@ -147,11 +153,11 @@ def main():
         ctx.run(nbin=0, nskip=1, n_rec=S, record_x=False, record_llp=False, record_accept=False,
                 accumulate=True, append=True)
     # end-of-run reduction: tile kernel -> RCCL all-gather of tile partials -> host combine
-    mean, sd, log_z_hm = reduce_stats(D, ctx.tile_stats(), device=dev)
+    mean, sd, log_z_hm = reduce_stats(D, ctx.tile_stats(), device=comm)
     barrier()
     elapsed = time.perf_counter() - t0
     if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=comm)
         tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
         elapsed = float(tt.item())
     timing = ctx.kernel_timing("mh")
@@ -165,7 +171,7 @@ def main():
         tn = time.perf_counter()
         out = nested_evidence_replicas(lik, pri, nlive=args.nested_nlive * world, nmcmc=args.nested_nmcmc,
                                        k=args.nested_k, mode_hopping_frac=0.1, seed=7, device=local,
-                                       comm_device=dev if dist else None, points=False)
+                                       comm_device=comm if dist else None, points=False)
         barrier()
         wall = time.perf_counter() - tn
         w = np.exp(out[3])
