@@ -104,6 +104,8 @@ def main():
     ap.add_argument("--nested-nlive", type=int, default=32768, help="live points per GPU (0 = skip)")
     ap.add_argument("--nested-k", type=int, default=2048)
     ap.add_argument("--nested-nmcmc", type=int, default=200)
+    ap.add_argument("--nested-seeds", type=int, default=8,
+                    help="extra single-GPU nested runs per rank (own seeds) for the bias estimate")
     ap.add_argument("--cpu-seconds", type=float, default=1.5,
                     help="wall seconds of the CPU baseline sample (x threads = CPU work)")
     args = ap.parse_args()
@@ -180,6 +182,29 @@ def main():
                     nlive=args.nested_nlive * world, k=args.nested_k, nmcmc=args.nested_nmcmc,
                     n_dead=int(out.n_dead), wall_s=wall,
                     constrained_steps_per_s=float(out.n_gen) * args.nested_k * args.nested_nmcmc / wall)
+        # bias estimate: independent single-GPU runs on every rank (seeds distinct over ranks),
+        # their deltas gathered on rank 0 -- one run's delta is a single draw of sd ~ sigma
+        if args.nested_seeds > 0:
+            from mcmc_amd import Context, nested as _nested
+            deltas, sig1 = [], []
+            for i in range(args.nested_seeds):
+                with Context(seed=100 + rank * args.nested_seeds + i, device=local) as c:
+                    o = _nested.nested_evidence(lik, pri, nlive=args.nested_nlive, nmcmc=args.nested_nmcmc,
+                                                k=args.nested_k, mode_hopping_frac=0.1, ctx=c)
+                h = float(np.sum(np.exp(o[3]) * o.ll) - o[0])
+                deltas.append(o[0] - analytic_log_z(mu, sg))
+                sig1.append(math.sqrt(max(h, 0.0) / args.nested_nlive))
+            if dist:
+                allr = [None] * world
+                tdist.all_gather_object(allr, (deltas, sig1))
+                deltas = [x for r in allr for x in r[0]]
+                sig1 = [x for r in allr for x in r[1]]
+            d = np.array(deltas)
+            nest["seed_sweep"] = dict(
+                runs=len(d), nlive=args.nested_nlive, mean_delta=float(d.mean()),
+                stderr=float(d.std(ddof=1) / math.sqrt(len(d))) if len(d) > 1 else None,
+                sd_delta=float(d.std(ddof=1)) if len(d) > 1 else None, sigma=float(np.mean(sig1)),
+                frac_within_1sigma=float(np.mean(np.abs(d) <= np.array(sig1))))
 
     steps_total = float(N) * world * S * args.steps
     value = steps_total / elapsed
@@ -243,6 +268,8 @@ def log_evidence_line(nest, log_z_hm, lz_true):
                      "within_1sigma": d <= nest["sigma"],
                      "nested_run": {k: nest[k] for k in ("nlive", "k", "nmcmc", "n_dead", "H", "wall_s",
                                                          "constrained_steps_per_s")}})
+        if "seed_sweep" in nest:
+            line["seed_sweep"] = nest["seed_sweep"]
     else:
         line.update({"estimator": "harmonic mean", "abs_delta": abs(log_z_hm - lz_true)})
     return line
