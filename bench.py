@@ -58,13 +58,13 @@ def cpu_baseline(args, mu, sg, s):
                 1, [s])
     rng = np.random.default_rng(7)
 
-    def run(nch, nsteps):
+    def run(nch, nsteps, nthreads=threads):
         x0 = rng.normal(mu[:, None], sg[:, None], size=(D, nch))
         ll = np.array([m.loglik(x0[:, i]) for i in range(nch)])
         lp = np.full(nch, m.logprior(x0[:, 0]))
         t = time.perf_counter()
         O.mh_run(m, 1, x0, ll, lp, nbin=nsteps, nskip=1, n_rec=1, record_x=False, record_llp=False,
-                 record_accept=False, accumulate=False, nthreads=threads)
+                 record_accept=False, accumulate=False, nthreads=nthreads)
         return time.perf_counter() - t
 
     nch = 64 * threads * 4
@@ -72,9 +72,16 @@ def cpu_baseline(args, mu, sg, s):
     rate = nch * 20 / dt
     nsteps = max(20, int(args.cpu_seconds * rate / nch))
     dt = run(nch, nsteps)
+    # one core: the single-threaded ocamlopt-equivalent proxy, ~3 s sample
+    n1 = 256
+    d1 = run(n1, 20, 1)
+    s1 = max(20, int(3.0 * (n1 * 20 / d1) / n1))
+    d1 = run(n1, s1, 1)
     return dict(value=nch * nsteps / dt, unit="MH steps/s", cores=threads, kind="port",
                 sample="%d chains x %d steps of the C2 target (oracle/oracle.c, -O2, %d threads)"
-                       % (nch, nsteps, threads))
+                       % (nch, nsteps, threads),
+                single_core_value=n1 * s1 / d1,
+                single_core_sample="%d chains x %d steps, 1 thread" % (n1, s1))
 
 
 def pmc_traffic(D, N, S):

@@ -29,8 +29,20 @@ def _flat(samples):
             np.ascontiguousarray(lp, np.float64))
 
 
-def evidence_harmonic_mean(ctx_or_samples):
-    """n / sum_i exp(-ll_i) (evidence.ml:101-107)."""
+def evidence_harmonic_mean(ctx_or_samples, naive=False):
+    """n / sum_i exp(-ll_i) (evidence.ml:101-107).  naive=True (sample arrays only) runs the
+    reference's linear-space loop itself, 1/exp(ll) summed in order, so it also reproduces its
+    overflow (ll < -709: the sum is inf and Z = 0) and underflow (ll > 709: 1/inf = 0)."""
+    if naive:
+        if hasattr(ctx_or_samples, "stats"):
+            raise ValueError("naive harmonic mean needs the sample array, not a context")
+        _, ll, _ = _flat(ctx_or_samples)
+        with np.errstate(over="ignore", divide="ignore"):
+            inv = (1.0 / np.exp(ll)).tolist()           # elementwise, as the reference's loop body
+        linv = 0.0
+        for v in inv:                                   # sequential left fold, in sample order
+            linv += v
+        return float(len(ll)) / linv if linv != 0.0 else float("inf")
     return float(np.exp(log_evidence_harmonic_mean(ctx_or_samples)))
 
 

@@ -82,3 +82,18 @@ def test_argument_errors(E):
     from mcmc_amd._lib import InvalidArgument
     with pytest.raises(InvalidArgument):
         E.evidence_direct((np.zeros((0, 2)), np.zeros(0), np.zeros(0)))
+
+
+def test_harmonic_mean_naive_mode(oracle, E, R):
+    """naive=True: the reference's linear-space loop (evidence.ml:101-107), including its
+    overflow (exp(-ll) = inf -> Z = 0) and underflow (all 1/exp(ll) = 0 -> Z = inf)."""
+    s = mcmc_samples(oracle, [0.2], [0.7], (PRIOR_FLAT, []), 2000, 11, [0.7])
+    ll = np.ascontiguousarray(s.log_likelihood[:, 0])
+    got = E.evidence_harmonic_mean(s, naive=True)
+    want = oracle.lib().or_harmonic_mean_naive(oracle.dptr(ll), len(ll))
+    assert abs(got - want) < 1e-13 * want
+    pts = np.zeros((2, 1))
+    assert E.evidence_harmonic_mean((pts, np.array([-800.0, 0.0]), np.zeros(2)), naive=True) == 0.0
+    assert E.evidence_harmonic_mean((pts, np.array([800.0, 800.0]), np.zeros(2)), naive=True) == np.inf
+    lz = E.log_evidence_harmonic_mean((pts, np.array([-800.0, 0.0]), np.zeros(2)))   # log-space form
+    assert abs(lz - (np.log(2.0) - 800.0)) < 1e-12 * 800
