@@ -5,7 +5,9 @@
 // the k new keys -> merge them into the n-k survivors (+ stop test).  All of it is enqueued
 // asynchronously in batches of generations; the device-side stop flag turns the kernels of any
 // generation after the stopping one into no-ops, so the host only synchronises once per batch.
-// evidence_error_and_weights (nested.ml:81-120) runs once on the host over the final points.
+// Batches are pipelined: while the GPU runs batch b + 1, a host worker folds batch b's dead
+// points into evidence_error_and_weights (nested.ml:81-120); the live points are folded in once
+// the run has stopped.
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -40,6 +42,18 @@ struct NestedBufs {
   DevBuf x, ll, lp, nx, nll, nlp, tv, prefix, qadd, st, dead_x, dead_ll, dead_lp, runl, runj;
   KeyBuf keys[2], newk, newk_tmp;
   int64_t dead_cap = 0;
+  // pinned staging of two in-flight batches' dead (ll, lp) and their completion events
+  double* h_stage[4] = {nullptr, nullptr, nullptr, nullptr};
+  int64_t h_cap = 0;
+  NestDevState* h_st = nullptr;
+  hipEvent_t done[2] = {nullptr, nullptr};
+  ~NestedBufs() {
+    for (auto h : h_stage)
+      if (h) (void)hipHostFree(h);
+    if (h_st) (void)hipHostFree(h_st);
+    for (auto e : done)
+      if (e) (void)hipEventDestroy(e);
+  }
 };
 
 double lse_host(double a, double b) {            // Stats.log_sum_logs (stats.ml:240-248)
@@ -50,82 +64,132 @@ double lse_host(double a, double b) {            // Stats.log_sum_logs (stats.ml
 
 // nested.ml:81-120; dead point i was retired with n - (i mod k) live points.
 // The reference is one loop of four log-sums per point: two running sums (low, high) and two
-// weight updates.  The running sums fold blocks of iterations in parallel (below); each weight
-// receives at most two contributions, from the neighbouring iterations, so the weights are
-// computed per index in parallel by replaying exactly those contributions in loop order.
-void evidence_weights(int64_t n, int64_t nlive, int64_t k, const double* ll, double* log_ev,
-                      double* log_dev, double* wts) {
-  const double log_half = -0.69314718055994530942;
-  const int64_t ilive = n - nlive;
-  std::vector<double> prefix((size_t)k + 1, 0.0);
-  for (int64_t j = 0; j < k; ++j) prefix[j + 1] = prefix[j] + std::log1p(-1.0 / (double)(nlive - j));
-  auto ldv_dead = [&](int64_t i) {
-    if (k == 1) return std::log(1.0 / (double)nlive) + (double)i * std::log1p(-1.0 / (double)nlive);
-    const int64_t j = i % k, g = i / k;
-    return std::log(1.0 / (double)(nlive - j)) + ((double)g * prefix[k] + prefix[j]);
-  };
-  double ldv_live;
-  if (k == 1) {
-    ldv_live = std::log(1.0 / (double)nlive) + (double)(ilive - 1) * std::log1p(-1.0 / (double)nlive);
-  } else {
-    const int64_t g = ilive / k, j = ilive % k;
-    ldv_live = ((double)g * prefix[k] + prefix[j]) + std::log(1.0 / (double)nlive);
+// weight updates.  The running sums fold blocks of kEvBlock iterations (in parallel), then fold
+// the block results in order -- the reference's fold exactly for n <= kEvBlock, within rounding
+// beyond (the oracle folds the same blocks, oracle.c or_evidence_weights).  Each weight receives
+// at most two contributions, from the neighbouring iterations, so the weights are computed per
+// index in parallel by replaying exactly those contributions in loop order.
+//
+// The fold is incremental: while the GPU runs a batch of generations, advance() folds every
+// block and weight whose inputs are dead points already on the host; finish() does the rest
+// (the live points, ldv_live) once the run has stopped.
+constexpr int64_t kEvBlock = 65536;
+constexpr double kLogHalf = -0.69314718055994530942;
+
+template <class F>
+void parallel_for(int64_t lo, int64_t hi, int threads, F f) {
+  if (hi <= lo) return;
+  const int64_t T = std::max<int64_t>(1, std::min<int64_t>(threads, hi - lo));
+  if (T == 1) {
+    for (int64_t i = lo; i < hi; ++i) f(i);
+    return;
   }
-  // iteration i's (dl, dh): first loop i < ilive, second loop i >= ilive (nested.ml:90-113)
-  auto dl = [&](int64_t i) { return i < ilive ? ldv_dead(i) + ll[i] : ldv_live + ll[i - 1]; };
-  auto dh = [&](int64_t i) { return i < ilive ? ldv_dead(i) + ll[i + 1] : ldv_live + ll[i]; };
-  // running sums: sequential log-sums over blocks of kEvBlock iterations (in parallel), then a
-  // sequential log-sum of the block results -- the reference's fold exactly for n <= kEvBlock,
-  // within rounding beyond (the oracle folds the same blocks, oracle.c or_evidence_weights)
-  constexpr int64_t kEvBlock = 65536;
-  const int64_t nb = (n + kEvBlock - 1) / kEvBlock;
-  std::vector<double> blow((size_t)nb, -HUGE_VAL), bhigh((size_t)nb, -HUGE_VAL);
-  std::vector<std::thread> tb;
-  const int TB = (int)std::max<int64_t>(1, std::min<int64_t>(nb, 8));
-  for (int t = 0; t < TB; ++t)
-    tb.emplace_back([&, t] {
-      for (int64_t b = t; b < nb; b += TB) {
-        double lo = -HUGE_VAL, hi = -HUGE_VAL;
-        for (int64_t i = b * kEvBlock; i < std::min(n, (b + 1) * kEvBlock); ++i) {
-          lo = lse_host(lo, dl(i));
-          hi = lse_host(hi, dh(i));
-        }
-        blow[(size_t)b] = lo;
-        bhigh[(size_t)b] = hi;
-      }
-    });
-  // weight m: first loop dh(m-1) then dl(m); second loop dh(m) then dl(m+1)
-  auto weight = [&](int64_t m) {
-    double w = -HUGE_VAL;
-    if (m >= 1 && m - 1 < ilive) w = lse_host(w, log_half + dh(m - 1));
-    if (m < ilive) w = lse_host(w, log_half + dl(m));
-    if (m >= ilive) w = lse_host(w, log_half + dh(m));
-    if (m + 1 >= ilive && m + 1 < n) w = lse_host(w, log_half + dl(m + 1));
-    return w;
-  };
-  const int T = (int)std::max<unsigned>(1, std::min<unsigned>(14, std::thread::hardware_concurrency()));
   std::vector<std::thread> tw;
-  for (int t = 0; t < T; ++t)
+  for (int64_t t = 0; t < T; ++t)
     tw.emplace_back([&, t] {
-      for (int64_t m = t * n / T; m < (t + 1) * n / T; ++m) wts[m] = weight(m);
-    });
-  for (auto& x : tw) x.join();
-  for (auto& x : tb) x.join();
-  double low = -HUGE_VAL, high = -HUGE_VAL;
-  for (int64_t b = 0; b < nb; ++b) {
-    low = lse_host(low, blow[(size_t)b]);
-    high = lse_host(high, bhigh[(size_t)b]);
-  }
-  *log_ev = log_half + lse_host(low, high);
-  *log_dev = high + std::log1p(-std::exp(low - high));
-  const double le = *log_ev;
-  tw.clear();
-  for (int t = 0; t < T; ++t)
-    tw.emplace_back([&, t] {
-      for (int64_t m = t * n / T; m < (t + 1) * n / T; ++m) wts[m] = wts[m] - le;
+      for (int64_t i = lo + t * (hi - lo) / T; i < lo + (t + 1) * (hi - lo) / T; ++i) f(i);
     });
   for (auto& x : tw) x.join();
 }
+
+class EvFold {
+ public:
+  EvFold(int64_t nlive, int64_t k) : n_(nlive), k_(k), prefix_((size_t)k + 1, 0.0) {
+    for (int64_t j = 0; j < k; ++j) prefix_[j + 1] = prefix_[j] + std::log1p(-1.0 / (double)(nlive - j));
+    threads_ = (int)std::max<unsigned>(1, std::min<unsigned>(14, std::thread::hardware_concurrency()));
+    // while the GPU runs (on the fold worker, beside the launching thread)
+    const char* e = std::getenv("MCG_NESTED_FOLD_THREADS");
+    stream_threads_ = std::max(1, std::min(threads_, e ? std::atoi(e) : 6));
+  }
+
+  // ll[0, avail) are dead points (avail <= ilive): fold the blocks and weights that need no
+  // later point; wts must hold avail entries
+  void advance(const double* ll, int64_t avail, double* wts) {
+    View v{this, ll, INT64_MAX, 0.0};
+    // block b is complete when its last iteration's ll[i + 1] is known: (b + 1) B < avail
+    const int64_t nb = avail > 0 ? (avail - 1) / kEvBlock : 0;
+    fold_blocks(v, nb, stream_threads_);
+    // weight m (dead, with m + 1 dead too) needs ll[m] only: m < avail - 1
+    const int64_t wend = std::max<int64_t>(wdone_, avail - 1);
+    parallel_for(wdone_, wend, stream_threads_, [&](int64_t m) { wts[m] = v.weight(m); });
+    wdone_ = wend;
+  }
+
+  // all ntot points known (ilive dead ones): fold the rest, combine, normalise
+  void finish(const double* ll, int64_t ntot, double* wts, double* log_ev, double* log_dev) {
+    const int64_t ilive = ntot - n_;
+    View v{this, ll, ilive, 0.0};
+    v.ntot = ntot;
+    if (k_ == 1) {
+      v.ldv_live = std::log(1.0 / (double)n_) + (double)(ilive - 1) * std::log1p(-1.0 / (double)n_);
+    } else {
+      const int64_t g = ilive / k_, j = ilive % k_;
+      v.ldv_live = ((double)g * prefix_[(size_t)k_] + prefix_[(size_t)j]) + std::log(1.0 / (double)n_);
+    }
+    fold_blocks(v, (ntot + kEvBlock - 1) / kEvBlock, threads_);
+    parallel_for(wdone_, ntot, threads_, [&](int64_t m) { wts[m] = v.weight(m); });
+    double low = -HUGE_VAL, high = -HUGE_VAL;
+    for (size_t b = 0; b < blow_.size(); ++b) {
+      low = lse_host(low, blow_[b]);
+      high = lse_host(high, bhigh_[b]);
+    }
+    *log_ev = kLogHalf + lse_host(low, high);
+    *log_dev = high + std::log1p(-std::exp(low - high));
+    const double le = *log_ev;
+    parallel_for(0, threads_, threads_, [&](int64_t t) {
+      for (int64_t m = t * ntot / threads_; m < (t + 1) * ntot / threads_; ++m) wts[m] -= le;
+    });
+  }
+
+ private:
+  struct View {
+    const EvFold* f;
+    const double* ll;
+    int64_t ilive;                      // INT64_MAX while streaming (every index is dead)
+    double ldv_live;
+    int64_t ntot = INT64_MAX;
+    double ldv_dead(int64_t i) const {
+      if (f->k_ == 1) return std::log(1.0 / (double)f->n_) + (double)i * std::log1p(-1.0 / (double)f->n_);
+      const int64_t j = i % f->k_, g = i / f->k_;
+      return std::log(1.0 / (double)(f->n_ - j)) + ((double)g * f->prefix_[(size_t)f->k_] + f->prefix_[(size_t)j]);
+    }
+    // iteration i's (dl, dh): first loop i < ilive, second loop i >= ilive (nested.ml:90-113)
+    double dl(int64_t i) const { return i < ilive ? ldv_dead(i) + ll[i] : ldv_live + ll[i - 1]; }
+    double dh(int64_t i) const { return i < ilive ? ldv_dead(i) + ll[i + 1] : ldv_live + ll[i]; }
+    // weight m: first loop dh(m-1) then dl(m); second loop dh(m) then dl(m+1)
+    double weight(int64_t m) const {
+      double w = -HUGE_VAL;
+      if (m >= 1 && m - 1 < ilive) w = lse_host(w, kLogHalf + dh(m - 1));
+      if (m < ilive) w = lse_host(w, kLogHalf + dl(m));
+      if (m >= ilive) w = lse_host(w, kLogHalf + dh(m));
+      if (m + 1 >= ilive && m + 1 < ntot) w = lse_host(w, kLogHalf + dl(m + 1));
+      return w;
+    }
+  };
+
+  void fold_blocks(const View& v, int64_t nb, int threads) {
+    const int64_t b0 = (int64_t)blow_.size();
+    if (nb <= b0) return;
+    blow_.resize((size_t)nb, -HUGE_VAL);
+    bhigh_.resize((size_t)nb, -HUGE_VAL);
+    const int64_t end = std::min<int64_t>(v.ntot, nb * kEvBlock);
+    parallel_for(b0, nb, threads, [&](int64_t b) {
+      double lo = -HUGE_VAL, hi = -HUGE_VAL;
+      for (int64_t i = b * kEvBlock; i < std::min(end, (b + 1) * kEvBlock); ++i) {
+        lo = lse_host(lo, v.dl(i));
+        hi = lse_host(hi, v.dh(i));
+      }
+      blow_[(size_t)b] = lo;
+      bhigh_[(size_t)b] = hi;
+    });
+  }
+
+  int64_t n_, k_;
+  std::vector<double> prefix_;
+  int threads_ = 1, stream_threads_ = 1;
+  std::vector<double> blow_, bhigh_;
+  int64_t wdone_ = 0;
+};
 
 }  // namespace
 
@@ -226,14 +290,30 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
                       B.keys[1].s(), n, &in_tmp, s, nullptr), "sort live keys");
   const int base = in_tmp ? 1 : 0;                   // generation g reads keys[(base + g) % 2]
 
-  int64_t gen = 0, reported = 0;
-  int64_t batch = 4;
-  NestDevState st{};
-  std::vector<double> hx, hll, hlp;
-  for (;;) {
-    const int64_t remaining = max_dead / k - gen;
-    if (remaining <= 0) break;
-    const int64_t G = std::min(batch, remaining);
+  // Batches of generations, pipelined: while the GPU runs batch b + 1, the host appends batch b's
+  // dead ll / lp (copied into pinned staging behind b's kernels) and folds them into the
+  // evidence sums (EvFold::advance).  The dead rows themselves stay on the device.
+  NestedState& R = ctx->nested;
+  R.ll.clear();
+  R.lp.clear();
+  R.wts.clear();
+  EvFold fold(n, k);
+  constexpr int64_t kMaxBatch = 64;
+  if (B.h_cap < kMaxBatch * k) {
+    for (auto& h : B.h_stage) {
+      if (h) (void)hipHostFree(h);
+      h = nullptr;
+    }
+    for (auto& h : B.h_stage) HC(hipHostMalloc(&h, (size_t)(kMaxBatch * k) * 8, 0), "alloc pinned staging");
+    B.h_cap = kMaxBatch * k;
+  }
+  // the state copies land in pinned memory too: an async copy into pageable memory would block
+  // the host until the batch completes and serialise the pipeline
+  if (!B.h_st) HC(hipHostMalloc((void**)&B.h_st, 2 * sizeof(NestDevState), 0), "alloc pinned state");
+  NestDevState* hst = B.h_st;
+  int64_t gen = 0, reported = 0, batch = 4;
+  // enqueue generations [gen, gen + G) and the copies of their state / dead ll, lp into slot q
+  auto launch_batch = [&](int64_t G, int q) -> int {
     const int64_t need = (gen + G) * k;
     if (need > B.dead_cap) {
       const int64_t cap = std::max<int64_t>(need, std::max<int64_t>(2 * B.dead_cap, 16 * n));
@@ -282,40 +362,88 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
       KeyBuf& nk = nk_tmp ? B.newk_tmp : B.newk;
       HC(launch_merge_new(a, nxt.l(), nxt.t(), nxt.s(), nk.l(), nk.t(), nk.s(), s), "merge keys");
     }
+    HC(hipMemcpyAsync(&hst[q], B.st.p, sizeof(NestDevState), hipMemcpyDeviceToHost, s), "read state");
+    HC(hipMemcpyAsync(B.h_stage[2 * q], (double*)B.dead_ll.p + gen * k, G * k * 8, hipMemcpyDeviceToHost, s),
+       "stage dead ll");
+    HC(hipMemcpyAsync(B.h_stage[2 * q + 1], (double*)B.dead_lp.p + gen * k, G * k * 8, hipMemcpyDeviceToHost, s),
+       "stage dead lp");
+    HC(hipEventRecord(B.done[q], s), "record batch");
     gen += G;
-    HC(hipMemcpyAsync(&st, B.st.p, sizeof st, hipMemcpyDeviceToHost, s), "read state");
-    HC(hipStreamSynchronize(s), "nested sync");
-    const int64_t ndead = st.gen_done * k;
-    if (observer && ndead > reported) {
-      const int64_t m = ndead - reported;
-      hx.resize(m * D); hll.resize(m); hlp.resize(m);
-      HC(hipMemcpy(hx.data(), (double*)B.dead_x.p + reported * D, m * D * 8, hipMemcpyDeviceToHost), "observer copy");
-      HC(hipMemcpy(hll.data(), (double*)B.dead_ll.p + reported, m * 8, hipMemcpyDeviceToHost), "observer copy");
-      HC(hipMemcpy(hlp.data(), (double*)B.dead_lp.p + reported, m * 8, hipMemcpyDeviceToHost), "observer copy");
-      observer(user, hx.data(), hll.data(), hlp.data(), m);
-      reported = ndead;
+    return MCG_OK;
+  };
+  for (auto& e : B.done)
+    if (!e) HC(hipEventCreateWithFlags(&e, hipEventDisableTiming), "create event");
+  int q = 0;
+  double t_launch = 0, t_wait = 0, t_fold = 0;
+  std::thread fw;                                     // fold worker (EvFold::advance)
+  struct Joiner {
+    std::thread& t;
+    ~Joiner() {
+      if (t.joinable()) t.join();
     }
+  } fw_guard{fw};
+  int64_t G = std::min<int64_t>(batch, max_dead / k);
+  if (G <= 0) return set_error(ctx, MCG_EINVAL, "max_dead below one generation");
+  if ((rc = launch_batch(G, q))) return rc;
+  int64_t gen_q = 0;                                  // first generation of the batch in slot q
+  NestDevState st{};
+  std::vector<double> hx;
+  for (;;) {
+    const auto tw0 = now();
+    HC(hipEventSynchronize(B.done[q]), "nested sync");
+    t_wait += ms(tw0, now());
+    st = hst[q];
     if (st.error)
       return set_error(ctx, MCG_EFAIL, "Error in draw_new_live_point: new log(L) below the threshold");
-    if (st.stopped) break;
-    batch = std::min<int64_t>(batch * 2, 64);
+    const int64_t remaining = max_dead / k - gen;
+    const bool last = st.stopped || remaining <= 0;
+    const int64_t gen_b = gen_q;
+    if (!last) {                                      // keep the GPU busy: enqueue the next batch
+      batch = std::min<int64_t>(batch * 2, kMaxBatch);
+      gen_q = gen;
+      const auto tl = now();
+      if ((rc = launch_batch(std::min(batch, remaining), q ^ 1))) return rc;
+      t_launch += ms(tl, now());
+    }
+    // the fold worker must be done with R.ll / R.wts before they grow
+    const auto tf = now();
+    if (fw.joinable()) fw.join();
+    t_fold += ms(tf, now());
+    // this batch's dead points: generations [gen_b, st.gen_done) of the ones it launched
+    const int64_t d0 = gen_b * k, d1 = st.gen_done * k;
+    if (d1 > d0) {
+      R.ll.insert(R.ll.end(), B.h_stage[2 * q], B.h_stage[2 * q] + (d1 - d0));
+      R.lp.insert(R.lp.end(), B.h_stage[2 * q + 1], B.h_stage[2 * q + 1] + (d1 - d0));
+    }
+    const int64_t ndead = d1;
+    if (observer && ndead > reported) {
+      const int64_t m = ndead - reported;
+      hx.resize(m * D);
+      HC(hipMemcpy(hx.data(), (double*)B.dead_x.p + reported * D, m * D * 8, hipMemcpyDeviceToHost), "observer copy");
+      observer(user, hx.data(), R.ll.data() + reported, R.lp.data() + reported, m);
+      reported = ndead;
+    }
+    if (last) break;
+    // fold what is final on the worker while this thread keeps the GPU fed
+    R.wts.resize(R.ll.size());
+    fw = std::thread([&fold, llp = R.ll.data(), av = (int64_t)R.ll.size(), wp = R.wts.data()] {
+      fold.advance(llp, av, wp);
+    });
+    q ^= 1;
   }
   const auto t_gen = now();
+  if (prof)
+    std::fprintf(stderr, "mcg_nested: host launch %.1f ms, wait %.1f ms, fold join %.1f ms\n", t_launch, t_wait, t_fold);
   // final: dead points in retirement order, then the live set ascending (nested.ml:143)
   const int64_t ndead = st.gen_done * k;
   const int64_t ntot = ndead + n;
   KeyBuf& fin = B.keys[(base + st.gen_done) % 2];
-  NestedState& R = ctx->nested;
   // the dead rows stay on the device (B.dead_x) until mcg_nested_get copies them straight into
   // the caller's buffer; the host keeps ll / lp (for the weights) and the final live rows
   R.pts.assign((size_t)n * D, 0.0);
   R.ll.resize((size_t)ntot);
   R.lp.resize((size_t)ntot);
   R.wts.resize((size_t)ntot);
-  if (ndead > 0) {
-    HC(hipMemcpy(R.ll.data(), B.dead_ll.p, ndead * 8, hipMemcpyDeviceToHost), "copy dead");
-    HC(hipMemcpy(R.lp.data(), B.dead_lp.p, ndead * 8, hipMemcpyDeviceToHost), "copy dead");
-  }
   std::vector<int> slots((size_t)n);
   std::vector<double> lx((size_t)n * D), lll((size_t)n), llp((size_t)n);
   HC(hipMemcpy(slots.data(), fin.slot.p, n * 4, hipMemcpyDeviceToHost), "copy keys");
@@ -329,7 +457,7 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
     R.lp[(size_t)(ndead + j)] = llp[(size_t)sl];
   }
   const auto t_copy = now();
-  evidence_weights(ntot, n, k, R.ll.data(), &R.log_ev, &R.log_dev, R.wts.data());
+  fold.finish(R.ll.data(), ntot, R.wts.data(), &R.log_ev, &R.log_dev);
   if (prof)
     std::fprintf(stderr, "mcg_nested: generations %.1f ms, final copies %.1f ms, weights %.1f ms\n",
                  ms(t_start, t_gen), ms(t_gen, t_copy), ms(t_copy, now()));
@@ -352,6 +480,7 @@ int mcg_nested_get(mcg_ctx* ctx, double* pts, double* ll, double* lp, double* lo
   if (!ctx) return MCG_EINVAL;
   const NestedState& R = ctx->nested;
   if (R.n_total == 0) return set_error(ctx, MCG_ESTATE, "no nested run");
+  const auto t0 = std::chrono::steady_clock::now();
   if (pts) {
     const int64_t D = (int64_t)(R.pts.size() / (size_t)R.nlive);
     if (R.n_dead > 0) {
@@ -361,9 +490,14 @@ int mcg_nested_get(mcg_ctx* ctx, double* pts, double* ll, double* lp, double* lo
     }
     std::copy(R.pts.begin(), R.pts.end(), pts + R.n_dead * D);
   }
+  const auto t1 = std::chrono::steady_clock::now();
   if (ll) std::copy(R.ll.begin(), R.ll.end(), ll);
   if (lp) std::copy(R.lp.begin(), R.lp.end(), lp);
   if (log_wts) std::copy(R.wts.begin(), R.wts.end(), log_wts);
+  if (std::getenv("MCG_NESTED_PROFILE"))
+    std::fprintf(stderr, "mcg_nested_get: points %.1f ms, ll/lp/wts %.1f ms\n",
+                 std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
   return MCG_OK;
 }
 
