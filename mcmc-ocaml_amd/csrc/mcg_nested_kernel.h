@@ -219,6 +219,31 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
     // the PD Philox / Box-Muller / log chains overlap instead of sitting in the serial chain
     double dsc_g[PD], lu_g[PD];
     uint32_t ip_g[PD], jp_g[PD];
+    if constexpr (P == 4 && PD == 4) {
+      // lane q of the walker's quad draws every random number of step s0 + q (its DE scale and
+      // accept uniform, and the DE indices of step s0 + q + PD, whose rows refill slot q); the
+      // quad broadcasts (DPP) hand step u's values from lane u to the whole quad.  Each lane
+      // runs three Philox calls, one Box-Muller and one log per group instead of per step.
+      const int64_t sq = s0 + sub;
+      const u32x4 rI = rng(wid, (uint32_t)(sq + PD), CALL_DE_IDX, TAG_NEST_WALK, 0u);
+      const u32x4 rS = rng(wid, (uint32_t)sq, CALL_DE_SCALE, TAG_NEST_WALK, 0u);
+      const u32x4 rA = rng(wid, (uint32_t)sq, CALL_ACCEPT, TAG_NEST_WALK, 0u);
+      const uint32_t pi = randint(rI.x, rI.y, n);
+      const uint32_t pjj = randint(rI.z, rI.w, n - 1);
+      const uint32_t pj = pjj + (pjj >= pi ? 1u : 0u);
+      double z0, z1;
+      normal_pair(rS.z, rS.w, z0, z1, s_lt, s_at);
+      const double dloc = (a.mode_hop != 0.0 && u53(rS.x, rS.y) < a.mode_hop) ? 1.0 : a.sigma_de * z0;
+      const double lloc = plog(u53(rA.x, rA.y), s_lt);
+      ip_g[0] = quad_bcast_u32<0>(pi); ip_g[1] = quad_bcast_u32<1>(pi);
+      ip_g[2] = quad_bcast_u32<2>(pi); ip_g[3] = quad_bcast_u32<3>(pi);
+      jp_g[0] = quad_bcast_u32<0>(pj); jp_g[1] = quad_bcast_u32<1>(pj);
+      jp_g[2] = quad_bcast_u32<2>(pj); jp_g[3] = quad_bcast_u32<3>(pj);
+      dsc_g[0] = quad_bcast_f64<0>(dloc); dsc_g[1] = quad_bcast_f64<1>(dloc);
+      dsc_g[2] = quad_bcast_f64<2>(dloc); dsc_g[3] = quad_bcast_f64<3>(dloc);
+      lu_g[0] = quad_bcast_f64<0>(lloc); lu_g[1] = quad_bcast_f64<1>(lloc);
+      lu_g[2] = quad_bcast_f64<2>(lloc); lu_g[3] = quad_bcast_f64<3>(lloc);
+    } else
 #pragma unroll
     for (int u = 0; u < PD; ++u) {
       const int64_t s = s0 + u;
