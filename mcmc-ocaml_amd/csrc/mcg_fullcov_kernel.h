@@ -69,10 +69,10 @@ __global__ void __launch_bounds__(256, MCG_FC_MIN_WAVES) mh_fullcov_kernel(const
   using F = FcLayout<D>;
   constexpr int NL = F::NKB;
   __shared__ double2 s_lt[kLogTabN];
-  __shared__ double2 s_at[kAngTabN];
+  __shared__ double2 s_nt[kNrmTabN];
   __shared__ double s_u[F::NFRAG * 64];
   for (int i = threadIdx.x; i < kLogTabN; i += blockDim.x) s_lt[i] = kLogTab[i];
-  for (int i = threadIdx.x; i < kAngTabN; i += blockDim.x) s_at[i] = kAngTab[i];
+  for (int i = threadIdx.x; i < kNrmTabN; i += blockDim.x) s_nt[i] = kNrmTab[i];
   {
     // U fragments in lane order: frag (ib, kb), lane l -> U[16 ib + (l & 15)][4 kb + (l >> 4)],
     // zero below the diagonal (the oracle's chains start at j = i)
@@ -179,8 +179,10 @@ __global__ void __launch_bounds__(256, MCG_FC_MIN_WAVES) mh_fullcov_kernel(const
       asm volatile("" ::: "memory");
       const u32x4 w = rng(gid, tlo, (uint32_t)(4 * m + q), TAG_MH, thi);
       double v[4];
-      normal_pair(w.x, w.y, v[0], v[1], s_lt, s_at);
-      normal_pair(w.z, w.w, v[2], v[3], s_lt, s_at);
+      v[0] = pnormal(w.x, s_nt);
+      v[1] = pnormal(w.y, s_nt);
+      v[2] = pnormal(w.z, s_nt);
+      v[3] = pnormal(w.w, s_nt);
       transpose_quadrants(v);                 // v[k'] = z[16 m + 4 k' + q]
 #pragma unroll
       for (int k2 = 0; k2 < 4; ++k2) {

@@ -149,30 +149,28 @@ __device__ __forceinline__ double psqrt(double a) {
   return a * y;
 }
 
-// Box-Muller pair from two words (spec v4): radius from a; angle 2 pi (b + 1/2) 2^-32 = theta_j + t
-// with j = b >> 22 (angle table, LDS-staged or kAngTab), t = 2 pi ((r + 1/2) 2^-22 - 1/2)/1024,
-// sin t / cos t by Taylor to t^5 / t^4 and a rotation by (cos theta_j, sin theta_j).
-__device__ __forceinline__ void normal_pair(uint32_t a, uint32_t b, double& z0, double& z1,
-                                            const double2* ltab = kLogTab,
-                                            const double2* atab = kAngTab) {
-  const double u1 = u32_open(a);
-  const double rho = psqrt(-2.0 * plog(u1, ltab));
-  const uint32_t j = b >> 22;
-  // (r + 1/2) 2^-22 - 1/2 exactly: (1 + (r + 1/2) 2^-22) - 3/2, r = b mod 2^22
-  const double tt = bitsd(((uint64_t)(0x3FF00000u | ((b & 0x3FFFFFu) >> 2)) << 32) |
-                          (uint64_t)((b << 30) | 0x20000000u)) - 1.5;
-  const double t = tt * 0x1.921fb54442d18p-8;
-  const double t2 = t * t;
-  const double t3 = t * t2;
-  const double ps = fma(t2, 0x1.1111111111111p-7, -0x1.5555555555555p-3);
-  const double st = fma(t3, ps, t);
-  const double pc = fma(t2, 0x1.5555555555555p-5, -0.5);
-  const double ct = fma(t2, pc, 1.0);
-  const double2 cs = atab[j];
-  const double cr = fma(cs.x, ct, -(cs.y * st));
-  const double sr = fma(cs.y, ct, cs.x * st);
-  z0 = rho * cr;
-  z1 = rho * sr;
+// standard normal from one 32-bit word (spec v5): the sign is bit 31; the other
+// 31 bits give v = 2w + 1 (odd), u = v 2^-33 in (0, 1/2).  double(v) = 2^E (1 + f) is exact; the
+// segment is (E, top kNrmS bits of f) = (high word >> 15) - (1023 << 5); the rest of f, put under
+// the exponent of 1.0, gives 1 + t/32 exactly, so x = t/32 with one exact subtraction, and
+// z = -+ p_seg(x): the segment's degree-5 polynomial in t (oracle/gen_tables.py), stored scaled by
+// 32^k so that Horner in x rounds exactly like the oracle's Horner in t.  Exactly symmetric:
+// flipping bit 31 negates z.  `tab` points at kNrmTab or at a copy staged in LDS (3 x 16-B gathers).
+static_assert(kNrmS == 5 && kNrmDeg == 5, "pnormal is written for 32 segments per octave, degree 5");
+__device__ __forceinline__ double pnormal(uint32_t w, const double2* tab) {
+  const uint32_t v = (w << 1) | 1u;
+  const double dv = (double)v;                                   // exact
+  const uint32_t hi = (uint32_t)__double2hiint(dv);
+  const uint32_t lo = (uint32_t)__double2loint(dv);
+  const double2* c = tab + 3u * ((hi >> 15) - (1023u << kNrmS));
+  const double x = __hiloint2double((int)((hi & 0x7FFFu) | 0x3FF00000u), (int)lo) - 1.0;
+  const double2 c0 = c[0], c1 = c[1], c2 = c[2];
+  double p = fma(c0.x, x, c0.y);
+  p = fma(p, x, c1.x);
+  p = fma(p, x, c1.y);
+  p = fma(p, x, c2.x);
+  p = fma(p, x, c2.y);
+  return __hiloint2double(__double2hiint(p) ^ (int)(w & 0x80000000u), __double2loint(p));
 }
 
 // log1p(r), r in [0,1] (Goldberg: r * log(1+r) / ((1+r)-1)); log-sum-exp on the portable

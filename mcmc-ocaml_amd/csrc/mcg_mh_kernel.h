@@ -5,7 +5,7 @@
 //   * P lanes per chain (P in {1,2,4,8}); lane `sub` owns the dims of Philox calls
 //     c = sub, sub+P, ... (4 dims per call); chain state stays in VGPRs for the whole launch;
 //   * SoA state x[d][chain] in HBM is read once and written once per launch (coalesced);
-//   * one Philox4x32-10 call gives 4 proposal normals (two Box-Muller pairs) per lane;
+//   * one Philox4x32-10 call gives 4 proposal normals (one quantile-table normal per word);
 //   * the log-target is a canonical 8-accumulator sum (reduction tree fixed, P-independent);
 //   * the accept test `log u < ratio` (mcmc.ml:49) is packed per step into a 64-lane
 //     wavefront ballot -> accept bitmap row;
@@ -293,9 +293,9 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
                                LIK == MCG_LIK_FLAT) && PROP == MCG_PROP_GAUSS;
   extern __shared__ double lds_acc[];
   __shared__ double2 s_lt[kLogTabN];                 // math tables staged in LDS (gathers)
-  __shared__ double2 s_at[kAngTabN];
+  __shared__ double2 s_nt[kNrmTabN];
   for (int i = threadIdx.x; i < kLogTabN; i += blockDim.x) s_lt[i] = kLogTab[i];
-  for (int i = threadIdx.x; i < kAngTabN; i += blockDim.x) s_at[i] = kAngTab[i];
+  for (int i = threadIdx.x; i < kNrmTabN; i += blockDim.x) s_nt[i] = kNrmTab[i];
   __syncthreads();
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int sub = (int)(tid & (P - 1));
@@ -443,8 +443,10 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
         const int cc = sub + P * i;
         const u32x4 w = rng(gid, tlo, (uint32_t)cc, TAG_MH, thi);
         double z[4];
-        normal_pair(w.x, w.y, z[0], z[1], s_lt, s_at);
-        normal_pair(w.z, w.w, z[2], z[3], s_lt, s_at);
+        z[0] = pnormal(w.x, s_nt);
+        z[1] = pnormal(w.y, s_nt);
+        z[2] = pnormal(w.z, s_nt);
+        z[3] = pnormal(w.w, s_nt);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           if (!L::valid(sub, i, k)) continue;
@@ -489,8 +491,10 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
           if (P == 1 && 4 * i >= D) continue;
           const u32x4 w = rng(gid, tlo, (uint32_t)cc, TAG_MH, thi);
           double z[4];
-          normal_pair(w.x, w.y, z[0], z[1], s_lt, s_at);
-          normal_pair(w.z, w.w, z[2], z[3], s_lt, s_at);
+          z[0] = pnormal(w.x, s_nt);
+          z[1] = pnormal(w.y, s_nt);
+          z[2] = pnormal(w.z, s_nt);
+          z[3] = pnormal(w.w, s_nt);
 #pragma unroll
           for (int k = 0; k < 4; ++k)
             if (L::valid(sub, i, k)) y[4 * i + k] = fma(qprop[L::dim(sub, i, k)], z[k], x[4 * i + k]);
@@ -554,8 +558,10 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
             if (4 * i >= D) continue;
             const u32x4 w = rng(gid, tlo, (uint32_t)i, TAG_MH, thi);
             double z[4];
-            normal_pair(w.x, w.y, z[0], z[1], s_lt, s_at);
-            normal_pair(w.z, w.w, z[2], z[3], s_lt, s_at);
+            z[0] = pnormal(w.x, s_nt);
+            z[1] = pnormal(w.y, s_nt);
+            z[2] = pnormal(w.z, s_nt);
+            z[3] = pnormal(w.w, s_nt);
 #pragma unroll
             for (int k = 0; k < 4; ++k)
               if (4 * i + k < D) y[4 * i + k] = fma(m[5 + 4 * i + k], z[k], x[4 * i + k]);

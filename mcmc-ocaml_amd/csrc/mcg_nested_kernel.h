@@ -155,9 +155,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   using Lay = Layout<D, P>;
   constexpr int NL = Lay::NL;
   __shared__ double2 s_lt[kLogTabN];                 // math tables staged in LDS (gathers)
-  __shared__ double2 s_at[kAngTabN];
   for (int i = threadIdx.x; i < kLogTabN; i += blockDim.x) s_lt[i] = kLogTab[i];
-  for (int i = threadIdx.x; i < kAngTabN; i += blockDim.x) s_at[i] = kAngTab[i];
   __syncthreads();
   if (a.st->stopped) return;
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -216,14 +214,14 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   // can count the in-flight loads (vmcnt) across iterations; steps past nmcmc only compute
   for (int64_t s0 = 0; s0 < a.nmcmc; s0 += PD) {
     // phase 1: the random numbers of the group's PD steps -- independent of the walker state, so
-    // the PD Philox / Box-Muller / log chains overlap instead of sitting in the serial chain
+    // the PD Philox / normal / log chains overlap instead of sitting in the serial chain
     double dsc_g[PD], lu_g[PD];
     uint32_t ip_g[PD], jp_g[PD];
     if constexpr (P == 4 && PD == 4) {
       // lane q of the walker's quad draws every random number of step s0 + q (its DE scale and
       // accept uniform, and the DE indices of step s0 + q + PD, whose rows refill slot q); the
       // quad broadcasts (DPP) hand step u's values from lane u to the whole quad.  Each lane
-      // runs three Philox calls, one Box-Muller and one log per group instead of per step.
+      // runs three Philox calls, one normal and one log per group instead of per step.
       const int64_t sq = s0 + sub;
       const u32x4 rI = rng(wid, (uint32_t)(sq + PD), CALL_DE_IDX, TAG_NEST_WALK, 0u);
       const u32x4 rS = rng(wid, (uint32_t)sq, CALL_DE_SCALE, TAG_NEST_WALK, 0u);
@@ -231,8 +229,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
       const uint32_t pi = randint(rI.x, rI.y, n);
       const uint32_t pjj = randint(rI.z, rI.w, n - 1);
       const uint32_t pj = pjj + (pjj >= pi ? 1u : 0u);
-      double z0, z1;
-      normal_pair(rS.z, rS.w, z0, z1, s_lt, s_at);
+      const double z0 = pnormal(rS.z, kNrmTab);
       const double dloc = (a.mode_hop != 0.0 && u53(rS.x, rS.y) < a.mode_hop) ? 1.0 : a.sigma_de * z0;
       const double lloc = plog(u53(rA.x, rA.y), s_lt);
       ip_g[0] = quad_bcast_u32<0>(pi); ip_g[1] = quad_bcast_u32<1>(pi);
@@ -257,8 +254,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
         const u32x4 r = rng(wid, (uint32_t)(sub == 0 ? sp : s), call, TAG_NEST_WALK, 0u);
         const uint32_t pi = randint(r.x, r.y, n);
         const uint32_t pjj = randint(r.z, r.w, n - 1);
-        double z0, z1;
-        normal_pair(r.z, r.w, z0, z1, s_lt, s_at);
+        const double z0 = pnormal(r.z, kNrmTab);
         const double hop_u = u53(r.x, r.y);
         const double dloc = (a.mode_hop != 0.0 && hop_u < a.mode_hop) ? 1.0 : a.sigma_de * z0;
         const double lloc = plog(hop_u, s_lt);
@@ -273,9 +269,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
         if (a.mode_hop != 0.0 && u53(rs.x, rs.y) < a.mode_hop) {
           dsc_g[u] = 1.0;
         } else {
-          double z0, z1;
-          normal_pair(rs.z, rs.w, z0, z1, s_lt, s_at);
-          dsc_g[u] = a.sigma_de * z0;
+          dsc_g[u] = a.sigma_de * pnormal(rs.z, kNrmTab);
         }
         const u32x4 ra = rng(wid, (uint32_t)s, CALL_ACCEPT, TAG_NEST_WALK, 0u);
         lu_g[u] = plog(u53(ra.x, ra.y), s_lt);

@@ -63,7 +63,7 @@ __device__ __forceinline__ double rj_ljp_to(const double* to, int Dm, int kind, 
 template <int DM>
 __device__ __forceinline__ int rj_draw(const double* x, double* y, int Dm, int kind, const double* q,
                                        const KdView& kd, const Rng& rng, uint32_t gid, uint32_t tlo,
-                                       uint32_t thi, const double2* lt, const double2* at) {
+                                       uint32_t thi, const double2* lt, const double2* nt) {
 #pragma unroll
   for (int d = 0; d < DM; ++d) y[d] = 0.0;
   if (kind == MCG_RJ_JUMP_GAUSS || kind == MCG_RJ_JUMP_INDEP_GAUSS) {
@@ -71,8 +71,10 @@ __device__ __forceinline__ int rj_draw(const double* x, double* y, int Dm, int k
     for (int i = 0; 4 * i < DM; ++i) {
       const u32x4 w = rng(gid, tlo, (uint32_t)i, TAG_MH, thi);
       double z[4];
-      normal_pair(w.x, w.y, z[0], z[1], lt, at);
-      normal_pair(w.z, w.w, z[2], z[3], lt, at);
+      z[0] = pnormal(w.x, nt);
+      z[1] = pnormal(w.y, nt);
+      z[2] = pnormal(w.z, nt);
+      z[3] = pnormal(w.w, nt);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int d = 4 * i + k;
@@ -117,9 +119,9 @@ __device__ __forceinline__ int rj_draw(const double* x, double* y, int Dm, int k
 template <int DM>
 __global__ void __launch_bounds__(256) rj_kernel(const MhArgs a) {
   __shared__ double2 s_lt[kLogTabN];
-  __shared__ double2 s_at[kAngTabN];
+  __shared__ double2 s_nt[kNrmTabN];
   for (int i = threadIdx.x; i < kLogTabN; i += blockDim.x) s_lt[i] = kLogTab[i];
-  for (int i = threadIdx.x; i < kAngTabN; i += blockDim.x) s_at[i] = kAngTab[i];
+  for (int i = threadIdx.x; i < kNrmTabN; i += blockDim.x) s_nt[i] = kNrmTab[i];
   __syncthreads();
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = tid < a.N;
@@ -168,7 +170,7 @@ __global__ void __launch_bounds__(256) rj_kernel(const MhArgs a) {
     const int Dy = (int)hy[0];
     const int jk = internal ? (int)hy[5] : (int)hy[6];
     const double* jq = H + (int64_t)(internal ? hy[9] : hy[10]);
-    const int leaf = rj_draw<DM>(x, y, Dy, jk, jq, a.rj_kd[ytag], rng, gid, tlo, thi, s_lt, s_at);
+    const int leaf = rj_draw<DM>(x, y, Dy, jk, jq, a.rj_kd[ytag], rng, gid, tlo, thi, s_lt, s_nt);
     // ---- log_jump_prob (mcmc.ml:104-112) ----
     double lf, lb;
     if (internal) {

@@ -147,28 +147,26 @@ double or_sqrt(double a) {
   return a * y;
 }
 
-/* Box-Muller from two 32-bit words (spec v4): radius from a, angle 2 pi (b + 1/2) 2^-32 from b
-   through the 1024-entry angle table: theta = theta_j + t, j = b >> 22, t = 2 pi ((r + 1/2)
-   2^-22 - 1/2) / 1024 (r = b mod 2^22, |t| <= pi/1024), sin t / cos t by their Taylor
-   polynomials to t^5 / t^4, rotated by (cos theta_j, sin theta_j).  Table entries j + 512 are
-   exact negations of entries j, so b -> b + 2^31 maps (z0, z1) -> (-z0, -z1) exactly. */
-void or_normal_pair(uint32_t a, uint32_t b, double* z0, double* z1) {
-  double u1 = ((double)a + 0.5) * 0x1p-32;
-  double rho = or_sqrt(-2.0 * or_log(u1));
-  uint32_t j = b >> 22;
-  double tt = ((double)(b & 0x3FFFFFu) + 0.5) * 0x1p-22 - 0.5;     /* exact */
-  double t = tt * 0x1.921fb54442d18p-8;                             /* RN(pi/512) */
-  double t2 = t * t;
-  double t3 = t * t2;
-  double ps = fma(t2, 0x1.1111111111111p-7, -0x1.5555555555555p-3);   /* 1/120, -1/6 */
-  double st = fma(t3, ps, t);
-  double pc = fma(t2, 0x1.5555555555555p-5, -0.5);                   /* 1/24 */
-  double ct = fma(t2, pc, 1.0);
-  double C = or_angtab[j][0], S = or_angtab[j][1];
-  double cr = fma(C, ct, -(S * st));
-  double sr = fma(S, ct, C * st);
-  *z0 = rho * cr;
-  *z1 = rho * sr;
+/* standard normal from one 32-bit word (spec v5): z = -+ q(u), the sign from bit 31, u = v 2^-33
+   with v = 2 (w mod 2^31) + 1, and q the spec's piecewise-polynomial normal quantile on (0, 1/2):
+   for v = 2^E (1 + f), segment (E, j = floor(32 f)), t = 32 f - j in [0, 1), Horner in t of the
+   segment's six coefficients (or_tables.h, highest first) with fma.  Replaces Leva's ratio-of-uniforms
+   Stats.draw_gaussian (stats.ml:113-124): any exactly symmetric proposal keeps MH exact, and the
+   table is within ~3e-14 of the exact quantile. */
+double or_normal(uint32_t w) {
+  uint32_t v = 2u * (w & 0x7FFFFFFFu) + 1u;
+  int E = 31 - __builtin_clz(v);
+  double fv = ldexp((double)v, -E);                /* exact, in [1, 2) */
+  double s32 = (fv - 1.0) * 32.0;                  /* exact */
+  int j = (int)s32;
+  double t = s32 - (double)j;                      /* exact, in [0, 1) */
+  const double(*c)[2] = &or_nrmtab[3 * (E * 32 + j)];
+  double p = fma(c[0][0], t, c[0][1]);
+  p = fma(p, t, c[1][0]);
+  p = fma(p, t, c[1][1]);
+  p = fma(p, t, c[2][0]);
+  p = fma(p, t, c[2][1]);
+  return (w >> 31) ? -p : p;
 }
 
 /* log1p(r) for r in [0,1] and log-sum-exp with the portable exp/log (device-reproducible):
@@ -186,16 +184,13 @@ double or_plse(double a, double b) {
   return a + or_plog1p(or_exp(b - a));
 }
 
-/* dims 4c..4c+3 of a step take Philox call c: pair (w0,w1) -> z[4c], z[4c+1]; (w2,w3) -> +2,+3 */
+/* dims 4c..4c+3 of a step take Philox call c: word k -> z[4c + k] */
 static void normals_tagged(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t tag, uint32_t hi16,
                            int D, double* z) {
   for (int c = 0; 4 * c < D; ++c) {
     uint32_t w[4];
     rng4(seed, c0, c1, (uint32_t)c, tag, hi16, w);
-    double t[4];
-    or_normal_pair(w[0], w[1], &t[0], &t[1]);
-    or_normal_pair(w[2], w[3], &t[2], &t[3]);
-    for (int j = 0; j < 4 && 4 * c + j < D; ++j) z[4 * c + j] = t[j];
+    for (int j = 0; j < 4 && 4 * c + j < D; ++j) z[4 * c + j] = or_normal(w[j]);
   }
 }
 
@@ -1153,7 +1148,7 @@ int or_nested(const or_model* m, uint64_t seed, const or_nested_opts* o, double*
         rng4(seed, wid, (uint32_t)s, CALL_DE_SCALE, TAG_NEST_WALK, 0u, rw);
         double dsc;
         if (o->mode_hop != 0.0 && or_u53(rw[0], rw[1]) < o->mode_hop) dsc = 1.0;
-        else { double z0, z1; or_normal_pair(rw[2], rw[3], &z0, &z1); dsc = sigma_de * z0; }
+        else dsc = sigma_de * or_normal(rw[2]);
         for (int d = 0; d < D; ++d) y[d] = cur[d] + dsc * (lx[(int64_t)j * D + d] - lx[(int64_t)i * D + d]);
         double lly = lik_eval(&p, y);
         double ml = (lly >= thr) ? prior_eval(&p, y) : -INFINITY;

@@ -30,7 +30,7 @@ uint32_t or_randint(uint32_t w0, uint32_t w1, uint32_t n);
 double or_log(double x);
 double or_exp(double x);
 double or_sqrt(double x);
-void or_normal_pair(uint32_t a, uint32_t b, double* z0, double* z1);
+double or_normal(uint32_t w);
 double or_plog1p(double r);
 double or_plse(double a, double b);
 /* normals for the MH proposal of chain c at step t: z[0..D) */

@@ -66,7 +66,8 @@ def lib():
         L.or_u53.restype = C.c_double
         L.or_randint.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32]
         L.or_randint.restype = C.c_uint32
-        L.or_normal_pair.argtypes = [C.c_uint32, C.c_uint32, _dp, _dp]
+        L.or_normal.argtypes = [C.c_uint32]
+        L.or_normal.restype = C.c_double
         L.or_step_normals.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, C.c_int, _dp]
         L.or_log_sum_logs.argtypes = [C.c_double, C.c_double]
         L.or_log_sum_logs.restype = C.c_double
@@ -140,10 +141,9 @@ def philox(ctr, key):
     return list(o)
 
 
-def normal_pair(a, b):
-    z0, z1 = C.c_double(), C.c_double()
-    lib().or_normal_pair(a, b, C.byref(z0), C.byref(z1))
-    return z0.value, z1.value
+def normal(w):
+    """Spec-v5 standard normal of one 32-bit word (oracle.c or_normal)."""
+    return lib().or_normal(w)
 
 
 def step_normals(seed, chain, step, D, tag=1):

@@ -59,7 +59,7 @@ def test_merge_of_one_run_is_the_reference_estimate(oracle):
 
 def test_merged_replicas_estimate_unit_evidence(oracle):
     """nested_test.ml:23-39 on a merged run: 4 replicas of 250 live points = one run of 1000."""
-    runs = _runs(oracle, [21, 22, 23, 24], 250, nmcmc=100)
+    runs = _runs(oracle, [21, 22, 23, 24], 250, nmcmc=1000)   # the reference default
     got = _merge(runs, 250, 1)
     ev = math.exp(got[0])
     err = math.exp(oracle.lib().or_log_total_error_estimate(got[0], got[1], 1000))

@@ -3,9 +3,12 @@
 reference's statistical tests (test/mcmc_test.ml, test/nested_test.ml) re-expressed on the
 oracle.  The oracle is the parity checker of the GPU path, so it is pinned first."""
 import math
+import os
 
 import numpy as np
 import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 LIK_FLAT, LIK_DIAG, LIK_FULLCOV, LIK_SHELL, LIK_GDATA, LIK_CDATA = range(6)
 PRIOR_FLAT, PRIOR_BOX, PRIOR_OPEN = 0, 1, 2
@@ -43,36 +46,43 @@ def test_portable_math_accuracy(oracle):
         assert abs(L.or_sqrt(x) - math.sqrt(x)) <= 2 * math.ulp(math.sqrt(x))
 
 
-def test_normal_pair_accuracy_and_exact_symmetry(oracle):
-    """Spec v4 Box-Muller: within a few ulp of rho (cos, sin)(2 pi (b + 1/2) 2^-32), and exactly
-    antisymmetric under b -> b + 2^31 (the angle table's second half negates the first), which
-    makes the proposal exactly symmetric."""
+def test_normal_accuracy_and_exact_symmetry(oracle):
+    """Spec v5 normal: within 5e-14 of the exact quantile -sqrt(2) erfinv(1 - 2u) of
+    u = (2 (w mod 2^31) + 1) 2^-33 (sign from bit 31), across every octave of u including the
+    extreme words, and exactly antisymmetric under w -> w ^ 2^31, which makes the proposal
+    exactly symmetric."""
     mp = pytest.importorskip("mpmath")
     mp.mp.dps = 40
     rng = np.random.default_rng(3)
-    for a, b in rng.integers(0, 2 ** 32, size=(300, 2)):
-        a, b = int(a), int(b)
-        z0, z1 = oracle.normal_pair(a, b)
-        rho = mp.sqrt(-2 * mp.log((mp.mpf(a) + 0.5) / 2 ** 32))
-        th = 2 * mp.pi * (mp.mpf(b) + 0.5) / 2 ** 32
-        assert abs(mp.mpf(z0) - rho * mp.cos(th)) <= 8 * rho * 2.0 ** -53
-        assert abs(mp.mpf(z1) - rho * mp.sin(th)) <= 8 * rho * 2.0 ** -53
-        w0, w1 = oracle.normal_pair(a, (b + 2 ** 31) % 2 ** 32)
-        assert (w0, w1) == (-z0, -z1)
+    words = [0, 1, 2, 3, 0x7FFFFFFF, 0x7FFFFFFE, 0x40000000, 0x3FFFFFFF, 0x80000000, 0xFFFFFFFF]
+    words += [int(w) for w in rng.integers(0, 2 ** 32, size=300)]
+    # every octave E of v = 2u 2^32: v in [2^E, 2^(E+1))
+    for E in range(1, 32):
+        lo = 1 << (E - 1)
+        words += [int(w) for w in rng.integers(lo, 2 * lo, size=4)]
+    for w in words:
+        z = oracle.normal(w)
+        u = (2 * mp.mpf(w & 0x7FFFFFFF) + 1) / mp.mpf(2) ** 33
+        q = mp.sqrt(2) * mp.erfinv(2 * u - 1)
+        ref = -q if (w >> 31) else q
+        assert abs(mp.mpf(z) - ref) <= 5e-14, (w, z, ref)
+        assert oracle.normal(w ^ 0x80000000) == -z
 
 
 def test_normal_generator_moments(oracle):
     z = []
-    for i in range(100000):
+    for i in range(50000):
         w = oracle.philox([i, 7, 0, 0], [3, 4])
-        z.extend(oracle.normal_pair(w[0], w[1]))
+        z.extend(oracle.normal(int(v)) for v in w)
     z = np.array(z)
     n = len(z)
     assert abs(z.mean()) < 5 / math.sqrt(n)
     assert abs(z.var() - 1) < 5 * math.sqrt(2 / n)
     assert abs((z ** 4).mean() - 3) < 5 * math.sqrt(96 / n)
-    # symmetric: the angle grid is symmetric, so odd moments vanish in expectation
+    # symmetric: the sign bit is independent of |z|, so odd moments vanish in expectation
     assert abs((z ** 3).mean()) < 5 * math.sqrt(15 / n)
+    p3 = 2 * 0.0013498980316300946        # P(|z| > 3)
+    assert abs((np.abs(z) > 3).mean() - p3) < 5 * math.sqrt(p3 / n)
 
 
 # ---------------------------------------------------------------- Stats KATs (stats_test.ml)
@@ -348,3 +358,40 @@ def test_evidence_weights_blocked_fold_close_to_sequential(oracle):
     lev = -0.69314718055994530942 + lse(low, high)
     assert abs(le - lev) <= 1e-13 * abs(lev)
     assert abs(ld - (high + math.log1p(-math.exp(low - high)))) <= 1e-12 * abs(ld)
+
+
+def test_device_normal_formulation_matches_oracle(oracle):
+    """The kernels' pnormal (mcg_math.h) reaches the same spec by bit tricks: segment from the high
+    word of double(v), x = t/32 from the low fraction bits, Horner in x with the 32^k-scaled
+    table of mcg_tables.h.  Restated here in exact rational arithmetic (one rounding per fma) and
+    compared with the oracle's Horner in t, word for word, over every octave of v."""
+    import re
+    import struct
+    from fractions import Fraction as Fr
+    src = open(os.path.join(ROOT, "mcmc-ocaml_amd", "csrc", "mcg_tables.h")).read()
+    i = src.index("kNrmTab[")
+    body = src[i:src.index("};", i)]
+    tab = list(zip([float.fromhex(a) for a in re.findall(r"\{(\S+), ", body)],
+                   [float.fromhex(b) for b in re.findall(r", (\S+)\},", body)]))
+
+    def fma(a, b, c):
+        return float(Fr(a) * Fr(b) + Fr(c))
+
+    def dev(w):
+        v = ((w << 1) | 1) & 0xFFFFFFFF
+        bits = struct.unpack("<Q", struct.pack("<d", float(v)))[0]
+        hi, lo = bits >> 32, bits & 0xFFFFFFFF
+        seg = (hi >> 15) - (1023 << 5)
+        x = struct.unpack("<d", struct.pack("<Q", (((hi & 0x7FFF) | 0x3FF00000) << 32) | lo))[0] - 1.0
+        c = tab[3 * seg:3 * seg + 3]
+        p = fma(c[0][0], x, c[0][1])
+        for a in (c[1][0], c[1][1], c[2][0], c[2][1]):
+            p = fma(p, x, a)
+        return -p if w >> 31 else p
+
+    rng = np.random.default_rng(5)
+    words = [0, 1, 2, 3, 5, 7, 0x7FFFFFFF, 0x80000000, 0xFFFFFFFF]
+    words += [int(w) for w in rng.integers(0, 2 ** 32, size=2000)]
+    words += [int(w) for E in range(1, 32) for w in rng.integers(1 << (E - 1), 1 << E, size=8)]
+    for w in words:
+        assert dev(w) == oracle.normal(w), hex(w)
