@@ -282,6 +282,10 @@ struct AccumCfg {
   static constexpr int kLdsBytes = kLds ? 2 * Layout<D, P>::NL * 256 * 8 : 0;
 };
 
+#ifndef MCG_CONST_MODE
+#define MCG_CONST_MODE 1   // model constants of the fused step: 0 generic loads, 1 global, 2 LDS
+#endif
+
 #ifndef MCG_MH_MIN_WAVES
 #define MCG_MH_MIN_WAVES 1
 #endif
@@ -296,6 +300,18 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
   __shared__ double2 s_nt[kNrmTabN];
   for (int i = threadIdx.x; i < kLogTabN; i += blockDim.x) s_lt[i] = kLogTab[i];
   for (int i = threadIdx.x; i < kNrmTabN; i += blockDim.x) s_nt[i] = kNrmTab[i];
+#if MCG_CONST_MODE == 2
+  // model constants of the fused separable step staged in LDS: proposal scales [D], likelihood
+  // [2D + 1] (DIAG: mu/sigma, 1/sigma, C; SHELL: c, R, iw, C), prior box [2D + 1]
+  __shared__ double s_qp[kSeparable ? D : 1], s_ql[kSeparable ? 2 * D + 3 : 1], s_qr[kSeparable ? 2 * D + 1 : 1];
+  if constexpr (kSeparable) {
+    for (int i = threadIdx.x; i < D; i += blockDim.x) s_qp[i] = a.prop[i];
+    const int nl = LIK == MCG_LIK_DIAG_GAUSS ? 2 * D + 1 : LIK == MCG_LIK_GAUSS_SHELL ? D + 3 : 0;
+    for (int i = threadIdx.x; i < nl; i += blockDim.x) s_ql[i] = a.lik[i];
+    if (a.prior_kind != MCG_PRIOR_FLAT)
+      for (int i = threadIdx.x; i < 2 * D + 1; i += blockDim.x) s_qr[i] = a.pri[i];
+  }
+#endif
   __syncthreads();
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int sub = (int)(tid & (P - 1));
@@ -431,6 +447,17 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
     if constexpr (kSeparable) {
       // fused: per Philox call -> 4 normals -> 4 proposed coordinates -> their terms of the
       // canonical sum and of the box test.  Keeps only x, y and 8/P accumulators live.
+#if MCG_CONST_MODE == 2
+      const double* qlik = s_ql;
+      const double* qpri = s_qr;
+      const double* qprop = s_qp;
+#elif MCG_CONST_MODE == 1
+      typedef const __attribute__((address_space(1))) double gdouble;
+      gdouble* qlik = (gdouble*)a.lik;
+      gdouble* qpri = (gdouble*)a.pri;
+      gdouble* qprop = (gdouble*)a.prop;
+      asm volatile("" : "+s"(qlik), "+s"(qpri), "+s"(qprop));
+#endif
       double A[L::NA];
 #pragma unroll
       for (int j = 0; j < L::NA; ++j) A[j] = 0.0;
