@@ -68,6 +68,8 @@ struct MhArgs {
   int32_t prior_kind;
   int32_t flags;        // RUNF_*
   int32_t is_cauchy;
+  int32_t uni;          // isotropic Gaussian proposal and one box for every dim (fused step only)
+  double uni_s, uni_lo, uni_hi;
   // reversible jump (mcg_rj_kernel.h): model descriptors, tags, recorded tags, B-record counts
   const double* rj;
   uint8_t* tag;                 // [N]

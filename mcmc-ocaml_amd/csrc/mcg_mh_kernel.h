@@ -268,6 +268,14 @@ __device__ __forceinline__ double eval_prior(const double* y, int sub, const MhA
   return inb ? q[2 * D] : -__builtin_inf();
 }
 
+// the fused step (per Philox call: normals, coordinates, likelihood terms, box test) applies to
+// separable likelihoods with a Gaussian random-walk proposal
+template <int LIK, int PROP>
+constexpr bool separable() {
+  return (LIK == MCG_LIK_DIAG_GAUSS || LIK == MCG_LIK_GAUSS_SHELL || LIK == MCG_LIK_FLAT) &&
+         PROP == MCG_PROP_GAUSS;
+}
+
 #ifndef MCG_ACC_REG_MAX
 #define MCG_ACC_REG_MAX 8
 #endif
@@ -290,11 +298,11 @@ struct AccumCfg {
 #define MCG_MH_MIN_WAVES 1
 #endif
 
-template <int D, int P, int LIK, int PROP>
+template <int D, int P, int LIK, int PROP, bool UNI>
 __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs a) {
   using L = Layout<D, P>;
-  constexpr bool kSeparable = (LIK == MCG_LIK_DIAG_GAUSS || LIK == MCG_LIK_GAUSS_SHELL ||
-                               LIK == MCG_LIK_FLAT) && PROP == MCG_PROP_GAUSS;
+  constexpr bool kSeparable = separable<LIK, PROP>();
+  static_assert(kSeparable || !UNI, "UNI applies to the fused separable step");
   extern __shared__ double lds_acc[];
   __shared__ double2 s_lt[kLogTabN];                 // math tables staged in LDS (gathers)
   __shared__ double2 s_nt[kNrmTabN];
@@ -433,6 +441,19 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
   }
 
   double lu_own = 0.0;
+  // UNI (isotropic proposal scale, one box for every dim): the scale and the box are kernel
+  // arguments (SGPRs), so the lane's likelihood constants fit in registers for the whole launch
+  double rc_m[UNI ? L::NL : 1], rc_i[UNI ? L::NL : 1];
+  if constexpr (UNI) {
+#pragma unroll
+    for (int i = 0; i < L::NCL; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int d = L::valid(sub, i, k) ? L::dim(sub, i, k) : 0;
+        rc_m[4 * i + k] = LIK == MCG_LIK_FLAT ? 0.0 : a.lik[d];
+        rc_i[4 * i + k] = LIK == MCG_LIK_DIAG_GAUSS ? a.lik[D + d] : 0.0;
+      }
+  }
   for (int64_t t = 0; t < a.nsteps; ++t) {
     const uint64_t T = a.step_base + (uint64_t)t;
     const uint32_t tlo = (uint32_t)T, thi = (uint32_t)(T >> 32);
@@ -478,19 +499,20 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
         for (int k = 0; k < 4; ++k) {
           if (!L::valid(sub, i, k)) continue;
           const int d = 4 * cc + k;
-          const double yv = fma(qprop[d], z[k], x[4 * i + k]);
+          const double yv = fma(UNI ? a.uni_s : qprop[d], z[k], x[4 * i + k]);
           y[4 * i + k] = yv;
           if constexpr (LIK == MCG_LIK_DIAG_GAUSS) {
-            const double e = fma(yv, qlik[D + d], -qlik[d]);   // (y - mu)/sigma
+            const double e = UNI ? fma(yv, rc_i[4 * i + k], -rc_m[4 * i + k])
+                                 : fma(yv, qlik[D + d], -qlik[d]);   // (y - mu)/sigma
             A[i % L::NA] = fma(e, e, A[i % L::NA]);
           } else if constexpr (LIK == MCG_LIK_GAUSS_SHELL) {
-            const double e = yv - qlik[d];
+            const double e = yv - (UNI ? rc_m[4 * i + k] : qlik[d]);
             A[i % L::NA] = fma(e, e, A[i % L::NA]);
           }
           {
             // branch-free closed-box test: the host stores an OPEN box as its closed equivalent
             // [nextafter(lo, +inf), nextafter(hi, -inf)] and pads FLAT priors with (-inf, inf)
-            const double lo = qpri[d], hi = qpri[D + d];
+            const double lo = UNI ? a.uni_lo : qpri[d], hi = UNI ? a.uni_hi : qpri[D + d];
             inb &= (int)(yv >= lo) & (int)(yv <= hi);
           }
         }
@@ -741,7 +763,13 @@ hipError_t launch_mh(const MhArgs& a, int64_t nthreads, hipStream_t s) {
   const int block = 256;
   const int64_t grid = (nthreads + block - 1) / block;
   constexpr int lds = AccumCfg<D, P>::kLdsBytes;
-  hipLaunchKernelGGL((mh_kernel<D, P, LIK, PROP>), dim3((unsigned)grid), dim3(block), lds, s, a);
+  if constexpr (separable<LIK, PROP>()) {
+    if (a.uni) {
+      hipLaunchKernelGGL((mh_kernel<D, P, LIK, PROP, true>), dim3((unsigned)grid), dim3(block), lds, s, a);
+      return hipGetLastError();
+    }
+  }
+  hipLaunchKernelGGL((mh_kernel<D, P, LIK, PROP, false>), dim3((unsigned)grid), dim3(block), lds, s, a);
   return hipGetLastError();
 }
 

@@ -502,6 +502,22 @@ MhArgs base_args(mcg_ctx* ctx) {
   a.kd_pt_leaf = (const int32_t*)ctx->kd.d_pt_leaf.p;
   a.kd_M = ctx->kd.M;
   if (ctx->rj_active) rj_args(ctx, a);
+  // one proposal scale and one box for every dim (bitwise): the fused step takes them as scalars
+  const int D = ctx->D;
+  const auto& sp = ctx->prop_host;
+  const auto& bx = ctx->pri_host;
+  if (ctx->prop_kind == MCG_PROP_GAUSS && D >= 1 && (int)sp.size() >= D && (int)bx.size() >= 2 * D) {
+    bool same = true;
+    for (int d = 1; d < D && same; ++d)
+      same = !std::memcmp(&sp[d], &sp[0], 8) && !std::memcmp(&bx[d], &bx[0], 8) &&
+             !std::memcmp(&bx[D + d], &bx[D], 8);
+    if (same) {
+      a.uni = 1;
+      a.uni_s = sp[0];
+      a.uni_lo = bx[0];
+      a.uni_hi = bx[D];
+    }
+  }
   return a;
 }
 
