@@ -9,6 +9,7 @@
 // points into evidence_error_and_weights (nested.ml:81-120); the live points are folded in once
 // the run has stopped.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -27,19 +28,24 @@ namespace {
 
 struct KeyBuf {
   DevBuf ll, tie, slot;
+  DevBuf samp_ll, samp_tie;   // every kKeySample-th key (indices 63, 127, ...): merge search samples
   hipError_t ensure(int64_t n) {
     hipError_t e;
     if ((e = ll.ensure(n * 8)) != hipSuccess) return e;
     if ((e = tie.ensure(n * 8)) != hipSuccess) return e;
+    if ((e = samp_ll.ensure((n / kKeySample + 1) * 8)) != hipSuccess) return e;
+    if ((e = samp_tie.ensure((n / kKeySample + 1) * 8)) != hipSuccess) return e;
     return slot.ensure(n * 4);
   }
   double* l() { return (double*)ll.p; }
   long long* t() { return (long long*)tie.p; }
   int* s() { return (int*)slot.p; }
+  double* sl() { return (double*)samp_ll.p; }
+  long long* st() { return (long long*)samp_tie.p; }
 };
 
 struct NestedBufs {
-  DevBuf x, ll, lp, nx, nll, nlp, tv, prefix, qadd, st, dead_x, dead_ll, dead_lp, runl, runj;
+  DevBuf x, ll, lp, nx, nll, nlp, tv, prefix, qadd, st, dead_x, dead_ll, dead_lp, rank, sync, trace;
   KeyBuf keys[2], newk, newk_tmp;
   int64_t dead_cap = 0;
   // pinned staging of two in-flight batches' dead (ll, lp) and their completion events
@@ -47,7 +53,16 @@ struct NestedBufs {
   int64_t h_cap = 0;
   NestDevState* h_st = nullptr;
   hipEvent_t done[2] = {nullptr, nullptr};
+  // pinned chunk ring of the large device -> host copy in mcg_nested_get (copy_d2h_large)
+  static constexpr int kRing = 4;
+  static constexpr size_t kRingChunk = (size_t)16 << 20;
+  void* h_ring[kRing] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev_ring[kRing] = {nullptr, nullptr, nullptr, nullptr};
   ~NestedBufs() {
+    for (auto h : h_ring)
+      if (h) (void)hipHostFree(h);
+    for (auto e : ev_ring)
+      if (e) (void)hipEventDestroy(e);
     for (auto h : h_stage)
       if (h) (void)hipHostFree(h);
     if (h_st) (void)hipHostFree(h_st);
@@ -234,8 +249,9 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   HC(B.nlp.ensure(k * 8), "alloc new");
   HC(B.newk.ensure(k), "alloc new keys");
   HC(B.newk_tmp.ensure(k), "alloc new keys");
-  HC(B.runl.ensure(((k + 255) / 256) * 256 * 8), "alloc sort runs");
-  HC(B.runj.ensure(((k + 255) / 256) * 256 * 4), "alloc sort runs");
+  HC(B.rank.ensure(k * 4), "alloc new-key ranks");
+  HC(B.sync.ensure(2 * kSyncUse * 4), "alloc hand-off counters");
+  HC(hipMemsetAsync(B.sync.p, 0, 2 * kSyncUse * 4, s), "clear hand-off counters");
   HC(B.tv.ensure(p2 * 8), "alloc tv");
   HC(B.prefix.ensure((k + 1) * 8), "alloc prefix");
   HC(B.qadd.ensure(k * 8), "alloc qadd");
@@ -263,6 +279,8 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   a.newk_ll = B.newk.l();
   a.newk_tie = B.newk.t();
   a.newk_slot = B.newk.s();
+  a.rank = (int*)B.rank.p;
+  a.sync = (uint32_t*)B.sync.p;
   a.tv = (double*)B.tv.p;
   a.prefix = (const double*)B.prefix.p;
   a.qadd = (const double*)B.qadd.p;
@@ -289,6 +307,8 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   HC(launch_sort_keys(B.keys[0].l(), B.keys[0].t(), B.keys[0].s(), B.keys[1].l(), B.keys[1].t(),
                       B.keys[1].s(), n, &in_tmp, s, nullptr), "sort live keys");
   const int base = in_tmp ? 1 : 0;                   // generation g reads keys[(base + g) % 2]
+  HC(launch_key_sample(B.keys[base].l(), B.keys[base].t(), n, B.keys[base].sl(), B.keys[base].st(), s),
+     "sample live keys");
 
   // Batches of generations, pipelined: while the GPU runs batch b + 1, the host appends batch b's
   // dead ll / lp (copied into pinned staging behind b's kernels) and folds them into the
@@ -312,6 +332,15 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   if (!B.h_st) HC(hipHostMalloc((void**)&B.h_st, 2 * sizeof(NestDevState), 0), "alloc pinned state");
   NestDevState* hst = B.h_st;
   int64_t gen = 0, reported = 0, batch = 4;
+#ifdef MCG_NEST_TRACE
+  // phase stamps of one generation (MCG_NEST_TRACE=<generation>), printed at the end
+  const char* trace_env = std::getenv("MCG_NEST_TRACE");
+  const int64_t trace_gen = trace_env ? std::atoll(trace_env) : -1;
+  if (trace_gen >= 0) {
+    HC(B.trace.ensure(4 * 1024 * 8 * 8), "alloc trace");
+    HC(hipMemsetAsync(B.trace.p, 0, 4 * 1024 * 8 * 8, s), "clear trace");
+  }
+#endif
   // enqueue generations [gen, gen + G) and the copies of their state / dead ll, lp into slot q
   auto launch_batch = [&](int64_t G, int q) -> int {
     const int64_t need = (gen + G) * k;
@@ -342,18 +371,22 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
       a.key_ll = cur.l();
       a.key_tie = cur.t();
       a.key_slot = cur.s();
+      a.key_samp_ll = cur.sl();
+      a.key_samp_tie = cur.st();
+      a.out_samp_ll = nxt.sl();
+      a.out_samp_tie = nxt.st();
       a.mrep = g * k;
+#ifdef MCG_NEST_TRACE
+      a.trace = (g == trace_gen) ? (unsigned long long*)B.trace.p : nullptr;
+#endif
       hipEvent_t e0 = nullptr, e1 = nullptr;
       if (ctx->timing) timing_begin(ctx, &e0, &e1);
       HC(walk(a, s), "nested walk");
       if (ctx->timing) timing_end(ctx, e0, e1, 1);
       HC(launch_retire(a, D, s), "nested retire");
-      HC(launch_estimate(a, s), "nested estimate");
       bool nk_tmp = false;
       if (k <= 4096) {
-        // run-sorted (ll, j) scratch of ceil(k/256)*256 entries
-        HC(launch_sort_new_small(a, (double*)B.runl.p, (int*)B.runj.p, B.newk_tmp.l(), B.newk_tmp.t(),
-                                 B.newk_tmp.s(), s), "sort new keys");
+        HC(launch_sort_new_small(a, B.newk_tmp.l(), B.newk_tmp.t(), B.newk_tmp.s(), s), "sort new keys");
         nk_tmp = true;
       } else {
         HC(launch_sort_keys(B.newk.l(), B.newk.t(), B.newk.s(), B.newk_tmp.l(), B.newk_tmp.t(),
@@ -432,6 +465,28 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
     q ^= 1;
   }
   const auto t_gen = now();
+#ifdef MCG_NEST_TRACE
+  if (trace_gen >= 0 && trace_gen < st.gen_done) {
+    std::vector<unsigned long long> tr(4 * 1024 * 8);
+    HC(hipMemcpy(tr.data(), B.trace.p, tr.size() * 8, hipMemcpyDeviceToHost), "copy trace");
+    unsigned long long t0 = ~0ull;
+    for (int b = 0; b < 1024; ++b)
+      if (tr[(size_t)b * 8]) t0 = std::min(t0, tr[(size_t)b * 8]);
+    const char* names[4] = {"walk", "retire", "rank_count", "merge_new"};
+    for (int kid = 0; kid < 4; ++kid)
+      for (int sl = 0; sl < 8; ++sl) {
+        std::vector<double> v;
+        for (int b = 0; b < 1024; ++b) {
+          const unsigned long long x = tr[((size_t)kid * 1024 + b) * 8 + sl];
+          if (x) v.push_back((double)(x - t0) * 0.01);          // 100 MHz -> us
+        }
+        if (v.empty()) continue;
+        std::sort(v.begin(), v.end());
+        std::fprintf(stderr, "trace gen %lld %-10s slot %d: n %4zu  min %7.2f  med %7.2f  max %7.2f us\n",
+                     (long long)trace_gen, names[kid], sl, v.size(), v.front(), v[v.size() / 2], v.back());
+      }
+  }
+#endif
   if (prof)
     std::fprintf(stderr, "mcg_nested: host launch %.1f ms, wait %.1f ms, fold join %.1f ms\n", t_launch, t_wait, t_fold);
   // final: dead points in retirement order, then the live set ascending (nested.ml:143)
@@ -476,6 +531,60 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   return MCG_OK;
 }
 
+// Device -> pageable host copy of a large buffer (the dead rows: 457 MB at C3).  A plain pageable
+// hipMemcpy stages through the driver with one host thread; here the DMA fills a ring of pinned
+// chunks while host threads copy finished chunks into the destination in parallel.
+static hipError_t copy_d2h_large(NestedBufs& B, void* dst, const void* src, size_t bytes, hipStream_t s) {
+  constexpr int R = NestedBufs::kRing;
+  constexpr size_t CH = NestedBufs::kRingChunk;
+  if (bytes <= CH) return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
+  for (int r = 0; r < R; ++r) {
+    hipError_t e;
+    if (!B.h_ring[r] && (e = hipHostMalloc(&B.h_ring[r], CH, 0)) != hipSuccess) return e;
+    if (!B.ev_ring[r] && (e = hipEventCreateWithFlags(&B.ev_ring[r], hipEventDisableTiming)) != hipSuccess) return e;
+  }
+  const size_t nch = (bytes + CH - 1) / CH;
+  auto len = [&](size_t c) { return std::min(CH, bytes - c * CH); };
+  auto enqueue = [&](size_t c) -> hipError_t {
+    const int r = (int)(c % R);
+    hipError_t e = hipMemcpyAsync(B.h_ring[r], (const char*)src + c * CH, len(c), hipMemcpyDeviceToHost, s);
+    return e == hipSuccess ? hipEventRecord(B.ev_ring[r], s) : e;
+  };
+  hipError_t err = hipSuccess;
+  for (size_t c = 0; c < nch && c < (size_t)R && err == hipSuccess; ++c) err = enqueue(c);
+  if (err != hipSuccess) return err;
+  const int T = (int)std::max<unsigned>(1, std::min<unsigned>(8, std::thread::hardware_concurrency()));
+  std::atomic<int64_t> ready{-1};                    // last chunk whose DMA has completed
+  std::atomic<int64_t> copied{0};                    // worker slices copied
+  std::atomic<bool> abort{false};
+  auto slice = [&](size_t c, int w) {
+    const size_t n = len(c), a = n * (size_t)w / T, b = n * (size_t)(w + 1) / T;
+    std::memcpy((char*)dst + c * CH + a, (const char*)B.h_ring[c % R] + a, b - a);
+  };
+  std::vector<std::thread> pool;
+  for (int w = 1; w < T; ++w)
+    pool.emplace_back([&, w] {
+      for (size_t c = 0; c < nch; ++c) {
+        while (ready.load(std::memory_order_acquire) < (int64_t)c) {
+          if (abort.load(std::memory_order_relaxed)) return;
+          std::this_thread::yield();
+        }
+        slice(c, w);
+        copied.fetch_add(1, std::memory_order_release);
+      }
+    });
+  for (size_t c = 0; c < nch; ++c) {
+    if ((err = hipEventSynchronize(B.ev_ring[c % R])) != hipSuccess) break;
+    ready.store((int64_t)c, std::memory_order_release);
+    slice(c, 0);
+    while (copied.load(std::memory_order_acquire) < (int64_t)((c + 1) * (size_t)(T - 1))) std::this_thread::yield();
+    if (c + R < nch && (err = enqueue(c + R)) != hipSuccess) break;
+  }
+  if (err != hipSuccess) abort.store(true);
+  for (auto& t : pool) t.join();
+  return err;
+}
+
 int mcg_nested_get(mcg_ctx* ctx, double* pts, double* ll, double* lp, double* log_wts) {
   if (!ctx) return MCG_EINVAL;
   const NestedState& R = ctx->nested;
@@ -484,16 +593,22 @@ int mcg_nested_get(mcg_ctx* ctx, double* pts, double* ll, double* lp, double* lo
   if (pts) {
     const int64_t D = (int64_t)(R.pts.size() / (size_t)R.nlive);
     if (R.n_dead > 0) {
-      int rc = hip_check(ctx, hipMemcpy(pts, ctx->nested_bufs->b.dead_x.p, (size_t)(R.n_dead * D) * 8,
-                                        hipMemcpyDeviceToHost), "copy dead points");
+      NestedBufs& B = ctx->nested_bufs->b;
+      int rc = hip_check(ctx, copy_d2h_large(B, pts, B.dead_x.p, (size_t)(R.n_dead * D) * 8, ctx->stream),
+                         "copy dead points");
       if (rc) return rc;
     }
     std::copy(R.pts.begin(), R.pts.end(), pts + R.n_dead * D);
   }
   const auto t1 = std::chrono::steady_clock::now();
-  if (ll) std::copy(R.ll.begin(), R.ll.end(), ll);
-  if (lp) std::copy(R.lp.begin(), R.lp.end(), lp);
-  if (log_wts) std::copy(R.wts.begin(), R.wts.end(), log_wts);
+  {
+    // the three host arrays in parallel (first touch of the caller's pages dominates)
+    std::thread tl([&] { if (ll) std::copy(R.ll.begin(), R.ll.end(), ll); });
+    std::thread tp([&] { if (lp) std::copy(R.lp.begin(), R.lp.end(), lp); });
+    if (log_wts) std::copy(R.wts.begin(), R.wts.end(), log_wts);
+    tl.join();
+    tp.join();
+  }
   if (std::getenv("MCG_NESTED_PROFILE"))
     std::fprintf(stderr, "mcg_nested_get: points %.1f ms, ll/lp/wts %.1f ms\n",
                  std::chrono::duration<double, std::milli>(t1 - t0).count(),

@@ -25,6 +25,12 @@ struct NestDevState {
   long long gen_done;
 };
 
+// last-workgroup hand-off counters (mcg_nested_kernels.hip, last_block_done): per use a top counter
+// and 16 group counters, each on a 128-B line of its own; every counter is reset by the workgroup
+// that completes it
+constexpr int kKeySample = 64;   // spacing of the sorted-key sample kept beside the keys
+constexpr int kSyncGroups = 16, kSyncStride = 32, kSyncUse = (kSyncGroups + 1) * kSyncStride;
+
 struct NestArgs {
   MhArgs m;                 // likelihood / prior constants (m.lik, m.pri, m.prior_kind, ...)
   double* x;                // live rows [n][D]
@@ -33,6 +39,10 @@ struct NestArgs {
   const double* key_ll;     // current sorted keys
   const long long* key_tie;
   const int* key_slot;
+  const double* key_samp_ll;    // every kKeySample-th current key (written by the previous merge)
+  const long long* key_samp_tie;
+  double* out_samp_ll;          // the same sample of the merged keys, for the next generation
+  long long* out_samp_tie;
   double* nx;               // new points [k][D]
   double* nll;
   double* nlp;
@@ -42,6 +52,9 @@ struct NestArgs {
   double* newk_ll;          // unsorted keys of the new points
   long long* newk_tie;
   int* newk_slot;
+  int* rank;                // [k] rank of new key j among the generation's new keys (k <= 4096)
+  uint32_t* sync;           // [2][kSyncUse] hand-off counters: retire -> estimate, rank count -> scatter
+  unsigned long long* trace;  // MCG_NEST_TRACE builds: per-workgroup phase stamps of one generation
   double* tv;               // ll + log dv of this generation's dead points (padded pow2)
   const double* prefix;     // [k+1] sum_{j'<j} log1p(-1/(n-j'))
   const double* qadd;       // [k] 1/(n-j) (nested.ml:140 quirk) or log(1/(n-j))
@@ -51,6 +64,18 @@ struct NestArgs {
   uint32_t k0, k1;
   uint64_t seed_unused;
 };
+
+// phase stamps (s_memrealtime, 100 MHz) of wave 0 of each workgroup, one generation, in
+// MCG_NEST_TRACE builds only: trace[(kernel * 1024 + block) * 8 + slot]
+#ifdef MCG_NEST_TRACE
+#define NT_STAMP(kid, slot)                                                                       \
+  do {                                                                                            \
+    if (a.trace && threadIdx.x == 0 && blockIdx.x < 1024)                                         \
+      a.trace[((size_t)(kid) * 1024 + blockIdx.x) * 8 + (slot)] = wall_clock64();                 \
+  } while (0)
+#else
+#define NT_STAMP(kid, slot) do {} while (0)
+#endif
 
 #ifndef MCG_NEST_PREFETCH
 #define MCG_NEST_PREFETCH 4
@@ -154,6 +179,7 @@ template <int D, int LIK, int P>
 __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   using Lay = Layout<D, P>;
   constexpr int NL = Lay::NL;
+  NT_STAMP(0, 0);
   __shared__ double2 s_lt[kLogTabN];                 // math tables staged in LDS (gathers)
   for (int i = threadIdx.x; i < kLogTabN; i += blockDim.x) s_lt[i] = kLogTab[i];
   __syncthreads();
@@ -363,11 +389,14 @@ hipError_t launch_sort_keys(double* ll, long long* tie, int* slot, double* tll, 
 hipError_t launch_merge_new(const NestArgs& a, double* out_ll, long long* out_tie, int* out_slot,
                             const double* new_ll, const long long* new_tie, const int* new_slot,
                             hipStream_t st);
+// retire the k lowest; the last workgroup also folds the generation into the running estimate
 hipError_t launch_retire(const NestArgs& a, int D, hipStream_t st);
-// k <= 4096: run-sorted (ll, j) scratch rl[ceil(k/256)*256], rj[...] then a rank merge into o*
-hipError_t launch_sort_new_small(const NestArgs& a, double* rl, int* rj, double* oll, long long* otie,
-                                 int* oslot, hipStream_t st);
-hipError_t launch_estimate(const NestArgs& a, hipStream_t st);
+// every kKeySample-th of n sorted keys (indices kKeySample-1, 2 kKeySample-1, ...) into s*
+hipError_t launch_key_sample(const double* ll, const long long* tie, int64_t n, double* sll,
+                             long long* stie, hipStream_t st);
+// k <= 4096: new keys sorted into o* by counting ranks (a.rank zeroed by the retire kernel)
+hipError_t launch_sort_new_small(const NestArgs& a, double* oll, long long* otie, int* oslot,
+                                 hipStream_t st);
 
 typedef hipError_t (*nest_walk_fn)(const NestArgs&, hipStream_t);
 typedef hipError_t (*nest_init_fn)(const NestArgs&, double*, long long*, int*, hipStream_t);

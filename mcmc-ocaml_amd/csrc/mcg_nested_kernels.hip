@@ -9,6 +9,7 @@
 
 namespace mcg {
 
+
 __device__ __forceinline__ bool key_less(double la, long long ta, double lb, long long tb) {
   return la < lb || (la == lb && ta < tb);
 }
@@ -112,174 +113,283 @@ hipError_t launch_sort_keys(double* ll, long long* tie, int* slot, double* tll, 
 }
 
 // Sort this generation's k <= 4096 new keys.  The new keys' ties are -(mrep + j + 1), decreasing
-// in j, so the key order is (ll ascending, j descending) and only (ll, j) move; tie and slot are
-// rebuilt from j at the end.  One workgroup would be bound by its CU's LDS unit (every exchange
-// of a bitonic network goes through it), so the sort is spread over CUs:
-//   1. sort_runs_kernel: ceil(k/256) single-wave workgroups each sort a run of 256 keys, lane l
-//      holding positions 4l .. 4l+3: strides 1, 2 inside the lane, strides 4 .. 128 by
-//      shuffles with lane l ^ (stride/4) -- no LDS storage, no barriers;
-//   2. rank_merge_kernel: each key's final position = its index in its run + the number of keys
-//      of every other run that precede it (binary searches; ties between runs broken by run
-//      order, which only pads can need -- real keys are unique).
+// in j, so the key order is (ll ascending, j descending) and only (ll, j) decide it.  The keys
+// are unique, so key j's position is its rank: the number of new keys below it.  The ranks are
+// counted, not searched: block (A, B) of a (k/256) x (k/128) grid compares each key of run A with
+// the 128 keys of sub-run B (LDS broadcast reads) and adds its count to rank[j] (integer atomics: the sum is
+// order-independent and exact).  The last block to finish scatters every key to its rank.  One
+// launch of 128 compares per lane replaces a run sort plus a rank merge, which were bound
+// by their serial shuffle / search latencies (12 + 20 us per generation at k = 4096).
 constexpr int kSmallSort = 4096;
 constexpr int kRun = 256;
 
-__device__ __forceinline__ bool nk_less(double la, int ja, double lb, int jb) {
-  return la < lb || (la == lb && ja > jb);
-}
-
-__global__ void __launch_bounds__(64) sort_runs_kernel(const NestArgs a, double* rl, int* rj) {
-  if (a.st->stopped) return;
-  const int k = (int)a.k;
-  const int t = threadIdx.x;
-  const int base = blockIdx.x * kRun;
-  double kl[4];
-  int kj[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int p = base + 4 * t + e;
-    kl[e] = p < k ? a.newk_ll[p] : __builtin_inf();
-    kj[e] = p < k ? p : -1;
-  }
-#pragma unroll
-  for (int size = 2; size <= kRun; size <<= 1) {
-#pragma unroll
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      if (stride <= 2) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if (e & stride) continue;
-          const int f = e | stride;
-          const bool asc = ((4 * t + e) & size) == 0;
-          const bool swap = asc ? nk_less(kl[f], kj[f], kl[e], kj[e]) : nk_less(kl[e], kj[e], kl[f], kj[f]);
-          if (swap) {
-            const double tl = kl[e]; kl[e] = kl[f]; kl[f] = tl;
-            const int tj = kj[e]; kj[e] = kj[f]; kj[f] = tj;
-          }
-        }
-      } else {
-        const int m = stride >> 2;                       // partner lane t ^ m
-        const bool keep_min = ((t & m) == 0) == (((4 * t) & size) == 0);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const double ol = __shfl_xor(kl[e], m, 64);
-          const int oj = __shfl_xor(kj[e], m, 64);
-          if (nk_less(ol, oj, kl[e], kj[e]) == keep_min) {
-            kl[e] = ol;
-            kj[e] = oj;
-          }
-        }
-      }
+// Last-workgroup hand-off (MI355X_MICROARCH.md, hand-offs with sc1 loads, first row): the
+// handed-off bytes are stored sc1 (or are agent-scope atomics) and loaded sc1 (ld1 / st1 below),
+// so no producer needs an L2 write-back (release); every wave waits for its stores, a workgroup
+// barrier, then one lane counts.  The count is two-level (16 group counters, then a top counter
+// added to by the workgroup completing its group): one counter taking every workgroup's add
+// serialises them (measured: 6 us of spread over 512 workgroups).  The workgroup completing the
+// top counter acquires once and runs the consumer part.  No workgroup waits on another.
+__device__ __forceinline__ bool last_block_done(uint32_t* sync) {
+  __shared__ int s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t nb = gridDim.x, g = blockIdx.x % kSyncGroups;
+    const uint32_t gsize = (nb - g + kSyncGroups - 1) / kSyncGroups;
+    const uint32_t ngroups = nb < (uint32_t)kSyncGroups ? nb : (uint32_t)kSyncGroups;
+    uint32_t* gc = sync + (1 + g) * kSyncStride;
+    int last = 0;
+    if (__hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
+      __hip_atomic_store(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ngroups - 1;
     }
-  }
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    rl[base + 4 * t + e] = kl[e];
-    rj[base + 4 * t + e] = kj[e];
-  }
-}
-
-// All runs staged in LDS (<= 48 KiB), then every run's binary search advances in lockstep
-// (one LDS read per run per round, eight rounds), so the reads of the other runs overlap.
-__global__ void __launch_bounds__(256) rank_merge_kernel(const NestArgs a, const double* rl, const int* rj,
-                                                         int nruns, double* oll, long long* otie, int* oslot) {
-  if (a.st->stopped) return;
-  __shared__ double sl[kSmallSort];
-  __shared__ int sj[kSmallSort];
-  const int n = nruns * kRun;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    sl[i] = rl[i];
-    sj[i] = rj[i];
+    if (last) {
+      // the consumer's one agent acquire (drops stale L1 / L2 copies of the handed-off lines)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __hip_atomic_store(sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_last = last;
   }
   __syncthreads();
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= n) return;
-  const int r = g / kRun;
-  const double l = sl[g];
-  const int j = sj[g];
-  if (j < 0) return;                                 // padding
-  constexpr int kMaxRuns = kSmallSort / kRun;
-  int lo[kMaxRuns];
-#pragma unroll
-  for (int q = 0; q < kMaxRuns; ++q) lo[q] = 0;
-  // lo[q] = number of entries of run q before the key: strictly less for q > r, less or equal
-  // (an equal key can only be padding) for q < r
-#pragma unroll
-  for (int w = kRun >> 1; w >= 1; w >>= 1) {
-#pragma unroll
-    for (int q = 0; q < kMaxRuns; ++q) {
-      if (q >= nruns || q == r) continue;
-      const int m = q * kRun + lo[q] + w - 1;
-      const double ml = sl[m];
-      const int mj = sj[m];
-      const bool before = nk_less(ml, mj, l, j) || (q < r && ml == l && mj == j);
-      if (before) lo[q] += w;
-    }
-  }
-  int pos = g - r * kRun;
-#pragma unroll
-  for (int q = 0; q < kMaxRuns; ++q) {
-    if (q >= nruns || q == r) continue;
-    // the last probe of the halving search: the entry at lo[q] itself
-    const int m = q * kRun + lo[q];
-    if (lo[q] < kRun) {
-      const double ml = sl[m];
-      const int mj = sj[m];
-      if (nk_less(ml, mj, l, j) || (q < r && ml == l && mj == j)) lo[q] += 1;
-    }
-    pos += lo[q];
-  }
-  oll[pos] = l;
-  otie[pos] = -(long long)(a.mrep + j + 1);
-  oslot[pos] = a.newk_slot[j];
+  return s_last != 0;
 }
 
-hipError_t launch_sort_new_small(const NestArgs& a, double* rl, int* rj, double* oll, long long* otie,
-                                 int* oslot, hipStream_t s) {
-  if (a.k > kSmallSort) return hipErrorInvalidValue;
-  const int nruns = (int)((a.k + kRun - 1) / kRun);
-  hipLaunchKernelGGL(sort_runs_kernel, dim3(nruns), dim3(64), 0, s, a, rl, rj);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(rank_merge_kernel, dim3((nruns * kRun + 255) / 256), dim3(256), 0, s, a, rl, rj, nruns,
+template <typename T>
+__device__ __forceinline__ T ld1(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void st1(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr int kSub = 128;                            // keys of the compared-against sub-run
+
+__global__ void __launch_bounds__(256) rank_count_kernel(const NestArgs a, int nruns, double* oll,
+                                                         long long* otie, int* oslot) {
+  NT_STAMP(2, 0);
+  if (a.st->stopped) return;                         // grid-uniform: set by an earlier launch
+  __shared__ double sl[kSub];
+  __shared__ double s_ll[kSmallSort];                // last block: keys placed at their ranks
+  __shared__ short s_j[kSmallSort];
+  const int k = (int)a.k;
+  const int A = (int)(blockIdx.x % nruns), B = (int)(blockIdx.x / nruns);
+  const int t = threadIdx.x;
+  const int b0 = B * kSub;
+  const int nb = min(kSub, k - b0);
+  if (t < nb) sl[t] = a.newk_ll[b0 + t];
+  __syncthreads();
+  NT_STAMP(2, 1);
+  const int p = A * kRun + t;
+  if (p < k) {
+    const double l = a.newk_ll[p];
+    int cnt = 0;
+    if (nb == kSub) {
+#pragma unroll 16
+      for (int q = 0; q < kSub; ++q) {
+        const double o = sl[q];
+        cnt += (int)((o < l) | ((o == l) & (b0 + q > p)));   // nk order: ll asc, j desc
+      }
+    } else {
+      for (int q = 0; q < nb; ++q) {
+        const double o = sl[q];
+        cnt += (int)((o < l) | ((o == l) & (b0 + q > p)));
+      }
+    }
+    NT_STAMP(2, 2);
+    if (cnt) atomicAdd(&a.rank[p], cnt);
+  }
+  const bool last = last_block_done(a.sync + kSyncUse);
+  NT_STAMP(2, 3);
+  if (!last) return;
+  // the last block places every key at its rank in LDS (a random scatter from one CU is bound by
+  // its store rate), then writes the sorted keys out coalesced
+  constexpr int kPer = kSmallSort / kRun;
+  int rr[kPer];
+  double rl[kPer];
+#pragma unroll
+  for (int e = 0; e < kPer; ++e) {
+    const int q = min(e * kRun + t, k - 1);
+    rr[e] = ld1(a.rank + q);
+    rl[e] = a.newk_ll[q];
+  }
+#pragma unroll
+  for (int e = 0; e < kPer; ++e) {
+    const int q = e * kRun + t;
+    if (q < k) {
+      s_ll[rr[e]] = rl[e];
+      s_j[rr[e]] = (short)q;
+    }
+  }
+  __syncthreads();
+  NT_STAMP(2, 4);
+  int js[kPer], sl_[kPer];
+#pragma unroll
+  for (int e = 0; e < kPer; ++e) {
+    const int r = min(e * kRun + t, k - 1);
+    js[e] = s_j[r];
+    sl_[e] = a.newk_slot[js[e]];
+  }
+#pragma unroll
+  for (int e = 0; e < kPer; ++e) {
+    const int r = e * kRun + t;
+    if (r < k) {
+      oll[r] = s_ll[r];
+      otie[r] = -(long long)(a.mrep + js[e] + 1);
+      oslot[r] = sl_[e];
+    }
+  }
+  NT_STAMP(2, 5);
+}
+
+hipError_t launch_sort_new_small(const NestArgs& a, double* oll, long long* otie, int* oslot,
+                                 hipStream_t s) {
+  if (a.k > kSmallSort || a.k < 1) return hipErrorInvalidValue;
+  const int nruns = (int)((a.k + kRun - 1) / kRun), nsub = (int)((a.k + kSub - 1) / kSub);
+  hipLaunchKernelGGL(rank_count_kernel, dim3((unsigned)(nruns * nsub)), dim3(kRun), 0, s, a, nruns,
                      oll, otie, oslot);
   return hipGetLastError();
 }
 
 __device__ __forceinline__ void stop_test(const NestArgs& a, double max_ll);
 
+// Search samples of a sorted key array staged in LDS: every S-th key (indices S-1, 2S-1, ...), at
+// most `cap` of them; S is the smallest power of two >= 16 that keeps the count within cap.
+struct KeySample {
+  int64_t S;
+  int n;
+};
+__device__ __forceinline__ KeySample key_sample(int64_t len, int cap) {
+  int64_t S = 16;
+  while (len / S > cap) S <<= 1;
+  return KeySample{S, (int)(len / S)};
+}
+
+// count of the sorted keys [0, len) strictly below (kl, kt): the first levels in the LDS sample,
+// the last log2 S in global memory
+__device__ __forceinline__ int64_t count_less_2l(const double* ll, const long long* tie, int64_t len,
+                                                 KeySample ks, const double* sll, const long long* stie,
+                                                 double kl, long long kt) {
+  int a = 0, b = ks.n;
+  while (a < b) {
+    const int m = (a + b) >> 1;
+    if (key_less(sll[m], stie[m], kl, kt)) a = m + 1;
+    else b = m;
+  }
+  const int64_t lo = (int64_t)a * ks.S;
+  const int64_t hi = a < ks.n ? lo + ks.S - 1 : len;   // sample a is not below the key
+  return lo + count_less(ll, tie, lo, hi, kl, kt);
+}
+
+constexpr int kSampNew = 256, kSampSurv = 2048;
+
 // survivors keys[k..n) + k sorted new keys -> out[0..n) by rank scatter; the thread placing the
-// largest key also runs the stop test of the generation.  (A two-level search with LDS-staged
-// samples measured slower: 29 vs 12 us at C3 -- the per-block sample loads cost more than the
-// L2-resident binary searches they save.)
+// largest key also runs the stop test of the generation.  Each binary search starts in an LDS
+// sample of the array it searches (survivors search the new keys, new keys the survivors), so
+// only its last log2 S probes are dependent global loads.
 __global__ void __launch_bounds__(256) merge_new_kernel(const NestArgs a, double* oll,
                                                         long long* otie, int* oslot,
                                                         const double* nl, const long long* nt,
                                                         const int* ns) {
-  if (a.st->stopped) return;
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  NT_STAMP(3, 0);
+  __shared__ double s_nl[kSampNew], s_sl[kSampSurv];
+  __shared__ long long s_nt[kSampNew], s_st[kSampSurv];
   const int64_t n = a.n, k = a.k, ns_ = n - k;
-  if (e >= n) return;
+  const int64_t e0 = (int64_t)blockIdx.x * blockDim.x, e = e0 + threadIdx.x;
+  const bool has_surv = e0 < ns_, has_new = e0 + blockDim.x > ns_;   // block-uniform
+  const double* sll = a.key_ll + k;
+  const long long* stie = a.key_tie + k;
+  const KeySample kn = key_sample(k, kSampNew), kv = key_sample(ns_, kSampSurv);
+  KeySample kv_use = kv;
+  // own key and the samples: all loads issued before the stop flag is read
+  const int64_t ec = e < n ? e : n - 1;
   double kl;
   long long kt;
   int ks;
-  int64_t pos;
-  if (e < ns_) {
-    kl = a.key_ll[k + e];
-    kt = a.key_tie[k + e];
-    ks = a.key_slot[k + e];
-    pos = e + count_less(nl, nt, 0, k, kl, kt);
+  if (ec < ns_) {
+    kl = sll[ec];
+    kt = stie[ec];
+    ks = a.key_slot[k + ec];
   } else {
-    const int64_t b = e - ns_;
-    kl = nl[b];
-    kt = nt[b];
-    ks = ns[b];
-    pos = b + count_less(a.key_ll + k, a.key_tie + k, 0, ns_, kl, kt);
+    kl = nl[ec - ns_];
+    kt = nt[ec - ns_];
+    ks = ns[ec - ns_];
   }
+  if (has_surv && threadIdx.x < kn.n) {
+    const int64_t q = (threadIdx.x + 1) * kn.S - 1;
+    s_nl[threadIdx.x] = nl[q];
+    s_nt[threadIdx.x] = nt[q];
+  }
+  if (has_new) {
+    // survivors' sample: from the compact sample the previous merge kept beside the keys
+    // (contiguous loads) when k is a multiple of its spacing, else strided from the keys
+    const bool compact = k % kKeySample == 0;
+    int64_t m = 1;
+    if (compact)
+      while (ns_ / (kKeySample * m) > kSampSurv) m <<= 1;
+    const KeySample kc{kKeySample * m, (int)(ns_ / (kKeySample * m))};
+    const KeySample ku = compact ? kc : kv;
+    constexpr int kPer = kSampSurv / 256;
+    double tl[kPer];
+    long long tt[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      const int i = min(r * 256 + (int)threadIdx.x, max(ku.n - 1, 0));
+      if (compact) {
+        const int64_t c = k / kKeySample + (int64_t)(i + 1) * m - 1;
+        tl[r] = ku.n > 0 ? a.key_samp_ll[c] : 0.0;
+        tt[r] = ku.n > 0 ? a.key_samp_tie[c] : 0;
+      } else {
+        const int64_t q = (int64_t)(i + 1) * ku.S - 1;
+        tl[r] = ku.n > 0 ? sll[q] : 0.0;
+        tt[r] = ku.n > 0 ? stie[q] : 0;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      const int i = r * 256 + threadIdx.x;
+      if (i < ku.n) {
+        s_sl[i] = tl[r];
+        s_st[i] = tt[r];
+      }
+    }
+    kv_use = ku;
+  }
+  __syncthreads();
+  if (a.st->stopped) return;
+  NT_STAMP(3, 1);
+  if (e >= n) return;
+  int64_t pos;
+  if (e < ns_) pos = e + count_less_2l(nl, nt, k, kn, s_nl, s_nt, kl, kt);
+  else pos = (e - ns_) + count_less_2l(sll, stie, ns_, kv_use, s_sl, s_st, kl, kt);
+  NT_STAMP(3, 2);
   oll[pos] = kl;
   otie[pos] = kt;
   oslot[pos] = ks;
+  if (pos % kKeySample == kKeySample - 1) {          // the next generation's key sample
+    a.out_samp_ll[pos / kKeySample] = kl;
+    a.out_samp_tie[pos / kKeySample] = kt;
+  }
   if (pos == n - 1) stop_test(a, kl);
+  NT_STAMP(3, 3);
+}
+
+__global__ void __launch_bounds__(256) key_sample_kernel(const double* ll, const long long* tie,
+                                                         int64_t n, double* sll, long long* stie) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n / kKeySample) return;
+  sll[c] = ll[(c + 1) * kKeySample - 1];
+  stie[c] = tie[(c + 1) * kKeySample - 1];
+}
+
+hipError_t launch_key_sample(const double* ll, const long long* tie, int64_t n, double* sll,
+                             long long* stie, hipStream_t s) {
+  const int64_t ns = n / kKeySample;
+  if (ns == 0) return hipSuccess;
+  hipLaunchKernelGGL(key_sample_kernel, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, s, ll, tie, n, sll, stie);
+  return hipGetLastError();
 }
 
 hipError_t launch_merge_new(const NestArgs& a, double* out_ll, long long* out_tie, int* out_slot,
@@ -291,67 +401,155 @@ hipError_t launch_merge_new(const NestArgs& a, double* out_ll, long long* out_ti
   return hipGetLastError();
 }
 
+// est = lse(est, G) and log_vol += sum_j log1p(-1/(n-j)), where G is the log-sum of this
+// generation's terms tv[0..k): tv[0] for k = 1 (the reference's fold, nested.ml:138-141), else
+// M + log(sum exp(tv_j - M)) with M = max tv and the exps added by a fixed pairwise tree (pad to a
+// power of two with 0; i + s into i) -- the oracle's tree_lse, operation for operation.  Run by
+// the last workgroup of the retire kernel (1024 threads), after every tv[j] is stored; the tree
+// runs in LDS when the padded generation fits (tv_len <= 4096), else in place in tv.
+constexpr int kEstLds = 4096;
+constexpr int kRetireBlock = 1024;
+
+__device__ __forceinline__ void estimate_body(const NestArgs& a) {
+  __shared__ double sv[kEstLds];
+  __shared__ double s_max[kRetireBlock / 64];
+  __shared__ double2 s_lt[kLogTabN];                 // log table staged in LDS
+  static_assert(kLogTabN <= kRetireBlock, "one log-table entry per thread");
+  if (threadIdx.x < kLogTabN) s_lt[threadIdx.x] = kLogTab[threadIdx.x];
+  const int64_t k = a.k, p2 = a.tv_len;
+  const bool lds = p2 <= kEstLds;
+  double* v = lds ? sv : a.tv;
+  double m = -__builtin_inf();
+  if (lds) {
+    // all loads in flight together (tv was stored sc1 by the retire workgroups)
+    constexpr int kPer = kEstLds / kRetireBlock;
+    double t[kPer];
+#pragma unroll
+    for (int e = 0; e < kPer; ++e) t[e] = ld1(a.tv + min((int64_t)(e * kRetireBlock + threadIdx.x), k - 1));
+#pragma unroll
+    for (int e = 0; e < kPer; ++e) {
+      const int64_t i = e * kRetireBlock + threadIdx.x;
+      if (i < k) m = fmax(m, t[e]);
+      if (i < p2) sv[i] = i < k ? t[e] : 0.0;
+    }
+  } else {
+    for (int64_t i = threadIdx.x; i < p2; i += blockDim.x) {
+      const double t = i < k ? ld1(a.tv + i) : 0.0;
+      if (i < k) m = fmax(m, t);
+      v[i] = t;
+    }
+  }
+  NT_STAMP(1, 5);
+  // M: the block max (exact in any order)
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = m;
+  __syncthreads();
+  double M = s_max[0];
+#pragma unroll
+  for (int w = 1; w < kRetireBlock / 64; ++w) M = fmax(M, s_max[w]);
+  NT_STAMP(1, 6);
+  if (k > 1 && M != -__builtin_inf()) {
+    if (lds) {
+      // the same tree (v[i] += v[i + s], s = p2/2 .. 1) with its levels where the data are:
+      // s >= 1024 in the thread's registers (it holds v[t + 1024 e]), 512 .. 64 in LDS, 32 .. 1
+      // by shuffles inside wave 0
+      constexpr int kPer = kEstLds / kRetireBlock;
+      const int t = threadIdx.x;
+      double e[kPer];
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) {
+        const int64_t i = q * kRetireBlock + t;
+        e[q] = i < k ? pexp(sv[i] - M) : 0.0;
+      }
+      int64_t s = p2 >> 1;
+      for (; s >= kRetireBlock; s >>= 1) {
+        const int d = (int)(s / kRetireBlock);
+#pragma unroll
+        for (int q = 0; q < kPer / 2; ++q)
+          if (q < d) e[q] = e[q] + e[q + d];
+      }
+      double x = e[0];
+      if (s >= 64) {
+        // levels s = 512 .. 64 after one barrier: final v[i] (i < 64) combines v[i + 64 m],
+        // m < 2s/64, by the same tree (m with m + d, d = s/64 .. 1) in wave 0's registers
+        __syncthreads();                             // sv is rewritten
+        sv[t] = x;
+        __syncthreads();
+        if (t < 64) {
+          const int nm = (int)(2 * s / 64);
+          double g[kRetireBlock / 64];
+#pragma unroll
+          for (int q = 0; q < kRetireBlock / 64; ++q) g[q] = q < nm ? sv[t + 64 * q] : 0.0;
+#pragma unroll
+          for (int d = kRetireBlock / 128; d >= 1; d >>= 1)
+            if (d < nm)
+#pragma unroll
+              for (int q = 0; q < d; ++q) g[q] = g[q] + g[q + d];
+          x = g[0];
+        }
+        s = 32;
+      }
+      for (; s >= 1; s >>= 1) x = x + __shfl_down(x, (unsigned)s, 64);
+      if (t == 0) v[0] = x;
+    } else {
+      for (int64_t i = threadIdx.x; i < k; i += blockDim.x) v[i] = pexp(v[i] - M);
+      __syncthreads();
+      for (int64_t s = p2 >> 1; s >= 1; s >>= 1) {
+        for (int64_t i = threadIdx.x; i < s; i += blockDim.x) v[i] = v[i] + v[i + s];
+        __syncthreads();
+      }
+    }
+  }
+  NT_STAMP(1, 7);
+  if (threadIdx.x == 0) {
+    const double G = k == 1 ? v[0] : (M == -__builtin_inf() ? M : M + plog(v[0], s_lt));
+    a.st->est = plse(a.st->est, G, s_lt);
+    a.st->log_vol = a.st->log_vol + a.prefix[k];
+  }
+}
+
 // retire the k lowest (replace_live_point, nested.ml:26-43, slot form): copy each retired row to
 // the dead buffer, put walker j's point into the freed slot, emit its key and ll + log dv.
-// One thread per (point, dim) element; the dim-0 thread also moves the point's scalars.
-__global__ void __launch_bounds__(256) retire_kernel(const NestArgs a, int D) {
-  if (a.st->stopped) return;
+// One thread per (point, dim) element; the dim-0 thread also moves the point's scalars.  The last
+// workgroup to finish folds the generation into the running estimate (estimate_body).
+__global__ void __launch_bounds__(kRetireBlock) retire_kernel(const NestArgs a, int D) {
+  NT_STAMP(1, 0);
+  if (a.st->stopped) return;                         // grid-uniform: set by an earlier launch
+  NT_STAMP(1, 1);
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= a.k * D) return;
-  const int64_t j = g / D;
-  const int d = (int)(g - j * D);
-  const int s = a.key_slot[j];
-  const int64_t m = a.mrep + j;
-  a.dead_x[m * D + d] = a.x[(int64_t)s * D + d];
-  a.x[(int64_t)s * D + d] = a.nx[j * D + d];
-  if (d != 0) return;
-  const double lls = a.ll[s];
-  a.dead_ll[m] = lls;
-  a.dead_lp[m] = a.lp[s];
-  const double lv = a.st->log_vol + a.prefix[j];
-  a.tv[j] = lls + (lv + a.qadd[j]);                 // nested.ml:138-141 (log_dv incl. :140)
-  a.ll[s] = a.nll[j];
-  a.lp[s] = a.nlp[j];
-  a.newk_ll[j] = a.nll[j];
-  a.newk_tie[j] = -(long long)(m + 1);
-  a.newk_slot[j] = s;
+  if (g < a.k * D) {
+    const int64_t j = g / D;
+    const int d = (int)(g - j * D);
+    const int s = a.key_slot[j];
+    const int64_t m = a.mrep + j;
+    a.dead_x[m * D + d] = a.x[(int64_t)s * D + d];
+    a.x[(int64_t)s * D + d] = a.nx[j * D + d];
+    if (d == 0) {
+      const double lls = a.ll[s];
+      a.dead_ll[m] = lls;
+      a.dead_lp[m] = a.lp[s];
+      const double lv = a.st->log_vol + a.prefix[j];
+      st1(a.tv + j, lls + (lv + a.qadd[j]));        // nested.ml:138-141 (log_dv incl. :140)
+      a.ll[s] = a.nll[j];
+      a.lp[s] = a.nlp[j];
+      a.newk_ll[j] = a.nll[j];
+      a.newk_tie[j] = -(long long)(m + 1);
+      a.newk_slot[j] = s;
+      if (a.rank) a.rank[j] = 0;
+    }
+  }
+  NT_STAMP(1, 2);
+  const bool last = last_block_done(a.sync);
+  NT_STAMP(1, 3);
+  if (!last) return;
+  estimate_body(a);
+  NT_STAMP(1, 4);
 }
 
 hipError_t launch_retire(const NestArgs& a, int D, hipStream_t s) {
-  const unsigned grid = (unsigned)((a.k * D + 255) / 256);
-  hipLaunchKernelGGL(retire_kernel, dim3(grid), dim3(256), 0, s, a, D);
-  return hipGetLastError();
-}
-
-// est = lse(est, tree_lse(tv)) with a fixed pairwise tree; log_vol += sum_j log1p(-1/(n-j)).
-// The tree runs in LDS when the padded generation fits (tv_len <= 4096), else in global memory.
-constexpr int kEstLds = 4096;
-
-__global__ void __launch_bounds__(1024) estimate_kernel(const NestArgs a) {
-  if (a.st->stopped) return;
-  __shared__ double sv[kEstLds];
-  __shared__ double2 s_lt[kLogTabN];                 // log table staged in LDS (per-level gathers)
-  for (int i = threadIdx.x; i < kLogTabN; i += blockDim.x) s_lt[i] = kLogTab[i];
-  const int64_t p2 = a.tv_len;
-  const bool lds = p2 <= kEstLds;
-  double* v = lds ? sv : a.tv;
-  for (int64_t i = threadIdx.x; i < p2; i += blockDim.x) {
-    if (i >= a.k) v[i] = -__builtin_inf();
-    else if (lds) v[i] = a.tv[i];
-  }
-  __syncthreads();
-  for (int64_t s = p2 >> 1; s >= 1; s >>= 1) {
-    for (int64_t i = threadIdx.x; i < s; i += blockDim.x) v[i] = plse(v[i], v[i + s], s_lt);
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    a.st->est = plse(a.st->est, v[0], s_lt);
-    a.st->log_vol = a.st->log_vol + a.prefix[a.k];
-  }
-}
-
-hipError_t launch_estimate(const NestArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(estimate_kernel, dim3(1), dim3(1024), 0, s, a);
+  const unsigned grid = (unsigned)((a.k * D + kRetireBlock - 1) / kRetireBlock);
+  hipLaunchKernelGGL(retire_kernel, dim3(grid), dim3(kRetireBlock), 0, s, a, D);
   return hipGetLastError();
 }
 

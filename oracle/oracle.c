@@ -1073,14 +1073,22 @@ static int key_cmp(const void* a, const void* b) {
   return 0;
 }
 
-/* fixed pairwise tree log-sum over v[0..n): pad to a power of two with -inf, combine i, i+s */
+/* log-sum of one generation's k > 1 terms v[0..n) (the k-at-a-time generalisation of the running
+   estimate, nested.ml:138-141; k = 1 is the reference's plain fold): M = max v, then
+   M + log(sum_i exp(v_i - M)) with the exps summed by a fixed pairwise tree (pad to a power of
+   two with 0, add i + s into i).  The kernel (estimate_body, mcg_nested_kernels.hip) does the
+   same operations in the same order. */
 static double tree_lse(double* v, int64_t n) {
+  double M = -INFINITY;
+  for (int64_t i = 0; i < n; ++i) M = v[i] > M ? v[i] : M;
+  if (M == -INFINITY) return -INFINITY;
   int64_t p2 = 1;
   while (p2 < n) p2 <<= 1;
-  for (int64_t i = n; i < p2; ++i) v[i] = -INFINITY;
+  for (int64_t i = 0; i < n; ++i) v[i] = or_exp(v[i] - M);
+  for (int64_t i = n; i < p2; ++i) v[i] = 0.0;
   for (int64_t s = p2 >> 1; s >= 1; s >>= 1)
-    for (int64_t i = 0; i < s; ++i) v[i] = or_plse(v[i], v[i + s]);
-  return v[0];
+    for (int64_t i = 0; i < s; ++i) v[i] = v[i] + v[i + s];
+  return M + or_log(v[0]);
 }
 
 int or_nested(const or_model* m, uint64_t seed, const or_nested_opts* o, double* pts, double* lls,

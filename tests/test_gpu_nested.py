@@ -193,3 +193,18 @@ def test_nested_multilane_walkers_bit_exact(oracle, T, D, k):
     g = gpu_nested(lik, pri, 6, nlive=300, nmcmc=15, mode_hopping_frac=0.1, k=k, max_dead=k * 40)
     o = oracle_nested(oracle, lik, pri, 6, nlive=300, nmcmc=15, mode_hop=0.1, k=k, max_iter=k * 40)
     assert_nested_same(g, o)
+
+
+@pytest.mark.gpu
+def test_nested_rank_count_sort_ties_and_partial_runs(oracle, T):
+    """k = 1000 new keys per generation: three full 256-key runs and a partial one in the
+    counted-rank sort, and walks of 2 steps on a thin shell, so many walkers reject every step and
+    return their (shared) start point: ties among the new keys and with the survivors."""
+    D = 4
+    lik = T.gauss_shell(np.zeros(D), 1.0, 0.02)
+    pri = T.box(-2 * np.ones(D), 2 * np.ones(D))
+    g = gpu_nested(lik, pri, 11, nlive=3000, nmcmc=2, mode_hopping_frac=0.0, k=1000, max_dead=1000 * 12)
+    o = oracle_nested(oracle, lik, pri, 11, nlive=3000, nmcmc=2, mode_hop=0.0, k=1000, max_iter=1000 * 12)
+    assert_nested_same(g, o)
+    u, c = np.unique(g.ll[: 1000 * 12], return_counts=True)
+    assert c.max() > 1                                  # the generations did contain tied keys
