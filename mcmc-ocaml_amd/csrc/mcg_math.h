@@ -173,6 +173,37 @@ __device__ __forceinline__ double pnormal(uint32_t w, const double2* tab) {
   return __hiloint2double(__double2hiint(p) ^ (int)(w & 0x80000000u), __double2loint(p));
 }
 
+// pnormal in two halves, for callers that issue the table gather early and finish later (the
+// nested walker: a gather issued after its prefetched rows would make the in-order vmcnt wait
+// for every row).  Same operations as pnormal.
+struct NrmPending {
+  double x;
+  double2 c0, c1, c2;
+  uint32_t sign;
+};
+__device__ __forceinline__ NrmPending pnormal_issue(uint32_t w, const double2* tab) {
+  const uint32_t v = (w << 1) | 1u;
+  const double dv = (double)v;
+  const uint32_t hi = (uint32_t)__double2hiint(dv);
+  const uint32_t lo = (uint32_t)__double2loint(dv);
+  const double2* c = tab + 3u * ((hi >> 15) - (1023u << kNrmS));
+  NrmPending r;
+  r.x = __hiloint2double((int)((hi & 0x7FFFu) | 0x3FF00000u), (int)lo) - 1.0;
+  r.c0 = c[0];
+  r.c1 = c[1];
+  r.c2 = c[2];
+  r.sign = w & 0x80000000u;
+  return r;
+}
+__device__ __forceinline__ double pnormal_finish(const NrmPending& q) {
+  double p = fma(q.c0.x, q.x, q.c0.y);
+  p = fma(p, q.x, q.c1.x);
+  p = fma(p, q.x, q.c1.y);
+  p = fma(p, q.x, q.c2.x);
+  p = fma(p, q.x, q.c2.y);
+  return __hiloint2double(__double2hiint(p) ^ (int)q.sign, __double2loint(p));
+}
+
 // log1p(r), r in [0,1] (Goldberg: r * log(1+r) / ((1+r)-1)); log-sum-exp on the portable
 // exp/log.  Drives the running nested-sampling estimate (nested.ml:139-142).
 __device__ __forceinline__ double plog1p(double r, const double2* tab = kLogTab) {

@@ -155,6 +155,64 @@ struct WalkTarget {
     }
   }
 
+  // SHELL: the step's constraint test lik(y) >= thr decided on S = |y - c|^2, off the sqrt:
+  // S in [s_in_lo, s_in_hi] passes, S below s_out_lo or above s_out_hi fails, and only S in the
+  // guard bands between is evaluated exactly (lik, psqrt).  The bands are ~1e-9 r wide plus a
+  // bound on the exact evaluation's rounding, so both routes give the same answer.
+  double s_in_lo = 0.0, s_in_hi = 0.0, s_out_lo = 0.0, s_out_hi = 0.0;
+
+  __device__ __forceinline__ void setup_constraint(double thr) {
+    if constexpr (kReg && LIK == MCG_LIK_GAUSS_SHELL) {
+      const double inf = __builtin_inf();
+      const double g = c2 - thr;                     // lik <= c2 everywhere
+      if (!(g >= 0.0) || !(c1 > 0.0) || !(c0 >= 0.0)) {
+        s_in_lo = inf; s_in_hi = -inf;               // nothing definitely passes
+        s_out_lo = g >= 0.0 ? -inf : inf;            // g < 0: everything fails, else exact
+        s_out_hi = g >= 0.0 ? inf : -inf;
+        return;
+      }
+      const double delta = sqrt(2.0 * g) / c1;       // lik = thr at r = c0 -+ delta
+      const double df = 64.0 * 2.220446049250313e-16 * (fabs(c2) + fabs(thr) + 1.0);
+      const double dr = fmax(df / (c1 * c1 * fmax(delta, 1e-300)), sqrt(2.0 * df) / c1);
+      const double band = 1e-9 * (c0 + delta) + 4.0 * dr;
+      const double r_lo = c0 - delta, r_hi = c0 + delta;
+      const double a_lo = fmax(r_lo + band, 0.0), a_hi = r_hi - band;
+      if (a_hi >= a_lo) { s_in_lo = a_lo * a_lo; s_in_hi = a_hi * a_hi; }
+      else { s_in_lo = inf; s_in_hi = -inf; }
+      s_out_lo = (r_lo - band > 0.0) ? (r_lo - band) * (r_lo - band) : -inf;
+      s_out_hi = (r_hi + band) * (r_hi + band);
+    }
+  }
+
+  // lik(y) >= thr, exactly as the comparison of the evaluated likelihood (mcmc_logl, nested.ml:54-59)
+  __device__ __forceinline__ bool constraint(const double* y, int sub, const MhArgs& a, double thr) const {
+    if constexpr (kReg && LIK == MCG_LIK_GAUSS_SHELL) {
+      double A[Lay::NA];
+#pragma unroll
+      for (int j = 0; j < Lay::NA; ++j) A[j] = 0.0;
+#pragma unroll
+      for (int i = 0; i < Lay::NCL; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (!Lay::valid(sub, i, k)) continue;
+          const int j = 4 * i + k;
+          const double e = y[j] - m0[j];
+          A[i % Lay::NA] = fma(e, e, A[i % Lay::NA]);
+        }
+      const double S = reduce_canon<P>(A);
+      bool in = (S >= s_in_lo) & (S <= s_in_hi);
+      const bool out = (S < s_out_lo) | (S > s_out_hi);
+      if (!(in | out)) {                             // guard band (rare): the exact evaluation
+        const double r = psqrt(S);
+        const double qq = (r - c0) * c1;
+        in = (c2 - 0.5 * qq * qq) >= thr;
+      }
+      return in;
+    } else {
+      return lik(y, sub, a) >= thr;
+    }
+  }
+
   __device__ __forceinline__ double prior(const double* y, int sub, const MhArgs& a) const {
     if constexpr (!kReg) {
       return eval_prior<D, P>(y, sub, a, a.pri);
@@ -181,6 +239,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   constexpr int NL = Lay::NL;
   NT_STAMP(0, 0);
   __shared__ double2 s_lt[kLogTabN];                 // math tables staged in LDS (gathers)
+  const double2* nt = kNrmTab;   // (an LDS copy costs more to stage than its gathers save: 62 vs 52 us)
   for (int i = threadIdx.x; i < kLogTabN; i += blockDim.x) s_lt[i] = kLogTab[i];
   __syncthreads();
   if (a.st->stopped) return;
@@ -224,10 +283,40 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   };
   WalkTarget<D, P, LIK> tgt;
   tgt.load(a.m, sub);
+  tgt.setup_constraint(thr);
   load_row(cur, start);
   double cur_l = (a.ll[start] >= thr) ? a.lp[start] : -__builtin_inf();   // mcmc_logl, :54-59
-  // partner rows of steps s .. s + PD - 1 in flight: ring slot u holds step s0 + u
   constexpr int PD = kNestPrefetch;
+  // The random numbers of a group of PD steps are independent of the walker state.  With P = 4
+  // lane q of the quad draws those of steps s0 + 4h + q (DE scale, accept uniform, and the DE
+  // indices of step s0 + 4h + q + PD, whose rows refill that slot), one group AHEAD: the normal's
+  // table gather of group g + 1 is issued before group g's row refills, so waiting for it never
+  // drains the prefetched rows (the vector-memory counter is in order).
+  struct GroupRng {
+    uint32_t pi[PD / 4 > 0 ? PD / 4 : 1], pj[PD / 4 > 0 ? PD / 4 : 1];
+    double hop[PD / 4 > 0 ? PD / 4 : 1], lu[PD / 4 > 0 ? PD / 4 : 1];
+    NrmPending z[PD / 4 > 0 ? PD / 4 : 1];
+  };
+  auto group_issue = [&](int64_t s0, GroupRng& G) {
+    if constexpr (P == 4 && PD % 4 == 0) {
+#pragma unroll
+      for (int h = 0; h < PD / 4; ++h) {
+        const int64_t sq = s0 + 4 * h + sub;
+        const u32x4 rI = rng(wid, (uint32_t)(sq + PD), CALL_DE_IDX, TAG_NEST_WALK, 0u);
+        const u32x4 rS = rng(wid, (uint32_t)sq, CALL_DE_SCALE, TAG_NEST_WALK, 0u);
+        const u32x4 rA = rng(wid, (uint32_t)sq, CALL_ACCEPT, TAG_NEST_WALK, 0u);
+        G.pi[h] = randint(rI.x, rI.y, n);
+        const uint32_t pjj = randint(rI.z, rI.w, n - 1);
+        G.pj[h] = pjj + (pjj >= G.pi[h] ? 1u : 0u);
+        G.z[h] = pnormal_issue(rS.z, nt);
+        G.hop[h] = u53(rS.x, rS.y);
+        G.lu[h] = plog(u53(rA.x, rA.y), s_lt);
+      }
+    }
+  };
+  GroupRng gcur, gnext;
+  group_issue(0, gcur);   // before the ring's first rows: its gather is then never the newest load
+  // partner rows of steps s .. s + PD - 1 in flight: ring slot u holds step s0 + u
   double bi[PD][NL], bj[PD][NL];
 #pragma unroll
   for (int u = 0; u < PD; ++u) {
@@ -239,33 +328,26 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   // whole groups of PD steps with no data-dependent branches around the loads, so the compiler
   // can count the in-flight loads (vmcnt) across iterations; steps past nmcmc only compute
   for (int64_t s0 = 0; s0 < a.nmcmc; s0 += PD) {
-    // phase 1: the random numbers of the group's PD steps -- independent of the walker state, so
-    // the PD Philox / normal / log chains overlap instead of sitting in the serial chain
     double dsc_g[PD], lu_g[PD];
     uint32_t ip_g[PD], jp_g[PD];
-    if constexpr (P == 4 && PD == 4) {
-      // lane q of the walker's quad draws every random number of step s0 + q (its DE scale and
-      // accept uniform, and the DE indices of step s0 + q + PD, whose rows refill slot q); the
-      // quad broadcasts (DPP) hand step u's values from lane u to the whole quad.  Each lane
-      // runs three Philox calls, one normal and one log per group instead of per step.
-      const int64_t sq = s0 + sub;
-      const u32x4 rI = rng(wid, (uint32_t)(sq + PD), CALL_DE_IDX, TAG_NEST_WALK, 0u);
-      const u32x4 rS = rng(wid, (uint32_t)sq, CALL_DE_SCALE, TAG_NEST_WALK, 0u);
-      const u32x4 rA = rng(wid, (uint32_t)sq, CALL_ACCEPT, TAG_NEST_WALK, 0u);
-      const uint32_t pi = randint(rI.x, rI.y, n);
-      const uint32_t pjj = randint(rI.z, rI.w, n - 1);
-      const uint32_t pj = pjj + (pjj >= pi ? 1u : 0u);
-      const double z0 = pnormal(rS.z, kNrmTab);
-      const double dloc = (a.mode_hop != 0.0 && u53(rS.x, rS.y) < a.mode_hop) ? 1.0 : a.sigma_de * z0;
-      const double lloc = plog(u53(rA.x, rA.y), s_lt);
-      ip_g[0] = quad_bcast_u32<0>(pi); ip_g[1] = quad_bcast_u32<1>(pi);
-      ip_g[2] = quad_bcast_u32<2>(pi); ip_g[3] = quad_bcast_u32<3>(pi);
-      jp_g[0] = quad_bcast_u32<0>(pj); jp_g[1] = quad_bcast_u32<1>(pj);
-      jp_g[2] = quad_bcast_u32<2>(pj); jp_g[3] = quad_bcast_u32<3>(pj);
-      dsc_g[0] = quad_bcast_f64<0>(dloc); dsc_g[1] = quad_bcast_f64<1>(dloc);
-      dsc_g[2] = quad_bcast_f64<2>(dloc); dsc_g[3] = quad_bcast_f64<3>(dloc);
-      lu_g[0] = quad_bcast_f64<0>(lloc); lu_g[1] = quad_bcast_f64<1>(lloc);
-      lu_g[2] = quad_bcast_f64<2>(lloc); lu_g[3] = quad_bcast_f64<3>(lloc);
+    if constexpr (P == 4 && PD % 4 == 0) {
+      // finish this group's draws and hand step u's values from lane u % 4 to the quad (DPP)
+#pragma unroll
+      for (int h = 0; h < PD / 4; ++h) {
+        const double z0 = pnormal_finish(gcur.z[h]);
+        const double dloc = (a.mode_hop != 0.0 && gcur.hop[h] < a.mode_hop) ? 1.0 : a.sigma_de * z0;
+        const uint32_t pi = gcur.pi[h], pj = gcur.pj[h];
+        const double lloc = gcur.lu[h];
+        ip_g[4 * h + 0] = quad_bcast_u32<0>(pi); ip_g[4 * h + 1] = quad_bcast_u32<1>(pi);
+        ip_g[4 * h + 2] = quad_bcast_u32<2>(pi); ip_g[4 * h + 3] = quad_bcast_u32<3>(pi);
+        jp_g[4 * h + 0] = quad_bcast_u32<0>(pj); jp_g[4 * h + 1] = quad_bcast_u32<1>(pj);
+        jp_g[4 * h + 2] = quad_bcast_u32<2>(pj); jp_g[4 * h + 3] = quad_bcast_u32<3>(pj);
+        dsc_g[4 * h + 0] = quad_bcast_f64<0>(dloc); dsc_g[4 * h + 1] = quad_bcast_f64<1>(dloc);
+        dsc_g[4 * h + 2] = quad_bcast_f64<2>(dloc); dsc_g[4 * h + 3] = quad_bcast_f64<3>(dloc);
+        lu_g[4 * h + 0] = quad_bcast_f64<0>(lloc); lu_g[4 * h + 1] = quad_bcast_f64<1>(lloc);
+        lu_g[4 * h + 2] = quad_bcast_f64<2>(lloc); lu_g[4 * h + 3] = quad_bcast_f64<3>(lloc);
+      }
+      group_issue(s0 + PD, gnext);                    // next group's gathers go out first
     } else
 #pragma unroll
     for (int u = 0; u < PD; ++u) {
@@ -280,7 +362,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
         const u32x4 r = rng(wid, (uint32_t)(sub == 0 ? sp : s), call, TAG_NEST_WALK, 0u);
         const uint32_t pi = randint(r.x, r.y, n);
         const uint32_t pjj = randint(r.z, r.w, n - 1);
-        const double z0 = pnormal(r.z, kNrmTab);
+        const double z0 = pnormal(r.z, nt);
         const double hop_u = u53(r.x, r.y);
         const double dloc = (a.mode_hop != 0.0 && hop_u < a.mode_hop) ? 1.0 : a.sigma_de * z0;
         const double lloc = plog(hop_u, s_lt);
@@ -295,13 +377,13 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
         if (a.mode_hop != 0.0 && u53(rs.x, rs.y) < a.mode_hop) {
           dsc_g[u] = 1.0;
         } else {
-          dsc_g[u] = a.sigma_de * pnormal(rs.z, kNrmTab);
+          dsc_g[u] = a.sigma_de * pnormal(rs.z, nt);
         }
         const u32x4 ra = rng(wid, (uint32_t)s, CALL_ACCEPT, TAG_NEST_WALK, 0u);
         lu_g[u] = plog(u53(ra.x, ra.y), s_lt);
       }
     }
-    // phase 2: the serial constrained steps
+    // the serial constrained steps
 #pragma unroll
     for (int u = 0; u < PD; ++u) {
       const bool live = s0 + u < a.nmcmc;
@@ -309,16 +391,19 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
       for (int d = 0; d < NL; ++d) y[d] = cur[d] + dsc_g[u] * (bj[u][d] - bi[u][d]);
       load_row(bi[u], ip_g[u]);                        // refill slot u with step s + PD's rows
       load_row(bj[u], jp_g[u]);
-      const double lly = tgt.lik(y, sub, a.m);
+      const bool ok = tgt.constraint(y, sub, a.m, thr);
       const double lpy = tgt.prior(y, sub, a.m);
-      const double ml = (lly >= thr) ? lpy : -__builtin_inf();
-      const double ratio = (((ml + 0.0) - (cur_l + 0.0)) + 0.0) - 0.0;   // mcmc.ml:47-48
+      const double ml = ok ? lpy : -__builtin_inf();
+      // mcmc.ml:47-48 computes (((ml + 0) - (cur_l + 0)) + 0) - 0 (flat proposal density); the
+      // +0 / -0 terms change at most the sign of a zero, so `lu < ratio` is the same test
+      const double ratio = ml - cur_l;
       if (live && lu_g[u] < ratio) {
 #pragma unroll
         for (int d = 0; d < NL; ++d) cur[d] = y[d];
         cur_l = ml;
       }
     }
+    if constexpr (P == 4 && PD % 4 == 0) gcur = gnext;
   }
   const double nl = tgt.lik(cur, sub, a.m);
   const double np = tgt.prior(cur, sub, a.m);
