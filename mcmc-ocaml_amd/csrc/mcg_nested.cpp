@@ -45,7 +45,7 @@ struct KeyBuf {
 };
 
 struct NestedBufs {
-  DevBuf x, ll, lp, nx, nll, nlp, tv, prefix, qadd, st, dead_x, dead_ll, dead_lp, rank, sync, trace;
+  DevBuf x, ll, lp, nx, nll, nlp, tv, prefix, qadd, st, dead_x, dead_ll, dead_lp, rank, sync, trace, chk;
   KeyBuf keys[2], newk, newk_tmp;
   int64_t dead_cap = 0;
   // pinned staging of two in-flight batches' dead (ll, lp) and their completion events
@@ -332,6 +332,11 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   if (!B.h_st) HC(hipHostMalloc((void**)&B.h_st, 2 * sizeof(NestDevState), 0), "alloc pinned state");
   NestDevState* hst = B.h_st;
   int64_t gen = 0, reported = 0, batch = 4;
+  const bool check = std::getenv("MCG_NESTED_CHECK") != nullptr;
+  if (check) {
+    HC(B.chk.ensure(4 * 8), "alloc check");
+    HC(hipMemsetAsync(B.chk.p, 0, 4 * 8, s), "clear check");
+  }
 #ifdef MCG_NEST_TRACE
   // phase stamps of one generation (MCG_NEST_TRACE=<generation>), printed at the end
   const char* trace_env = std::getenv("MCG_NEST_TRACE");
@@ -393,7 +398,9 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
                             B.newk_tmp.s(), k, &nk_tmp, s, a.st), "sort new keys");
       }
       KeyBuf& nk = nk_tmp ? B.newk_tmp : B.newk;
+      if (check) HC(launch_check_sorted(nk.l(), nk.t(), k, g, (long long*)B.chk.p, s), "check");
       HC(launch_merge_new(a, nxt.l(), nxt.t(), nxt.s(), nk.l(), nk.t(), nk.s(), s), "merge keys");
+      if (check) HC(launch_check_sorted(nxt.l(), nxt.t(), n, g, (long long*)B.chk.p + 1, s), "check");
     }
     HC(hipMemcpyAsync(&hst[q], B.st.p, sizeof(NestDevState), hipMemcpyDeviceToHost, s), "read state");
     HC(hipMemcpyAsync(B.h_stage[2 * q], (double*)B.dead_ll.p + gen * k, G * k * 8, hipMemcpyDeviceToHost, s),
@@ -505,6 +512,33 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   HC(hipMemcpy(lx.data(), B.x.p, n * D * 8, hipMemcpyDeviceToHost), "copy live");
   HC(hipMemcpy(lll.data(), B.ll.p, n * 8, hipMemcpyDeviceToHost), "copy live");
   HC(hipMemcpy(llp.data(), B.lp.p, n * 8, hipMemcpyDeviceToHost), "copy live");
+  if (std::getenv("MCG_NESTED_CHECK")) {
+    // diagnostics: the same copies after a device-wide synchronisation, and the final keys
+    // against the live set they index
+    HC(hipDeviceSynchronize(), "check sync");
+    std::vector<int> slots2((size_t)n);
+    std::vector<double> lll2((size_t)n), kl((size_t)n);
+    NestDevState st2{};
+    long long ck[4];
+    HC(hipMemcpy(ck, B.chk.p, sizeof ck, hipMemcpyDeviceToHost), "check");
+    std::fprintf(stderr, "mcg_nested check: first unsorted generation+1: new keys %lld, merged %lld (pairs %lld)\n",
+                 ck[0], ck[1], ck[2]);
+    HC(hipMemcpy(slots2.data(), fin.slot.p, n * 4, hipMemcpyDeviceToHost), "check");
+    HC(hipMemcpy(lll2.data(), B.ll.p, n * 8, hipMemcpyDeviceToHost), "check");
+    HC(hipMemcpy(kl.data(), fin.ll.p, n * 8, hipMemcpyDeviceToHost), "check");
+    HC(hipMemcpy(&st2, B.st.p, sizeof st2, hipMemcpyDeviceToHost), "check");
+    int64_t dslot = 0, dll = 0, incons = 0, unsorted = 0, first = -1;
+    for (int64_t j = 0; j < n; ++j) {
+      dslot += slots2[(size_t)j] != slots[(size_t)j];
+      dll += lll2[(size_t)j] != lll[(size_t)j];
+      if (lll2[(size_t)slots2[(size_t)j]] != kl[(size_t)j]) { ++incons; if (first < 0) first = j; }
+      if (j && kl[(size_t)j] < kl[(size_t)j - 1]) ++unsorted;
+    }
+    std::fprintf(stderr, "mcg_nested check: gen_done host %lld dev %lld stopped %d/%d; recopy diffs slots %lld ll %lld; "
+                 "keys vs live ll mismatches %lld (first %lld); unsorted keys %lld\n",
+                 (long long)st.gen_done, (long long)st2.gen_done, st.stopped, st2.stopped, (long long)dslot,
+                 (long long)dll, (long long)incons, (long long)first, (long long)unsorted);
+  }
   for (int64_t j = 0; j < n; ++j) {
     const int sl = slots[(size_t)j];
     std::memcpy(&R.pts[(size_t)j * D], &lx[(size_t)sl * D], sizeof(double) * D);

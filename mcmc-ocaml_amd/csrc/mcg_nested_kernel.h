@@ -25,6 +25,17 @@ struct NestDevState {
   long long gen_done;
 };
 
+// The stop / error flags and the generation count are read and written with agent-scope atomics
+// (sc1: past the L1 and scalar caches).  A kernel that read a stale stopped == 0 after the
+// stopping generation would run a partial generation after the stop (seen with another process
+// sharing the GPU: a retire kernel replaced live rows that the final keys no longer described).
+__device__ __forceinline__ bool nest_stopped(const NestDevState* st) {
+  return __hip_atomic_load(&st->stopped, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
+__device__ __forceinline__ void nest_set(int32_t* flag) {
+  __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // last-workgroup hand-off counters (mcg_nested_kernels.hip, last_block_done): per use a top counter
 // and 16 group counters, each on a 128-B line of its own; every counter is reset by the workgroup
 // that completes it
@@ -242,7 +253,19 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   const double2* nt = kNrmTab;   // (an LDS copy costs more to stage than its gathers save: 62 vs 52 us)
   for (int i = threadIdx.x; i < kLogTabN; i += blockDim.x) s_lt[i] = kLogTab[i];
   __syncthreads();
-  if (a.st->stopped) return;
+  if (nest_stopped(a.st)) return;
+  if (a.mrep > 0) {
+    // the previous generation's stop test (remaining_integral_negligable, nested.ml:45-48, on the
+    // max live ll; or a failed draw, nested.ml:70-72), made by every workgroup from the same
+    // inputs: a flag set inside a kernel could be seen by only some of its workgroups (a late
+    // starter would skip its share of the work), so no kernel reads the flag it may set
+    const double live = a.st->log_vol + a.key_ll[a.n - 1];
+    const bool err = __hip_atomic_load(&a.st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    if (live - plse(a.st->est, live, s_lt) <= a.log_epsrel || err) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) nest_set(&a.st->stopped);
+      return;
+    }
+  }
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int sub = (int)(tid & (P - 1));
   const int64_t w = tid / P;
@@ -416,7 +439,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   if (sub == 0) {
     a.nll[w] = nl;
     a.nlp[w] = np;
-    if (!(nl >= thr)) a.st->error = 1;               // nested.ml:70-72 -> Failure
+    if (!(nl >= thr)) nest_set(&a.st->error);        // nested.ml:70-72 -> Failure
   }
 }
 
@@ -474,6 +497,8 @@ hipError_t launch_sort_keys(double* ll, long long* tie, int* slot, double* tll, 
 hipError_t launch_merge_new(const NestArgs& a, double* out_ll, long long* out_tie, int* out_slot,
                             const double* new_ll, const long long* new_tie, const int* new_slot,
                             hipStream_t st);
+hipError_t launch_check_sorted(const double* ll, const long long* tie, int64_t n, long long gen,
+                               long long* out, hipStream_t st);
 // retire the k lowest; the last workgroup also folds the generation into the running estimate
 hipError_t launch_retire(const NestArgs& a, int D, hipStream_t st);
 // every kKeySample-th of n sorted keys (indices kKeySample-1, 2 kKeySample-1, ...) into s*

@@ -31,7 +31,7 @@ constexpr int kChunk = 2048;
 // bitonic sort of independent 2048-key chunks in LDS
 __global__ void __launch_bounds__(256) sort_chunks_kernel(double* ll, long long* tie, int* slot,
                                                           int64_t n, const NestDevState* stop) {
-  if (stop && stop->stopped) return;
+  if (stop && nest_stopped(stop)) return;
   __shared__ double sl[kChunk];
   __shared__ long long st[kChunk];
   __shared__ int ss[kChunk];
@@ -75,7 +75,7 @@ __global__ void __launch_bounds__(256) merge_pass_kernel(const double* ll, const
                                                          const int* slot, double* oll, long long* otie,
                                                          int* oslot, int64_t n, int64_t w,
                                                          const NestDevState* stop) {
-  if (stop && stop->stopped) return;
+  if (stop && nest_stopped(stop)) return;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   const int64_t base = (e / (2 * w)) * (2 * w);
@@ -170,7 +170,7 @@ constexpr int kSub = 128;                            // keys of the compared-aga
 __global__ void __launch_bounds__(256) rank_count_kernel(const NestArgs a, int nruns, double* oll,
                                                          long long* otie, int* oslot) {
   NT_STAMP(2, 0);
-  if (a.st->stopped) return;                         // grid-uniform: set by an earlier launch
+  if (nest_stopped(a.st)) return;                         // grid-uniform: set by an earlier launch
   __shared__ double sl[kSub];
   __shared__ double s_ll[kSmallSort];                // last block: keys placed at their ranks
   __shared__ short s_j[kSmallSort];
@@ -253,8 +253,6 @@ hipError_t launch_sort_new_small(const NestArgs& a, double* oll, long long* otie
   return hipGetLastError();
 }
 
-__device__ __forceinline__ void stop_test(const NestArgs& a, double max_ll);
-
 // Search samples of a sorted key array staged in LDS: every S-th key (indices S-1, 2S-1, ...), at
 // most `cap` of them; S is the smallest power of two >= 16 that keeps the count within cap.
 struct KeySample {
@@ -286,7 +284,7 @@ __device__ __forceinline__ int64_t count_less_2l(const double* ll, const long lo
 constexpr int kSampNew = 256, kSampSurv = 2048;
 
 // survivors keys[k..n) + k sorted new keys -> out[0..n) by rank scatter; the thread placing the
-// largest key also runs the stop test of the generation.  Each binary search starts in an LDS
+// largest key also counts the generation (the stop test runs at the start of the next walk).  Each binary search starts in an LDS
 // sample of the array it searches (survivors search the new keys, new keys the survivors), so
 // only its last log2 S probes are dependent global loads.
 __global__ void __launch_bounds__(256) merge_new_kernel(const NestArgs a, double* oll,
@@ -358,7 +356,7 @@ __global__ void __launch_bounds__(256) merge_new_kernel(const NestArgs a, double
     kv_use = ku;
   }
   __syncthreads();
-  if (a.st->stopped) return;
+  if (nest_stopped(a.st)) return;
   NT_STAMP(3, 1);
   if (e >= n) return;
   int64_t pos;
@@ -372,7 +370,7 @@ __global__ void __launch_bounds__(256) merge_new_kernel(const NestArgs a, double
     a.out_samp_ll[pos / kKeySample] = kl;
     a.out_samp_tie[pos / kKeySample] = kt;
   }
-  if (pos == n - 1) stop_test(a, kl);
+  if (pos == n - 1) __hip_atomic_fetch_add(&a.st->gen_done, 1LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   NT_STAMP(3, 3);
 }
 
@@ -515,7 +513,7 @@ __device__ __forceinline__ void estimate_body(const NestArgs& a) {
 // workgroup to finish folds the generation into the running estimate (estimate_body).
 __global__ void __launch_bounds__(kRetireBlock) retire_kernel(const NestArgs a, int D) {
   NT_STAMP(1, 0);
-  if (a.st->stopped) return;                         // grid-uniform: set by an earlier launch
+  if (nest_stopped(a.st)) return;                         // grid-uniform: set by an earlier launch
   NT_STAMP(1, 1);
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g < a.k * D) {
@@ -553,13 +551,25 @@ hipError_t launch_retire(const NestArgs& a, int D, hipStream_t s) {
   return hipGetLastError();
 }
 
-// remaining_integral_negligable (nested.ml:45-48) on the replaced live set; run by the thread of
-// merge_new_kernel that places the largest key (final_ll[n - 1])
-__device__ __forceinline__ void stop_test(const NestArgs& a, double max_ll) {
-  const double live = a.st->log_vol + max_ll;
-  if (live - plse(a.st->est, live) <= a.log_epsrel) a.st->stopped = 1;
-  if (a.st->error) a.st->stopped = 1;
-  a.st->gen_done += 1;
+
+
+// diagnostics (MCG_NESTED_CHECK): records in out[0..1] the first generation (+1) whose keys
+// [0, n) are not strictly ascending in (ll, tie), out[2] the count of such pairs
+__global__ void __launch_bounds__(256) check_sorted_kernel(const double* ll, const long long* tie,
+                                                           int64_t n, long long gen, long long* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i + 1 >= n) return;
+  if (!key_less(ll[i], tie[i], ll[i + 1], tie[i + 1])) {
+    atomicCAS((unsigned long long*)out, 0ull, (unsigned long long)(gen + 1));
+    atomicAdd((unsigned long long*)(out + 2), 1ull);
+  }
+}
+
+hipError_t launch_check_sorted(const double* ll, const long long* tie, int64_t n, long long gen,
+                               long long* out, hipStream_t s) {
+  if (n < 2) return hipSuccess;
+  hipLaunchKernelGGL(check_sorted_kernel, dim3((unsigned)((n + 254) / 256)), dim3(256), 0, s, ll, tie, n, gen, out);
+  return hipGetLastError();
 }
 
 }  // namespace mcg

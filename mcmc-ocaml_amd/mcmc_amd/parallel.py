@@ -8,6 +8,9 @@ partials (2D+3 doubles per tile); every rank then folds the tiles in global orde
 mcg_combine_tiles, which makes the moments and the harmonic-mean evidence bit-identical for any
 number of GPUs.
 """
+import os
+import sys
+
 import numpy as np
 
 from . import nested as _nested
@@ -95,6 +98,17 @@ def nested_evidence_replicas(log_likelihood, log_prior, epsrel=0.01, nmcmc=1000,
     with Context(seed=replica_seed(seed, rank), device=device) as ctx:
         out = _nested.nested_evidence(log_likelihood, log_prior, epsrel=epsrel, nmcmc=nmcmc,
                                       nlive=nl, mode_hopping_frac=mode_hopping_frac, k=kk, ctx=ctx)
+    if os.environ.get("MCG_DEBUG_REPLICAS"):
+        print("replica rank %d: log Z %.6f n_dead %d n_gen %d" % (rank, out[0], out.n_dead, out.n_gen),
+              file=sys.stderr, flush=True)
     if world == 1:
         return out
-    return _nested.merge_runs(allgather_runs(out, nl, kk, comm_device, group, points=points))
+    runs = allgather_runs(out, nl, kk, comm_device, group, points=points)
+    merged = _nested.merge_runs(runs)
+    if os.environ.get("MCG_DEBUG_REPLICAS"):
+        for i, (o, a, b) in enumerate(runs):
+            print("rank %d sees run %d: n %d nlive %d k %d ll[0] %.4f ll[-1] %.4f sorted %s" % (
+                rank, i, len(o.ll), a, b, o.ll[0], o.ll[-1], bool(np.all(np.diff(o.ll) >= 0))),
+                file=sys.stderr, flush=True)
+        print("rank %d merged log Z %.6f" % (rank, merged[0]), file=sys.stderr, flush=True)
+    return merged
