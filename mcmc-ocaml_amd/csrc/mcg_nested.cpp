@@ -8,6 +8,8 @@
 // Batches are pipelined: while the GPU runs batch b + 1, a host worker folds batch b's dead
 // points into evidence_error_and_weights (nested.ml:81-120); the live points are folded in once
 // the run has stopped.
+#include <sys/mman.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -500,50 +502,49 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   const int64_t ndead = st.gen_done * k;
   const int64_t ntot = ndead + n;
   KeyBuf& fin = B.keys[(base + st.gen_done) % 2];
-  // the dead rows stay on the device (B.dead_x) until mcg_nested_get copies them straight into
-  // the caller's buffer; the host keeps ll / lp (for the weights) and the final live rows
-  R.pts.assign((size_t)n * D, 0.0);
+  // every row stays on the device: the live rows are gathered in key order behind the dead rows
+  // (B.dead_x), where mcg_nested_get copies all of them straight into the caller's buffer; the
+  // host gets ll / lp (for the weights)
+  if (ntot > B.dead_cap) {
+    DevBuf nxb, nlb, npb;
+    HC(nxb.ensure(ntot * D * 8), "alloc dead");
+    HC(nlb.ensure(ntot * 8), "alloc dead");
+    HC(npb.ensure(ntot * 8), "alloc dead");
+    if (ndead > 0) {
+      HC(hipMemcpyAsync(nxb.p, B.dead_x.p, ndead * D * 8, hipMemcpyDeviceToDevice, s), "grow dead");
+      HC(hipMemcpyAsync(nlb.p, B.dead_ll.p, ndead * 8, hipMemcpyDeviceToDevice, s), "grow dead");
+      HC(hipMemcpyAsync(npb.p, B.dead_lp.p, ndead * 8, hipMemcpyDeviceToDevice, s), "grow dead");
+    }
+    HC(hipStreamSynchronize(s), "grow dead");
+    std::swap(B.dead_x.p, nxb.p); std::swap(B.dead_x.bytes, nxb.bytes);
+    std::swap(B.dead_ll.p, nlb.p); std::swap(B.dead_ll.bytes, nlb.bytes);
+    std::swap(B.dead_lp.p, npb.p); std::swap(B.dead_lp.bytes, npb.bytes);
+    B.dead_cap = ntot;
+  }
+  HC(launch_gather_live((const double*)B.x.p, (const double*)B.ll.p, (const double*)B.lp.p, fin.s(), n, D,
+                        (double*)B.dead_x.p + ndead * D, (double*)B.dead_ll.p + ndead,
+                        (double*)B.dead_lp.p + ndead, s), "gather live");
   R.ll.resize((size_t)ntot);
   R.lp.resize((size_t)ntot);
   R.wts.resize((size_t)ntot);
-  std::vector<int> slots((size_t)n);
-  std::vector<double> lx((size_t)n * D), lll((size_t)n), llp((size_t)n);
-  HC(hipMemcpy(slots.data(), fin.slot.p, n * 4, hipMemcpyDeviceToHost), "copy keys");
-  HC(hipMemcpy(lx.data(), B.x.p, n * D * 8, hipMemcpyDeviceToHost), "copy live");
-  HC(hipMemcpy(lll.data(), B.ll.p, n * 8, hipMemcpyDeviceToHost), "copy live");
-  HC(hipMemcpy(llp.data(), B.lp.p, n * 8, hipMemcpyDeviceToHost), "copy live");
+  HC(hipMemcpyAsync(R.ll.data() + ndead, (double*)B.dead_ll.p + ndead, n * 8, hipMemcpyDeviceToHost, s), "copy live");
+  HC(hipMemcpyAsync(R.lp.data() + ndead, (double*)B.dead_lp.p + ndead, n * 8, hipMemcpyDeviceToHost, s), "copy live");
+  HC(hipStreamSynchronize(s), "copy live");
   if (std::getenv("MCG_NESTED_CHECK")) {
-    // diagnostics: the same copies after a device-wide synchronisation, and the final keys
-    // against the live set they index
-    HC(hipDeviceSynchronize(), "check sync");
-    std::vector<int> slots2((size_t)n);
-    std::vector<double> lll2((size_t)n), kl((size_t)n);
-    NestDevState st2{};
+    // diagnostics: device-side sortedness of every generation, and the final keys against the
+    // live ll they index
     long long ck[4];
+    std::vector<double> kl((size_t)n);
     HC(hipMemcpy(ck, B.chk.p, sizeof ck, hipMemcpyDeviceToHost), "check");
-    std::fprintf(stderr, "mcg_nested check: first unsorted generation+1: new keys %lld, merged %lld (pairs %lld)\n",
-                 ck[0], ck[1], ck[2]);
-    HC(hipMemcpy(slots2.data(), fin.slot.p, n * 4, hipMemcpyDeviceToHost), "check");
-    HC(hipMemcpy(lll2.data(), B.ll.p, n * 8, hipMemcpyDeviceToHost), "check");
     HC(hipMemcpy(kl.data(), fin.ll.p, n * 8, hipMemcpyDeviceToHost), "check");
-    HC(hipMemcpy(&st2, B.st.p, sizeof st2, hipMemcpyDeviceToHost), "check");
-    int64_t dslot = 0, dll = 0, incons = 0, unsorted = 0, first = -1;
+    int64_t incons = 0, unsorted = 0;
     for (int64_t j = 0; j < n; ++j) {
-      dslot += slots2[(size_t)j] != slots[(size_t)j];
-      dll += lll2[(size_t)j] != lll[(size_t)j];
-      if (lll2[(size_t)slots2[(size_t)j]] != kl[(size_t)j]) { ++incons; if (first < 0) first = j; }
+      incons += R.ll[(size_t)(ndead + j)] != kl[(size_t)j];
       if (j && kl[(size_t)j] < kl[(size_t)j - 1]) ++unsorted;
     }
-    std::fprintf(stderr, "mcg_nested check: gen_done host %lld dev %lld stopped %d/%d; recopy diffs slots %lld ll %lld; "
-                 "keys vs live ll mismatches %lld (first %lld); unsorted keys %lld\n",
-                 (long long)st.gen_done, (long long)st2.gen_done, st.stopped, st2.stopped, (long long)dslot,
-                 (long long)dll, (long long)incons, (long long)first, (long long)unsorted);
-  }
-  for (int64_t j = 0; j < n; ++j) {
-    const int sl = slots[(size_t)j];
-    std::memcpy(&R.pts[(size_t)j * D], &lx[(size_t)sl * D], sizeof(double) * D);
-    R.ll[(size_t)(ndead + j)] = lll[(size_t)sl];
-    R.lp[(size_t)(ndead + j)] = llp[(size_t)sl];
+    std::fprintf(stderr, "mcg_nested check: first unsorted generation+1: new keys %lld, merged %lld; final keys "
+                 "vs live ll mismatches %lld, unsorted keys %lld\n", ck[0], ck[1], (long long)incons,
+                 (long long)unsorted);
   }
   const auto t_copy = now();
   fold.finish(R.ll.data(), ntot, R.wts.data(), &R.log_ev, &R.log_dev);
@@ -552,6 +553,7 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
                  ms(t_start, t_gen), ms(t_gen, t_copy), ms(t_copy, now()));
   R.n_total = ntot;
   R.n_dead = ndead;
+  R.ndim = D;
   R.n_gen = st.gen_done;
   R.nlive = n;
   if (res) {
@@ -576,6 +578,13 @@ static hipError_t copy_d2h_large(NestedBufs& B, void* dst, const void* src, size
     hipError_t e;
     if (!B.h_ring[r] && (e = hipHostMalloc(&B.h_ring[r], CH, 0)) != hipSuccess) return e;
     if (!B.ev_ring[r] && (e = hipEventCreateWithFlags(&B.ev_ring[r], hipEventDisableTiming)) != hipSuccess) return e;
+  }
+  {
+    // the destination is usually fresh (numpy) memory: ask for transparent huge pages, so first
+    // touch takes ~1/512 of the page faults (advice only; ignored where THP is off)
+    const uintptr_t a0 = ((uintptr_t)dst + (2u << 20) - 1) & ~(uintptr_t)((2u << 20) - 1);
+    const uintptr_t a1 = ((uintptr_t)dst + bytes) & ~(uintptr_t)((2u << 20) - 1);
+    if (a1 > a0) (void)madvise((void*)a0, a1 - a0, MADV_HUGEPAGE);
   }
   const size_t nch = (bytes + CH - 1) / CH;
   auto len = [&](size_t c) { return std::min(CH, bytes - c * CH); };
@@ -625,14 +634,10 @@ int mcg_nested_get(mcg_ctx* ctx, double* pts, double* ll, double* lp, double* lo
   if (R.n_total == 0) return set_error(ctx, MCG_ESTATE, "no nested run");
   const auto t0 = std::chrono::steady_clock::now();
   if (pts) {
-    const int64_t D = (int64_t)(R.pts.size() / (size_t)R.nlive);
-    if (R.n_dead > 0) {
-      NestedBufs& B = ctx->nested_bufs->b;
-      int rc = hip_check(ctx, copy_d2h_large(B, pts, B.dead_x.p, (size_t)(R.n_dead * D) * 8, ctx->stream),
-                         "copy dead points");
-      if (rc) return rc;
-    }
-    std::copy(R.pts.begin(), R.pts.end(), pts + R.n_dead * D);
+    NestedBufs& B = ctx->nested_bufs->b;
+    int rc = hip_check(ctx, copy_d2h_large(B, pts, B.dead_x.p, (size_t)(R.n_total * R.ndim) * 8, ctx->stream),
+                       "copy points");
+    if (rc) return rc;
   }
   const auto t1 = std::chrono::steady_clock::now();
   {

@@ -497,6 +497,9 @@ hipError_t launch_sort_keys(double* ll, long long* tie, int* slot, double* tll, 
 hipError_t launch_merge_new(const NestArgs& a, double* out_ll, long long* out_tie, int* out_slot,
                             const double* new_ll, const long long* new_tie, const int* new_slot,
                             hipStream_t st);
+// the final live rows in key order behind the dead rows
+hipError_t launch_gather_live(const double* x, const double* ll, const double* lp, const int* slot, int64_t n,
+                              int D, double* ox, double* oll, double* olp, hipStream_t st);
 hipError_t launch_check_sorted(const double* ll, const long long* tie, int64_t n, long long gen,
                                long long* out, hipStream_t st);
 // retire the k lowest; the last workgroup also folds the generation into the running estimate

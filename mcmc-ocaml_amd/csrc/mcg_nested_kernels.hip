@@ -572,4 +572,28 @@ hipError_t launch_check_sorted(const double* ll, const long long* tie, int64_t n
   return hipGetLastError();
 }
 
+
+// the final live rows in key order (slot[j] of the sorted keys), written behind the dead rows
+__global__ void __launch_bounds__(256) gather_live_kernel(const double* x, const double* ll, const double* lp,
+                                                          const int* slot, int64_t n, int D, double* ox,
+                                                          double* oll, double* olp) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n * D) return;
+  const int64_t j = g / D;
+  const int d = (int)(g - j * D);
+  const int s = slot[j];
+  ox[g] = x[(int64_t)s * D + d];
+  if (d == 0) {
+    oll[j] = ll[s];
+    olp[j] = lp[s];
+  }
+}
+
+hipError_t launch_gather_live(const double* x, const double* ll, const double* lp, const int* slot, int64_t n,
+                              int D, double* ox, double* oll, double* olp, hipStream_t s) {
+  hipLaunchKernelGGL(gather_live_kernel, dim3((unsigned)((n * D + 255) / 256)), dim3(256), 0, s, x, ll, lp, slot,
+                     n, D, ox, oll, olp);
+  return hipGetLastError();
+}
+
 }  // namespace mcg

@@ -34,10 +34,10 @@ struct KdState {
 };
 
 struct NestedState {
-  // last run: ll, lp, wts of every point (dead in retirement order, then live ascending); pts
-  // holds the final live rows only (the dead rows stay in the device dead buffer)
-  std::vector<double> pts, ll, lp, wts;
-  int64_t n_total = 0, n_dead = 0, n_gen = 0, nlive = 0;
+  // last run: ll, lp, wts of every point (dead in retirement order, then live ascending); the
+  // rows of every point stay in the device dead buffer (the live rows gathered behind the dead)
+  std::vector<double> ll, lp, wts;
+  int64_t n_total = 0, n_dead = 0, n_gen = 0, nlive = 0, ndim = 0;
   double log_ev = 0.0, log_dev = 0.0;
 };
 

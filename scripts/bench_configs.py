@@ -103,7 +103,9 @@ def c3(args):
     # args.reps timed runs in one context (the same seed: identical runs; the first also pays the
     # buffer allocations), then one run with per-walk HIP events for the roofline
     walls = []
+    out = None
     for _ in range(max(1, args.reps)):
+        out = None              # the previous run's arrays are freed outside the timed call (~25 ms)
         t0 = time.perf_counter()
         out = nested.nested_evidence(lik, pri, epsrel=0.01, nmcmc=nmcmc, nlive=nlive,
                                      mode_hopping_frac=0.1, k=k, ctx=ctx)
