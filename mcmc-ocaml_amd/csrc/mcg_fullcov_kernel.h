@@ -61,10 +61,11 @@ __device__ __forceinline__ void transpose_quadrants(double* v) {
   swap16(v[2], v[3]);
 }
 
-template <int D>
 #ifndef MCG_FC_MIN_WAVES
 #define MCG_FC_MIN_WAVES 2   // occupancy 2 with a few spills beats occupancy 1 (+50%, C5)
 #endif
+// UNI: one proposal scale and one box for every dim (MhArgs::uni): scalars, no per-step loads
+template <int D, bool UNI>
 __global__ void __launch_bounds__(256, MCG_FC_MIN_WAVES) mh_fullcov_kernel(const MhArgs a) {
   using F = FcLayout<D>;
   constexpr int NL = F::NKB;
@@ -168,9 +169,12 @@ __global__ void __launch_bounds__(256, MCG_FC_MIN_WAVES) mh_fullcov_kernel(const
   for (int64_t t = 0; t < a.nsteps; ++t) {
     const uint64_t T = a.step_base + (uint64_t)t;
     const uint32_t tlo = (uint32_t)T, thi = (uint32_t)(T >> 32);
-    const double* qlik = a.lik;
-    const double* qpri = a.pri;
-    const double* qprop = a.prop;
+    // model constants through global (not flat) pointers: a flat load counts against the LDS
+    // counter too, so every wait for one would also drain the table gathers and U fragments
+    typedef const __attribute__((address_space(1))) double gdouble;
+    gdouble* qlik = (gdouble*)a.lik;
+    gdouble* qpri = (gdouble*)a.pri;
+    gdouble* qprop = (gdouble*)a.prop;
     asm volatile("" : "+s"(qlik), "+s"(qpri), "+s"(qprop));
     // ---- proposal: y = x + s z (mcmc.ml:41); calls 4m + q, transposed to the lane's dims ----
     int inb = 1;
@@ -188,9 +192,9 @@ __global__ void __launch_bounds__(256, MCG_FC_MIN_WAVES) mh_fullcov_kernel(const
       for (int k2 = 0; k2 < 4; ++k2) {
         const int kb = 4 * m + k2;
         const int d = dim(kb);
-        const double yv = fma(qprop[d], v[k2], x[kb]);
+        const double yv = fma(UNI ? a.uni_s : qprop[d], v[k2], x[kb]);
         y[kb] = yv;
-        inb &= (int)(yv >= qpri[d]) & (int)(yv <= qpri[D + d]);
+        inb &= (int)(yv >= (UNI ? a.uni_lo : qpri[d])) & (int)(yv <= (UNI ? a.uni_hi : qpri[D + d]));
       }
     }
     // ---- log-likelihood: e = U (y - mu) on the matrix cores, S = sum e_i^2 ----
@@ -275,7 +279,8 @@ __global__ void __launch_bounds__(256, MCG_FC_MIN_WAVES) mh_fullcov_kernel(const
 template <int D>
 hipError_t launch_mh_fullcov(const MhArgs& a, int64_t nthreads, hipStream_t s) {
   const int64_t grid = (nthreads + 255) / 256;          // nthreads = 4 N: 64 chains per block
-  hipLaunchKernelGGL((mh_fullcov_kernel<D>), dim3((unsigned)grid), dim3(256), 0, s, a);
+  if (a.uni) hipLaunchKernelGGL((mh_fullcov_kernel<D, true>), dim3((unsigned)grid), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((mh_fullcov_kernel<D, false>), dim3((unsigned)grid), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

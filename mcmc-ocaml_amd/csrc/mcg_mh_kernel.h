@@ -460,10 +460,16 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
     double lf = 0.0, lb = 0.0, lqy = 0.0;
     // Re-read the (tiny, cache-resident) model constants every step: opaque pointers stop the
     // compiler from hoisting D*5 doubles into registers, which would cap occupancy.
-    const double* qlik = a.lik;
-    const double* qpri = a.pri;
-    const double* qprop = a.prop;
-    asm volatile("" : "+s"(qlik), "+s"(qpri), "+s"(qprop));
+    // They are global-memory pointers (address space 1) through the asm: an opaque generic
+    // pointer would make every constant a flat load, which also counts against the LDS counter.
+    typedef const __attribute__((address_space(1))) double gconst;
+    gconst* glik = (gconst*)a.lik;
+    gconst* gpri = (gconst*)a.pri;
+    gconst* gprop = (gconst*)a.prop;
+    asm volatile("" : "+s"(glik), "+s"(gpri), "+s"(gprop));
+    const double* qlik = (const double*)glik;
+    const double* qpri = (const double*)gpri;
+    const double* qprop = (const double*)gprop;
     double lly, lpy;
     if constexpr (kSeparable) {
       // fused: per Philox call -> 4 normals -> 4 proposed coordinates -> their terms of the

@@ -232,6 +232,8 @@ void mcg_ctx_destroy(mcg_ctx* ctx) {
   (void)hipEventDestroy(ctx->ev1);
   (void)hipEventDestroy(ctx->inv_ev[0]);
   (void)hipEventDestroy(ctx->inv_ev[1]);
+  for (double* h : ctx->inv_host)
+    if (h) (void)hipHostFree(h);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -624,13 +626,22 @@ int mcg_run(mcg_ctx* ctx, const mcg_run_opts* o) {
   {
     const int slot = ctx->inv_slot;
     ctx->inv_slot ^= 1;
-    std::vector<double>& ih = ctx->inv_host[slot];
     if ((rc = hip_check(ctx, hipEventSynchronize(ctx->inv_ev[slot]), "inv wait"))) return rc;
-    ih.resize((size_t)std::max<int64_t>(n_rec, 1));
-    for (int64_t q = 0; q < n_rec; ++q) ih[(size_t)q] = 1.0 / (double)(rec_base + q + 1);
-    if ((rc = hip_check(ctx, ctx->d_inv[slot].ensure(ih.size() * 8), "alloc inv"))) return rc;
-    if ((rc = hip_check(ctx, hipMemcpyAsync(ctx->d_inv[slot].p, ih.data(), ih.size() * 8,
-                                            hipMemcpyHostToDevice, ctx->stream), "copy inv"))) return rc;
+    const int64_t len = std::max<int64_t>(n_rec, 1);
+    if (len > ctx->inv_cap[slot]) {
+      if (ctx->inv_host[slot]) (void)hipHostFree(ctx->inv_host[slot]);
+      ctx->inv_host[slot] = nullptr;
+      ctx->inv_cap[slot] = 0;
+      const int64_t cap = std::max<int64_t>(len, 4096);
+      if ((rc = hip_check(ctx, hipHostMalloc((void**)&ctx->inv_host[slot], cap * 8, 0), "alloc inv staging"))) return rc;
+      ctx->inv_cap[slot] = cap;
+    }
+    double* ih = ctx->inv_host[slot];
+    ih[0] = 0.0;
+    for (int64_t q = 0; q < n_rec; ++q) ih[q] = 1.0 / (double)(rec_base + q + 1);
+    if ((rc = hip_check(ctx, ctx->d_inv[slot].ensure(len * 8), "alloc inv"))) return rc;
+    if ((rc = hip_check(ctx, hipMemcpyAsync(ctx->d_inv[slot].p, ih, len * 8, hipMemcpyHostToDevice,
+                                            ctx->stream), "copy inv"))) return rc;
     a.inv_n = (const double*)ctx->d_inv[slot].p;
     a.next_r0 = rec_base;
     ctx->inv_cur = slot;

@@ -74,7 +74,8 @@ struct mcg_ctx {
   mcg::DevBuf d_inv[2];                  // Welford 1/(R+1) tables, double-buffered per launch
   hipEvent_t inv_ev[2] = {nullptr, nullptr};
   int inv_slot = 0, inv_cur = 0;
-  std::vector<double> inv_host[2];
+  double* inv_host[2] = {nullptr, nullptr};  // pinned staging of the tables (an async copy from
+  int64_t inv_cap[2] = {0, 0};                 //   pageable memory would stall the launch queue)
   bool rec_x_valid = false, rec_llp_valid = false, last_record_accept = false;
   // reversible jump (mcg_rj.cpp)
   bool rj_active = false;

@@ -210,7 +210,7 @@ def main():
     ap.add_argument("--nlive", type=int, default=131072)
     ap.add_argument("--k", type=int, default=4096)
     ap.add_argument("--nmcmc", type=int, default=100)
-    ap.add_argument("--launches", type=int, default=20)
+    ap.add_argument("--launches", type=int, default=100, help="C4/C5: timed launches of 100 sweeps")
     ap.add_argument("--reps", type=int, default=3, help="C3: timed nested runs (median reported)")
     ap.add_argument("--c5-chains", type=int, default=131072)
     args = ap.parse_args()
