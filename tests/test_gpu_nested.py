@@ -2,10 +2,12 @@
 parity with the oracle for k = 1 (the reference algorithm) and k > 1 (batched retirement), and
 the reference's own statistical tests (test/nested_test.ml) on the GPU path."""
 import math
+import os
 
 import numpy as np
 import pytest
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.fixture(scope="module")
@@ -208,3 +210,22 @@ def test_nested_rank_count_sort_ties_and_partial_runs(oracle, T):
     assert_nested_same(g, o)
     u, c = np.unique(g.ll[: 1000 * 12], return_counts=True)
     assert c.max() > 1                                  # the generations did contain tied keys
+
+
+@pytest.mark.gpu
+def test_nested_runs_beside_another_process_equal_solo_runs():
+    """Two processes sharing the GPU, each with a busy MH context, each running the bench's D=32
+    nested replica: every run must equal the same run made alone, bit for bit, with sorted ll.
+    (The stop test once ran inside the merge kernel; a merge workgroup that started after it set
+    the flag skipped its share of the stopping generation, which only a shared GPU exposed.)"""
+    import subprocess
+    import sys
+    probe = os.path.join(ROOT, "scripts", "probes", "concurrent_nested.py")
+    env = dict(os.environ, WITH_MH="1")
+    out = subprocess.run([sys.executable, probe], env=env, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("proc")]
+    solo = {l.split()[3]: l.split("log Z")[1] for l in lines[:2]}
+    conc = {l.split()[3]: l.split("log Z")[1] for l in lines[2:]}
+    assert len(solo) == 2 and solo == conc, out.stdout
+    assert all("sorted True" in l for l in lines), out.stdout
