@@ -47,7 +47,7 @@ struct KeyBuf {
 };
 
 struct NestedBufs {
-  DevBuf x, ll, lp, nx, nll, nlp, tv, prefix, qadd, st, dead_x, dead_ll, dead_lp, rank, sync, trace, chk;
+  DevBuf x, ll, lp, nx, nll, nlp, tv, prefix, qadd, st, dead_x, dead_ll, dead_lp, rank, sync, trace, chk, rt_ix, rt_sc;
   KeyBuf keys[2], newk, newk_tmp;
   int64_t dead_cap = 0;
   // pinned staging of two in-flight batches' dead (ll, lp) and their completion events
@@ -282,6 +282,15 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   a.newk_tie = B.newk.t();
   a.newk_slot = B.newk.s();
   a.rank = (int*)B.rank.p;
+  // the walkers' draws of a generation in a table the previous merge fills (when it fits)
+  a.rt_ix = nullptr;
+  a.rt_sc = nullptr;
+  if (2 * k * nmcmc * 24 <= ((int64_t)512 << 20) && std::getenv("MCG_NESTED_NO_TABLE") == nullptr) {
+    HC(B.rt_ix.ensure(2 * k * nmcmc * 8), "alloc draw table");
+    HC(B.rt_sc.ensure(2 * k * nmcmc * 16), "alloc draw table");
+    a.rt_ix = (unsigned long long*)B.rt_ix.p;
+    a.rt_sc = (double2*)B.rt_sc.p;
+  }
   a.sync = (uint32_t*)B.sync.p;
   a.tv = (double*)B.tv.p;
   a.prefix = (const double*)B.prefix.p;
@@ -311,6 +320,7 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   const int base = in_tmp ? 1 : 0;                   // generation g reads keys[(base + g) % 2]
   HC(launch_key_sample(B.keys[base].l(), B.keys[base].t(), n, B.keys[base].sl(), B.keys[base].st(), s),
      "sample live keys");
+  HC(launch_walk_draws(a, 0, s), "first draws");
 
   // Batches of generations, pipelined: while the GPU runs batch b + 1, the host appends batch b's
   // dead ll / lp (copied into pinned staging behind b's kernels) and folds them into the

@@ -66,6 +66,11 @@ struct NestArgs {
   int* rank;                // [k] rank of new key j among the generation's new keys (k <= 4096)
   uint32_t* sync;           // [2][kSyncUse] hand-off counters: retire -> estimate, rank count -> scatter
   unsigned long long* trace;  // MCG_NEST_TRACE builds: per-workgroup phase stamps of one generation
+  // the walkers' draws of a generation, [2][nmcmc][k] (null: the walk draws them itself): DE
+  // indices i | j << 32 and (DE scale, log accept uniform).  The walk of generation g reads half
+  // g & 1 while its spare waves fill the other half for generation g + 1.
+  unsigned long long* rt_ix;
+  double2* rt_sc;
   double* tv;               // ll + log dv of this generation's dead points (padded pow2)
   const double* prefix;     // [k+1] sum_{j'<j} log1p(-1/(n-j'))
   const double* qadd;       // [k] 1/(n-j) (nested.ml:140 quirk) or log(1/(n-j))
@@ -96,6 +101,44 @@ constexpr int kNestPrefetch = MCG_NEST_PREFETCH;    // DE steps whose partner ro
 #define MCG_NEST_WALK_BLOCK 64
 #endif
 constexpr int kNestWalkBlock = MCG_NEST_WALK_BLOCK;
+
+// The random numbers of walker step s (draw_new_live_point, nested.ml:50-74): the DE pair i != j
+// (pick_samples, mcmc.ml:199-203), the DE scale (1 with probability mode_hop, else
+// N(0, 2.38/sqrt(2D)), mcmc.ml:209-213) and log u of the accept test (mcmc.ml:49).
+__device__ __forceinline__ void walk_draw(const NestArgs& a, uint32_t wid, uint32_t s,
+                                          const double2* nt, const double2* lt,
+                                          unsigned long long& ix, double2& sc) {
+  const Rng rng{a.k0, a.k1};
+  const uint32_t n = (uint32_t)a.n;
+  const u32x4 rI = rng(wid, s, CALL_DE_IDX, TAG_NEST_WALK, 0u);
+  const u32x4 rS = rng(wid, s, CALL_DE_SCALE, TAG_NEST_WALK, 0u);
+  const u32x4 rA = rng(wid, s, CALL_ACCEPT, TAG_NEST_WALK, 0u);
+  const uint32_t i = randint(rI.x, rI.y, n);
+  const uint32_t jj = randint(rI.z, rI.w, n - 1);
+  const uint32_t j = jj + (jj >= i ? 1u : 0u);
+  ix = (unsigned long long)i | ((unsigned long long)j << 32);
+  sc.x = (a.mode_hop != 0.0 && u53(rS.x, rS.y) < a.mode_hop) ? 1.0 : a.sigma_de * pnormal(rS.z, nt);
+  sc.y = plog(u53(rA.x, rA.y), lt);
+}
+
+// the draws of every walker step of the generation that starts at replacement mrep, entries
+// [e0, k nmcmc) with stride `stride` (layout [step][walker])
+// Generation g = mrep / k uses half g & 1 of the double-buffered table.
+__device__ __forceinline__ int64_t walk_tab_base(const NestArgs& a, int64_t mrep) {
+  return ((mrep / a.k) & 1) * a.k * a.nmcmc;
+}
+__device__ __forceinline__ void walk_draws_fill(const NestArgs& a, int64_t mrep, int64_t e0, int64_t stride,
+                                                const double2* lt) {
+  const int64_t tot = a.k * a.nmcmc, base = walk_tab_base(a, mrep);
+  for (int64_t e = e0; e < tot; e += stride) {
+    const int64_t s = e / a.k, w = e - s * a.k;
+    unsigned long long ix;
+    double2 sc;
+    walk_draw(a, (uint32_t)(mrep + w), (uint32_t)s, kNrmTab, lt, ix, sc);
+    a.rt_ix[base + e] = ix;
+    a.rt_sc[base + e] = sc;
+  }
+}
 
 // The log-target constants of one walker lane (its dims of mu/sigma or the shell centre, the box
 // bounds), loaded into registers once per launch.  Loaded per step through the parameter
@@ -244,7 +287,7 @@ struct WalkTarget {
 // scale, accept decision and start point agree without communication; the log-target is the
 // canonical sum reduced across the P lanes (reduce_canon).  The DE partner rows of step s + 1
 // depend only on the RNG, so they are loaded while step s computes (one step of prefetch).
-template <int D, int LIK, int P>
+template <int D, int LIK, int P, bool TAB>
 __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   using Lay = Layout<D, P>;
   constexpr int NL = Lay::NL;
@@ -266,7 +309,16 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
       return;
     }
   }
-  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if constexpr (TAB) {
+    // waves 1-3 of the workgroup (one SIMD each; the walkers are wave 0) draw the next
+    // generation's table and leave
+    if (threadIdx.x >= 64) {
+      const int64_t nf = blockDim.x - 64;
+      walk_draws_fill(a, a.mrep + a.k, (int64_t)blockIdx.x * nf + (threadIdx.x - 64), (int64_t)gridDim.x * nf, s_lt);
+      return;
+    }
+  }
+  const int64_t tid = (int64_t)blockIdx.x * (TAB ? 64 : blockDim.x) + threadIdx.x;
   const int sub = (int)(tid & (P - 1));
   const int64_t w = tid / P;
   const bool active = w < a.k;
@@ -338,13 +390,33 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
     }
   };
   GroupRng gcur, gnext;
-  group_issue(0, gcur);   // before the ring's first rows: its gather is then never the newest load
+  if constexpr (!TAB) group_issue(0, gcur);   // before the ring's first rows: its gather is then never the newest load
+  // TAB: the generation's draws come from the table the previous merge filled (rt_ix, rt_sc),
+  // loaded one group ahead like the rows: (scale, log u) of steps s0 + u and the refill indices
+  // of steps s0 + PD + u
+  const int64_t tbase = TAB ? walk_tab_base(a, a.mrep) : 0;
+  auto tab_at = [&](int64_t st) { return tbase + (st < a.nmcmc ? st : a.nmcmc - 1) * a.k + wc; };
+  unsigned long long tix_cur[PD], tix_next[PD];
+  double2 tsc_cur[PD], tsc_next[PD];
+  if constexpr (TAB) {
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+      tsc_cur[u] = a.rt_sc[tab_at(u)];
+      tix_cur[u] = a.rt_ix[tab_at(PD + u)];
+    }
+  }
   // partner rows of steps s .. s + PD - 1 in flight: ring slot u holds step s0 + u
   double bi[PD][NL], bj[PD][NL];
 #pragma unroll
   for (int u = 0; u < PD; ++u) {
     uint32_t i0, j0;
-    pick(u, i0, j0);
+    if constexpr (TAB) {
+      const unsigned long long ix = a.rt_ix[tab_at(u)];
+      i0 = (uint32_t)ix;
+      j0 = (uint32_t)(ix >> 32);
+    } else {
+      pick(u, i0, j0);
+    }
     load_row(bi[u], i0);
     load_row(bj[u], j0);
   }
@@ -353,7 +425,20 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   for (int64_t s0 = 0; s0 < a.nmcmc; s0 += PD) {
     double dsc_g[PD], lu_g[PD];
     uint32_t ip_g[PD], jp_g[PD];
-    if constexpr (P == 4 && PD % 4 == 0) {
+    if constexpr (TAB) {
+#pragma unroll
+      for (int u = 0; u < PD; ++u) {
+        dsc_g[u] = tsc_cur[u].x;
+        lu_g[u] = tsc_cur[u].y;
+        ip_g[u] = (uint32_t)tix_cur[u];
+        jp_g[u] = (uint32_t)(tix_cur[u] >> 32);
+      }
+#pragma unroll
+      for (int u = 0; u < PD; ++u) {                  // the next group's draws go out first
+        tsc_next[u] = a.rt_sc[tab_at(s0 + PD + u)];
+        tix_next[u] = a.rt_ix[tab_at(s0 + 2 * PD + u)];
+      }
+    } else if constexpr (P == 4 && PD % 4 == 0) {
       // finish this group's draws and hand step u's values from lane u % 4 to the quad (DPP)
 #pragma unroll
       for (int h = 0; h < PD / 4; ++h) {
@@ -426,7 +511,15 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
         cur_l = ml;
       }
     }
-    if constexpr (P == 4 && PD % 4 == 0) gcur = gnext;
+    if constexpr (TAB) {
+#pragma unroll
+      for (int u = 0; u < PD; ++u) {
+        tsc_cur[u] = tsc_next[u];
+        tix_cur[u] = tix_next[u];
+      }
+    } else if constexpr (P == 4 && PD % 4 == 0) {
+      gcur = gnext;
+    }
   }
   const double nl = tgt.lik(cur, sub, a.m);
   const double np = tgt.prior(cur, sub, a.m);
@@ -479,7 +572,9 @@ hipError_t launch_nest_walk(const NestArgs& a, hipStream_t st) {
   // over all CUs (their LDS tables, L1 and scalar units) instead of packing four per CU
   const int block = kNestWalkBlock;
   const int64_t grid = (a.k * P + block - 1) / block;
-  hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P>), dim3((unsigned)grid), dim3(block), 0, st, a);
+  // with the draw table: the same walker waves, each with three table-filling waves beside it
+  if (a.rt_ix) hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true>), dim3((unsigned)((a.k * P + 63) / 64)), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, false>), dim3((unsigned)grid), dim3(block), 0, st, a);
   return hipGetLastError();
 }
 
@@ -500,6 +595,8 @@ hipError_t launch_merge_new(const NestArgs& a, double* out_ll, long long* out_ti
 // the final live rows in key order behind the dead rows
 hipError_t launch_gather_live(const double* x, const double* ll, const double* lp, const int* slot, int64_t n,
                               int D, double* ox, double* oll, double* olp, hipStream_t st);
+// the walkers' draws of the generation starting at replacement mrep (the first generation's table)
+hipError_t launch_walk_draws(const NestArgs& a, int64_t mrep, hipStream_t st);
 hipError_t launch_check_sorted(const double* ll, const long long* tie, int64_t n, long long gen,
                                long long* out, hipStream_t st);
 // retire the k lowest; the last workgroup also folds the generation into the running estimate

@@ -5,6 +5,8 @@
 // and merge produce.  tie: initial points get their slot index, the m-th replacement gets -m,
 // which reproduces the reference's tie order (stable initial sort, nested.ml:132; a new point is
 // inserted before equal likelihoods, the strict > of nested.ml:36).
+#include <algorithm>
+
 #include "mcg_nested_kernel.h"
 
 namespace mcg {
@@ -593,6 +595,19 @@ hipError_t launch_gather_live(const double* x, const double* ll, const double* l
                               int D, double* ox, double* oll, double* olp, hipStream_t s) {
   hipLaunchKernelGGL(gather_live_kernel, dim3((unsigned)((n * D + 255) / 256)), dim3(256), 0, s, x, ll, lp, slot,
                      n, D, ox, oll, olp);
+  return hipGetLastError();
+}
+
+
+__global__ void __launch_bounds__(256) walk_draws_kernel(const NestArgs a, int64_t mrep) {
+  walk_draws_fill(a, mrep, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x, kLogTab);
+}
+
+hipError_t launch_walk_draws(const NestArgs& a, int64_t mrep, hipStream_t s) {
+  if (!a.rt_ix) return hipSuccess;
+  const int64_t tot = a.k * a.nmcmc;
+  const unsigned grid = (unsigned)std::min<int64_t>((tot + 255) / 256, 4096);
+  hipLaunchKernelGGL(walk_draws_kernel, dim3(grid), dim3(256), 0, s, a, mrep);
   return hipGetLastError();
 }
 
