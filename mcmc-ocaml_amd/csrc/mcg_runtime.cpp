@@ -206,8 +206,7 @@ int mcg_ctx_create(mcg_ctx** out, const mcg_opts* opts) {
   mcg_ctx* ctx = new mcg_ctx();
   ctx->opts = o;
   if (hipSetDevice(o.device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
-      hipEventCreate(&ctx->inv_ev[0]) != hipSuccess || hipEventCreate(&ctx->inv_ev[1]) != hipSuccess) {
+      hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) {
     delete ctx;
     return MCG_EDEVICE;
   }
@@ -230,10 +229,6 @@ void mcg_ctx_destroy(mcg_ctx* ctx) {
   for (hipEvent_t e : ctx->ev_free) (void)hipEventDestroy(e);
   (void)hipEventDestroy(ctx->ev0);
   (void)hipEventDestroy(ctx->ev1);
-  (void)hipEventDestroy(ctx->inv_ev[0]);
-  (void)hipEventDestroy(ctx->inv_ev[1]);
-  for (double* h : ctx->inv_host)
-    if (h) (void)hipHostFree(h);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -620,31 +615,23 @@ int mcg_run(mcg_ctx* ctx, const mcg_run_opts* o) {
   a.nskip = o->nskip;
   a.rec_base = rec_base;
   a.rec_end = rec_base + n_rec;
-  // Welford weights 1/(R+1) of every record of this run (IEEE division on the host, so the
-  // kernel needs no per-step division).  Two buffers alternate between runs; an event guards the
-  // reuse of the one a still-running previous run may read.
+  // Welford weights 1/(R+1) of the records (IEEE division on the host, so the kernel needs no
+  // per-step division): one device table inv[R] for every absolute record index R, grown rarely.
+  // (A per-run upload put a copy between consecutive MH kernels: two engine hand-offs per run.)
   {
-    const int slot = ctx->inv_slot;
-    ctx->inv_slot ^= 1;
-    if ((rc = hip_check(ctx, hipEventSynchronize(ctx->inv_ev[slot]), "inv wait"))) return rc;
-    const int64_t len = std::max<int64_t>(n_rec, 1);
-    if (len > ctx->inv_cap[slot]) {
-      if (ctx->inv_host[slot]) (void)hipHostFree(ctx->inv_host[slot]);
-      ctx->inv_host[slot] = nullptr;
-      ctx->inv_cap[slot] = 0;
-      const int64_t cap = std::max<int64_t>(len, 4096);
-      if ((rc = hip_check(ctx, hipHostMalloc((void**)&ctx->inv_host[slot], cap * 8, 0), "alloc inv staging"))) return rc;
-      ctx->inv_cap[slot] = cap;
+    const int64_t need = rec_base + std::max<int64_t>(n_rec, 1);
+    if (need > ctx->inv_cap) {
+      const int64_t cap = std::max<int64_t>(need, std::max<int64_t>(2 * ctx->inv_cap, (int64_t)1 << 20));
+      std::vector<double> ih((size_t)cap);
+      for (int64_t q = 0; q < cap; ++q) ih[(size_t)q] = 1.0 / (double)(q + 1);
+      // the running kernels may read the old table: let them finish before it is replaced
+      if ((rc = hip_check(ctx, hipStreamSynchronize(ctx->stream), "inv sync"))) return rc;
+      if ((rc = hip_check(ctx, ctx->d_invtab.ensure(cap * 8), "alloc inv"))) return rc;
+      if ((rc = hip_check(ctx, hipMemcpy(ctx->d_invtab.p, ih.data(), cap * 8, hipMemcpyHostToDevice), "copy inv"))) return rc;
+      ctx->inv_cap = cap;
     }
-    double* ih = ctx->inv_host[slot];
-    ih[0] = 0.0;
-    for (int64_t q = 0; q < n_rec; ++q) ih[q] = 1.0 / (double)(rec_base + q + 1);
-    if ((rc = hip_check(ctx, ctx->d_inv[slot].ensure(len * 8), "alloc inv"))) return rc;
-    if ((rc = hip_check(ctx, hipMemcpyAsync(ctx->d_inv[slot].p, ih, len * 8, hipMemcpyHostToDevice,
-                                            ctx->stream), "copy inv"))) return rc;
-    a.inv_n = (const double*)ctx->d_inv[slot].p;
-    a.next_r0 = rec_base;
-    ctx->inv_cur = slot;
+    a.inv_n = (const double*)ctx->d_invtab.p;
+    a.next_r0 = 0;
   }
   int64_t spl = ctx->opts.steps_per_launch;
   if (const char* env = std::getenv("MCG_STEPS_PER_LAUNCH")) spl = std::atoll(env);
@@ -680,7 +667,6 @@ int mcg_run(mcg_ctx* ctx, const mcg_run_opts* o) {
     t0 += n;
     first = false;
   } while (t0 < nsteps);
-  (void)hipEventRecord(ctx->inv_ev[ctx->inv_cur], ctx->stream);
   ctx->steps_done += (uint64_t)nsteps;
   ctx->nsteps_total += nsteps;
   ctx->last_nsteps = nsteps;

@@ -71,11 +71,8 @@ struct mcg_ctx {
   // records and statistics
   mcg::DevBuf d_rec_x, d_rec_ll, d_rec_lp, d_bits, d_mean, d_m2, d_hm_m, d_hm_s, d_tiles;
   int64_t nrec_total = 0, rec_stored = 0;
-  mcg::DevBuf d_inv[2];                  // Welford 1/(R+1) tables, double-buffered per launch
-  hipEvent_t inv_ev[2] = {nullptr, nullptr};
-  int inv_slot = 0, inv_cur = 0;
-  double* inv_host[2] = {nullptr, nullptr};  // pinned staging of the tables (an async copy from
-  int64_t inv_cap[2] = {0, 0};                 //   pageable memory would stall the launch queue)
+  mcg::DevBuf d_invtab;                  // Welford weights 1/(R+1), R = absolute record index
+  int64_t inv_cap = 0;
   bool rec_x_valid = false, rec_llp_valid = false, last_record_accept = false;
   // reversible jump (mcg_rj.cpp)
   bool rj_active = false;
