@@ -685,9 +685,32 @@ int mcg_nested_merge(int32_t nruns, const int64_t* n_total, const int64_t* nlive
     const int64_t ndead = n_total[r] - nlive[r];
     return i < ndead ? nlive[r] - i % k[r] : nlive[r] - (i - ndead);
   };
-  for (int64_t p = 0; p < n; ++p) order[p] = p;
   // ascending ll; ties by concatenation index (= run, then position in the run)
-  std::stable_sort(order, order + n, [&](int64_t a, int64_t b) { return ll[a] < ll[b]; });
+  bool runs_sorted = true;
+  for (int r = 0; r < nruns && runs_sorted; ++r)
+    for (int64_t i = base[(size_t)r] + 1; i < base[(size_t)r + 1] && runs_sorted; ++i) runs_sorted = !(ll[i] < ll[i - 1]);
+  if (runs_sorted && nruns > 1) {
+    // nested outputs are already ascending: merge the runs pairwise (std::merge takes the first
+    // range on ties, so the concatenation order of ties is kept) instead of sorting n indices
+    std::vector<std::pair<double, int64_t>> a((size_t)n), b((size_t)n);
+    for (int64_t p = 0; p < n; ++p) a[(size_t)p] = {ll[p], p};
+    std::vector<int64_t> seg(base.begin(), base.end());
+    auto less = [](const std::pair<double, int64_t>& x, const std::pair<double, int64_t>& y) { return x.first < y.first; };
+    while (seg.size() > 2) {
+      std::vector<int64_t> nseg{0};
+      for (size_t r = 0; r + 1 < seg.size(); r += 2) {
+        const int64_t lo = seg[r], mid = seg[r + 1], hi = r + 2 < seg.size() ? seg[r + 2] : seg[r + 1];
+        std::merge(a.begin() + lo, a.begin() + mid, a.begin() + mid, a.begin() + hi, b.begin() + lo, less);
+        nseg.push_back(hi);
+      }
+      a.swap(b);
+      seg.swap(nseg);
+    }
+    for (int64_t p = 0; p < n; ++p) order[p] = a[(size_t)p].second;
+  } else {
+    for (int64_t p = 0; p < n; ++p) order[p] = p;
+    std::stable_sort(order, order + n, [&](int64_t x, int64_t y) { return ll[x] < ll[y]; });
+  }
   // pos[r] = first index of run r with ll >= the current level; ll is nondecreasing within a run
   std::vector<int64_t> pos((size_t)nruns, 0);
   const double log_half = -0.69314718055994530942;
