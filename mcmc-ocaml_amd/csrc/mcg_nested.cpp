@@ -228,6 +228,8 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   const int64_t nmcmc = opts->nmcmc >= 0 ? opts->nmcmc : 1000;
   const double epsrel = opts->epsrel > 0 ? opts->epsrel : 0.01;
   if (n < 2 || k >= n || n > 0x7FFFFFFF) return set_error(ctx, MCG_EINVAL, "need 2 <= nlive, 1 <= k < nlive");
+  // the generation's estimate tree holds 16 retirements per thread of one 1024-thread workgroup
+  if (k > 16384) return set_error(ctx, MCG_EINVAL, "k (points retired per generation) must be <= 16384");
   const int64_t max_dead = opts->max_dead > 0 ? opts->max_dead : 1000 * n;
   nest_walk_fn walk = find_nest_walk(D, ctx->lik_kind);
   nest_init_fn init = find_nest_init(D, ctx->lik_kind);
@@ -282,6 +284,7 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   a.newk_tie = B.newk.t();
   a.newk_slot = B.newk.s();
   a.rank = (int*)B.rank.p;
+  a.est_in_rank = k <= 4096 ? 1 : 0;                  // the counted-rank sort path
   // the walkers' draws of a generation in a table the previous merge fills (when it fits)
   a.rt_ix = nullptr;
   a.rt_sc = nullptr;

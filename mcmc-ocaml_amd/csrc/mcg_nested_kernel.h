@@ -71,6 +71,7 @@ struct NestArgs {
   // g & 1 while its spare waves fill the other half for generation g + 1.
   unsigned long long* rt_ix;
   double2* rt_sc;
+  int32_t est_in_rank;      // the estimate is folded by an extra rank_count workgroup (k <= 4096)
   double* tv;               // ll + log dv of this generation's dead points (padded pow2)
   const double* prefix;     // [k+1] sum_{j'<j} log1p(-1/(n-j'))
   const double* qadd;       // [k] 1/(n-j) (nested.ml:140 quirk) or log(1/(n-j))

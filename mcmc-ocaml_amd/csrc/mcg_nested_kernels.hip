@@ -132,12 +132,12 @@ constexpr int kRun = 256;
 // added to by the workgroup completing its group): one counter taking every workgroup's add
 // serialises them (measured: 6 us of spread over 512 workgroups).  The workgroup completing the
 // top counter acquires once and runs the consumer part.  No workgroup waits on another.
-__device__ __forceinline__ bool last_block_done(uint32_t* sync) {
+__device__ __forceinline__ bool last_block_done(uint32_t* sync, uint32_t nblocks) {
   __shared__ int s_last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint32_t nb = gridDim.x, g = blockIdx.x % kSyncGroups;
+    const uint32_t nb = nblocks, g = blockIdx.x % kSyncGroups;
     const uint32_t gsize = (nb - g + kSyncGroups - 1) / kSyncGroups;
     const uint32_t ngroups = nb < (uint32_t)kSyncGroups ? nb : (uint32_t)kSyncGroups;
     uint32_t* gc = sync + (1 + g) * kSyncStride;
@@ -167,12 +167,103 @@ __device__ __forceinline__ void st1(T* p, T v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// est = lse(est, G) and log_vol += sum_j log1p(-1/(n-j)), where G is the log-sum of this
+// generation's terms tv[0..k): tv[0] for k = 1 (the reference's fold, nested.ml:138-141), else
+// M + log(sum exp(tv_j - M)) with M = max tv and the exps added by a fixed pairwise tree (pad to a
+// power of two with 0; i + s into i) -- the oracle's tree_lse, operation for operation.  Run by
+// the last workgroup of the retire kernel (1024 threads: up to 16,384 retirements) or by an extra
+// rank-count workgroup (256 threads: k <= 4096), after every tv[j] is stored.
+constexpr int kEstPer = 16;                          // retirements per thread of the estimate
+constexpr int kRetireBlock = 1024;
+
+template <int B>   // workgroup size; generations up to kEstPer * B retirements
+__device__ __forceinline__ void estimate_body(const NestArgs& a) {
+  __shared__ double sv[B];
+  __shared__ double s_max[B / 64];
+  __shared__ double2 s_lt[kLogTabN];                 // log table staged in LDS
+  for (int i = threadIdx.x; i < kLogTabN; i += B) s_lt[i] = kLogTab[i];
+  const int64_t k = a.k, p2 = a.tv_len;              // p2 <= kEstPer * B (checked on the host)
+  const int t = threadIdx.x;
+  // thread t holds v[t + B q]: all loads in flight together (tv was stored sc1 by the retire
+  // workgroups)
+  double e[kEstPer];
+  double m = -__builtin_inf();
+#pragma unroll
+  for (int q = 0; q < kEstPer; ++q) {
+    const int64_t i = (int64_t)q * B + t;
+    e[q] = ld1(a.tv + (i < k ? i : k - 1));
+  }
+#pragma unroll
+  for (int q = 0; q < kEstPer; ++q)
+    if ((int64_t)q * B + t < k) m = fmax(m, e[q]);
+  NT_STAMP(1, 5);
+  // M: the block max (exact in any order)
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+  if ((t & 63) == 0) s_max[t >> 6] = m;
+  __syncthreads();
+  double M = s_max[0];
+#pragma unroll
+  for (int w = 1; w < B / 64; ++w) M = fmax(M, s_max[w]);
+  NT_STAMP(1, 6);
+  const double v_first = e[0];                       // tv[0] (t == 0): the k == 1 fold
+  double x = 0.0;
+  if (k > 1 && M != -__builtin_inf()) {
+    // the same tree (v[i] += v[i + s], s = p2/2 .. 1) with its levels where the data are:
+    // s >= B pairs elements of one thread (i and i + s are both t mod B), in its registers;
+    // 512 .. 64 in LDS after one barrier; 32 .. 1 by shuffles inside wave 0
+#pragma unroll
+    for (int q = 0; q < kEstPer; ++q) e[q] = ((int64_t)q * B + t < k) ? pexp(e[q] - M) : 0.0;
+    int64_t s = p2 >> 1;
+    for (; s >= B; s >>= 1) {
+      const int d = (int)(s / B);
+#pragma unroll
+      for (int q = 0; q < kEstPer / 2; ++q)
+        if (q < d) e[q] = e[q] + e[q + d];
+    }
+    x = e[0];
+    if (s >= 64) {
+      // levels s = 512 .. 64 after one barrier: final v[i] (i < 64) combines v[i + 64 m],
+      // m < 2s/64, by the same tree (m with m + d, d = s/64 .. 1) in wave 0's registers
+      sv[t] = x;
+      __syncthreads();
+      if (t < 64) {
+        const int nm = (int)(2 * s / 64);
+        double g[B / 64];
+#pragma unroll
+        for (int q = 0; q < B / 64; ++q) g[q] = q < nm ? sv[t + 64 * q] : 0.0;
+#pragma unroll
+        for (int d = B / 128; d >= 1; d >>= 1)
+          if (d < nm)
+#pragma unroll
+            for (int q = 0; q < d; ++q) g[q] = g[q] + g[q + d];
+        x = g[0];
+      }
+      s = 32;
+    }
+    for (; s >= 1; s >>= 1) x = x + __shfl_down(x, (unsigned)s, 64);
+  }
+  NT_STAMP(1, 7);
+  if (t == 0) {
+    const double G = k == 1 ? v_first : (M == -__builtin_inf() ? M : M + plog(x, s_lt));
+    a.st->est = plse(a.st->est, G, s_lt);
+    a.st->log_vol = a.st->log_vol + a.prefix[k];
+  }
+}
+
 constexpr int kSub = 128;                            // keys of the compared-against sub-run
 
 __global__ void __launch_bounds__(256) rank_count_kernel(const NestArgs a, int nruns, double* oll,
                                                          long long* otie, int* oslot) {
   NT_STAMP(2, 0);
   if (nest_stopped(a.st)) return;                         // grid-uniform: set by an earlier launch
+  if (a.est_in_rank && blockIdx.x == gridDim.x - 1) {
+    // the extra workgroup folds the generation into the running estimate (retire wrote tv),
+    // beside the counting: off the generation's serial path
+    estimate_body<kRun>(a);
+    return;
+  }
+  const uint32_t ncount = gridDim.x - (a.est_in_rank ? 1u : 0u);
   __shared__ double sl[kSub];
   __shared__ double s_ll[kSmallSort];                // last block: keys placed at their ranks
   __shared__ short s_j[kSmallSort];
@@ -203,7 +294,7 @@ __global__ void __launch_bounds__(256) rank_count_kernel(const NestArgs a, int n
     NT_STAMP(2, 2);
     if (cnt) atomicAdd(&a.rank[p], cnt);
   }
-  const bool last = last_block_done(a.sync + kSyncUse);
+  const bool last = last_block_done(a.sync + kSyncUse, ncount);
   NT_STAMP(2, 3);
   if (!last) return;
   // the last block places every key at its rank in LDS (a random scatter from one CU is bound by
@@ -250,8 +341,8 @@ hipError_t launch_sort_new_small(const NestArgs& a, double* oll, long long* otie
                                  hipStream_t s) {
   if (a.k > kSmallSort || a.k < 1) return hipErrorInvalidValue;
   const int nruns = (int)((a.k + kRun - 1) / kRun), nsub = (int)((a.k + kSub - 1) / kSub);
-  hipLaunchKernelGGL(rank_count_kernel, dim3((unsigned)(nruns * nsub)), dim3(kRun), 0, s, a, nruns,
-                     oll, otie, oslot);
+  hipLaunchKernelGGL(rank_count_kernel, dim3((unsigned)(nruns * nsub + (a.est_in_rank ? 1 : 0))), dim3(kRun), 0, s,
+                     a, nruns, oll, otie, oslot);
   return hipGetLastError();
 }
 
@@ -401,113 +492,6 @@ hipError_t launch_merge_new(const NestArgs& a, double* out_ll, long long* out_ti
   return hipGetLastError();
 }
 
-// est = lse(est, G) and log_vol += sum_j log1p(-1/(n-j)), where G is the log-sum of this
-// generation's terms tv[0..k): tv[0] for k = 1 (the reference's fold, nested.ml:138-141), else
-// M + log(sum exp(tv_j - M)) with M = max tv and the exps added by a fixed pairwise tree (pad to a
-// power of two with 0; i + s into i) -- the oracle's tree_lse, operation for operation.  Run by
-// the last workgroup of the retire kernel (1024 threads), after every tv[j] is stored; the tree
-// runs in LDS when the padded generation fits (tv_len <= 4096), else in place in tv.
-constexpr int kEstLds = 4096;
-constexpr int kRetireBlock = 1024;
-
-__device__ __forceinline__ void estimate_body(const NestArgs& a) {
-  __shared__ double sv[kEstLds];
-  __shared__ double s_max[kRetireBlock / 64];
-  __shared__ double2 s_lt[kLogTabN];                 // log table staged in LDS
-  static_assert(kLogTabN <= kRetireBlock, "one log-table entry per thread");
-  if (threadIdx.x < kLogTabN) s_lt[threadIdx.x] = kLogTab[threadIdx.x];
-  const int64_t k = a.k, p2 = a.tv_len;
-  const bool lds = p2 <= kEstLds;
-  double* v = lds ? sv : a.tv;
-  double m = -__builtin_inf();
-  if (lds) {
-    // all loads in flight together (tv was stored sc1 by the retire workgroups)
-    constexpr int kPer = kEstLds / kRetireBlock;
-    double t[kPer];
-#pragma unroll
-    for (int e = 0; e < kPer; ++e) t[e] = ld1(a.tv + min((int64_t)(e * kRetireBlock + threadIdx.x), k - 1));
-#pragma unroll
-    for (int e = 0; e < kPer; ++e) {
-      const int64_t i = e * kRetireBlock + threadIdx.x;
-      if (i < k) m = fmax(m, t[e]);
-      if (i < p2) sv[i] = i < k ? t[e] : 0.0;
-    }
-  } else {
-    for (int64_t i = threadIdx.x; i < p2; i += blockDim.x) {
-      const double t = i < k ? ld1(a.tv + i) : 0.0;
-      if (i < k) m = fmax(m, t);
-      v[i] = t;
-    }
-  }
-  NT_STAMP(1, 5);
-  // M: the block max (exact in any order)
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
-  if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = m;
-  __syncthreads();
-  double M = s_max[0];
-#pragma unroll
-  for (int w = 1; w < kRetireBlock / 64; ++w) M = fmax(M, s_max[w]);
-  NT_STAMP(1, 6);
-  if (k > 1 && M != -__builtin_inf()) {
-    if (lds) {
-      // the same tree (v[i] += v[i + s], s = p2/2 .. 1) with its levels where the data are:
-      // s >= 1024 in the thread's registers (it holds v[t + 1024 e]), 512 .. 64 in LDS, 32 .. 1
-      // by shuffles inside wave 0
-      constexpr int kPer = kEstLds / kRetireBlock;
-      const int t = threadIdx.x;
-      double e[kPer];
-#pragma unroll
-      for (int q = 0; q < kPer; ++q) {
-        const int64_t i = q * kRetireBlock + t;
-        e[q] = i < k ? pexp(sv[i] - M) : 0.0;
-      }
-      int64_t s = p2 >> 1;
-      for (; s >= kRetireBlock; s >>= 1) {
-        const int d = (int)(s / kRetireBlock);
-#pragma unroll
-        for (int q = 0; q < kPer / 2; ++q)
-          if (q < d) e[q] = e[q] + e[q + d];
-      }
-      double x = e[0];
-      if (s >= 64) {
-        // levels s = 512 .. 64 after one barrier: final v[i] (i < 64) combines v[i + 64 m],
-        // m < 2s/64, by the same tree (m with m + d, d = s/64 .. 1) in wave 0's registers
-        __syncthreads();                             // sv is rewritten
-        sv[t] = x;
-        __syncthreads();
-        if (t < 64) {
-          const int nm = (int)(2 * s / 64);
-          double g[kRetireBlock / 64];
-#pragma unroll
-          for (int q = 0; q < kRetireBlock / 64; ++q) g[q] = q < nm ? sv[t + 64 * q] : 0.0;
-#pragma unroll
-          for (int d = kRetireBlock / 128; d >= 1; d >>= 1)
-            if (d < nm)
-#pragma unroll
-              for (int q = 0; q < d; ++q) g[q] = g[q] + g[q + d];
-          x = g[0];
-        }
-        s = 32;
-      }
-      for (; s >= 1; s >>= 1) x = x + __shfl_down(x, (unsigned)s, 64);
-      if (t == 0) v[0] = x;
-    } else {
-      for (int64_t i = threadIdx.x; i < k; i += blockDim.x) v[i] = pexp(v[i] - M);
-      __syncthreads();
-      for (int64_t s = p2 >> 1; s >= 1; s >>= 1) {
-        for (int64_t i = threadIdx.x; i < s; i += blockDim.x) v[i] = v[i] + v[i + s];
-        __syncthreads();
-      }
-    }
-  }
-  NT_STAMP(1, 7);
-  if (threadIdx.x == 0) {
-    const double G = k == 1 ? v[0] : (M == -__builtin_inf() ? M : M + plog(v[0], s_lt));
-    a.st->est = plse(a.st->est, G, s_lt);
-    a.st->log_vol = a.st->log_vol + a.prefix[k];
-  }
-}
 
 // retire the k lowest (replace_live_point, nested.ml:26-43, slot form): copy each retired row to
 // the dead buffer, put walker j's point into the freed slot, emit its key and ll + log dv.
@@ -539,11 +523,12 @@ __global__ void __launch_bounds__(kRetireBlock) retire_kernel(const NestArgs a, 
       if (a.rank) a.rank[j] = 0;
     }
   }
+  if (a.est_in_rank) return;                         // rank_count_kernel folds the estimate
   NT_STAMP(1, 2);
-  const bool last = last_block_done(a.sync);
+  const bool last = last_block_done(a.sync, gridDim.x);
   NT_STAMP(1, 3);
   if (!last) return;
-  estimate_body(a);
+  estimate_body<kRetireBlock>(a);
   NT_STAMP(1, 4);
 }
 

@@ -229,3 +229,15 @@ def test_nested_runs_beside_another_process_equal_solo_runs():
     conc = {l.split()[3]: l.split("log Z")[1] for l in lines[2:]}
     assert len(solo) == 2 and solo == conc, out.stdout
     assert all("sorted True" in l for l in lines), out.stdout
+
+
+@pytest.mark.gpu
+def test_nested_large_k_bit_exact(oracle, T):
+    """k > 4096: the new keys go through the chunked sort + merge passes, and the retire kernel's
+    last workgroup folds the estimate (instead of the extra rank-count workgroup)."""
+    D = 4
+    lik = T.gauss_shell(np.zeros(D), 1.0, 0.2)
+    pri = T.box(-2 * np.ones(D), 2 * np.ones(D))
+    g = gpu_nested(lik, pri, 13, nlive=12000, nmcmc=6, mode_hopping_frac=0.1, k=5000, max_dead=5000 * 6)
+    o = oracle_nested(oracle, lik, pri, 13, nlive=12000, nmcmc=6, mode_hop=0.1, k=5000, max_iter=5000 * 6)
+    assert_nested_same(g, o)
