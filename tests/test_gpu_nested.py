@@ -241,3 +241,19 @@ def test_nested_large_k_bit_exact(oracle, T):
     g = gpu_nested(lik, pri, 13, nlive=12000, nmcmc=6, mode_hopping_frac=0.1, k=5000, max_dead=5000 * 6)
     o = oracle_nested(oracle, lik, pri, 13, nlive=12000, nmcmc=6, mode_hop=0.1, k=5000, max_iter=5000 * 6)
     assert_nested_same(g, o)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nlive,k,what", [(20000, 16385, "16384"), (64, 64, "k < nlive"),
+                                          (1, 1, "2 <= nlive")])
+def test_nested_rejects_bad_generation_sizes(T, nlive, k, what):
+    # mcg_nested checks its sizes before any device work and reports MCG_EINVAL with a message
+    from mcmc_amd._lib import InvalidArgument
+    lik, pri = unit_square_gauss(T)
+    from mcmc_amd import Context, nested
+    ctx = Context(seed=1)
+    try:
+        with pytest.raises(InvalidArgument, match=what):
+            nested.nested_evidence(lik, pri, ctx=ctx, nlive=nlive, nmcmc=2, k=k)
+    finally:
+        ctx.close()
