@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define MCG_ABI_VERSION 1
+#define MCG_ABI_VERSION 2
 
 /* ---- status codes ---- */
 enum {
@@ -241,6 +241,9 @@ typedef struct {
   int64_t n_dead;
   int64_t n_total;        /* n_dead + nlive */
   int64_t n_gen;
+  int32_t converged;      /* 1: remaining_integral_negligable fired (nested.ml:45-48, 144);
+                             0: the max_dead cap ended the run first -- log_ev / log_dev /
+                             weights then come from an unconverged run */
 } mcg_nested_result;
 
 /* observer: called after each batch of generations with the newly retired points (batch form
@@ -309,6 +312,12 @@ int mcg_get_kernel_timing(mcg_ctx* ctx, const char* kernel, mcg_kernel_timing* o
 int mcg_set_timing(mcg_ctx* ctx, int32_t enabled);
 /* synchronize the context's stream */
 int mcg_sync(mcg_ctx* ctx);
+/* Random.init seed (the reference's global RNG state, mcmc.ml:49): set the Philox key and restart
+   the context's step counter at 0.  Without it the counter runs on across mcg_init / mcg_run /
+   mcg_rj_init, so repeated runs on one context never replay a draw. */
+int mcg_reseed(mcg_ctx* ctx, uint64_t seed);
+/* the Philox step index the next MH step will draw at */
+uint64_t mcg_rng_step(const mcg_ctx* ctx);
 
 #ifdef __cplusplus
 }

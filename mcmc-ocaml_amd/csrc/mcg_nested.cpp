@@ -137,11 +137,11 @@ class EvFold {
     const int64_t ilive = ntot - n_;
     View v{this, ll, ilive, 0.0};
     v.ntot = ntot;
+    // the final live points reuse the last dead iteration's log_dv (nested.ml:104), for every k
     if (k_ == 1) {
       v.ldv_live = std::log(1.0 / (double)n_) + (double)(ilive - 1) * std::log1p(-1.0 / (double)n_);
     } else {
-      const int64_t g = ilive / k_, j = ilive % k_;
-      v.ldv_live = ((double)g * prefix_[(size_t)k_] + prefix_[(size_t)j]) + std::log(1.0 / (double)n_);
+      v.ldv_live = ilive > 0 ? v.ldv_dead(ilive - 1) : std::log(1.0 / (double)n_);
     }
     fold_blocks(v, (ntot + kEvBlock - 1) / kEvBlock, threads_);
     parallel_for(wdone_, ntot, threads_, [&](int64_t m) { wts[m] = v.weight(m); });
@@ -235,6 +235,13 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   nest_init_fn init = find_nest_init(D, ctx->lik_kind);
   if (!walk || !init) return set_error(ctx, MCG_EINVAL, "no compiled nested kernel for D=%d likelihood=%d", D, ctx->lik_kind);
   (void)hipSetDevice(ctx->opts.device);
+  // forget the previous run up front: a run that fails below must not leave mcg_nested_get
+  // sizing its copies from the previous run's counts over this run's partial data
+  {
+    NestedState& R0 = ctx->nested;
+    R0.n_total = R0.n_dead = R0.n_gen = 0;
+    R0.converged = false;
+  }
   if (!ctx->nested_bufs) ctx->nested_bufs = new mcg_nested_bufs_holder();
   NestedBufs& B = ctx->nested_bufs->b;
   hipStream_t s = ctx->stream;
@@ -565,6 +572,7 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
     std::fprintf(stderr, "mcg_nested: generations %.1f ms, final copies %.1f ms, weights %.1f ms\n",
                  ms(t_start, t_gen), ms(t_gen, t_copy), ms(t_copy, now()));
   R.n_total = ntot;
+  R.converged = st.stopped != 0;
   R.n_dead = ndead;
   R.ndim = D;
   R.n_gen = st.gen_done;
@@ -575,6 +583,7 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
     res->n_dead = ndead;
     res->n_total = ntot;
     res->n_gen = st.gen_done;
+    res->converged = st.stopped ? 1 : 0;
   }
 #undef HC
   return MCG_OK;

@@ -110,6 +110,8 @@ int mcg_set_rjmcmc(mcg_ctx* ctx, const mcg_rj_model* a, const mcg_rj_model* b) {
   if (a->ndim < 1 || b->ndim < 1) return set_error(ctx, MCG_EINVAL, "RJ: ndim >= 1");
   if (!find_rj_kernel(DM)) return set_error(ctx, MCG_EINVAL, "RJ: no compiled kernel for max ndim %d", DM);
   (void)hipSetDevice(ctx->opts.device);
+  int qrc;
+  if ((qrc = quiesce(ctx)) || (qrc = fold_counters(ctx))) return qrc;
   std::vector<double> dev(32, 0.0);
   int rc;
   for (int k = 0; k < 2; ++k) {
@@ -175,6 +177,7 @@ int mcg_rj_init(mcg_ctx* ctx, int64_t nchains, const uint8_t* model, const doubl
   const int DM = ctx->D;
   const size_t N = (size_t)nchains;
   int rc;
+  if ((rc = quiesce(ctx)) || (rc = fold_counters(ctx))) return rc;
   if ((rc = hip_check(ctx, ctx->d_x.ensure(N * DM * 8), "alloc x"))) return rc;
   if ((rc = hip_check(ctx, ctx->d_ll.ensure(N * 8), "alloc ll"))) return rc;
   if ((rc = hip_check(ctx, ctx->d_lp.ensure(N * 8), "alloc lp"))) return rc;
@@ -195,12 +198,12 @@ int mcg_rj_init(mcg_ctx* ctx, int64_t nchains, const uint8_t* model, const doubl
     if ((rc = hip_check(ctx, hipMemcpy(ctx->d_tag.p, model, N, hipMemcpyHostToDevice), "copy tags"))) return rc;
   }
   ctx->N = nchains;
-  ctx->steps_done = 0;
-  ctx->nsteps_total = 0;
+  // the Philox step counter runs on (mcg_init); the start coin draws at the current step
   ctx->last_nsteps = 0;
   ctx->nrec_total = 0;
   ctx->rec_stored = 0;
   MhArgs a = base_args(ctx);
+  a.step_base = ctx->steps_done;
   if ((rc = hip_check(ctx, find_rj_init(DM)(a, model ? 0 : 1, (const double*)dxa.p, (const double*)dxb.p,
                                             ctx->stream), "rj init launch"))) return rc;
   return hip_check(ctx, hipStreamSynchronize(ctx->stream), "rj init sync");

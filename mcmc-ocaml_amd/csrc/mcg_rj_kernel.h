@@ -229,7 +229,7 @@ __global__ void __launch_bounds__(256) rj_init_kernel(const MhArgs a, int draw_t
   int tag = a.tag[c];
   if (draw_tags) {
     const Rng rng{a.k0, a.k1};
-    const u32x4 w = rng(gid, 0u, CALL_RJ_START, TAG_MH, 0u);
+    const u32x4 w = rng(gid, (uint32_t)a.step_base, CALL_RJ_START, TAG_MH, (uint32_t)(a.step_base >> 32));
     tag = u53(w.x, w.y) < 0.5 ? 0 : 1;
     a.tag[c] = (uint8_t)tag;
   }

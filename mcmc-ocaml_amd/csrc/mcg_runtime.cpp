@@ -34,6 +34,31 @@ int hip_check(mcg_ctx* ctx, hipError_t e, const char* what) {
                    hipGetErrorString(e));
 }
 
+// Host-side writes to context buffers (blocking copies, frees) do not order against the
+// context's non-blocking stream: every entry point that rewrites them drains the stream first.
+int quiesce(mcg_ctx* ctx) {
+  if (!ctx->stream) return MCG_OK;
+  return hip_check(ctx, hipStreamSynchronize(ctx->stream), "drain context stream");
+}
+
+// Fold the per-chain device accept counters of the current chains into the context totals
+// (acc_base / rej_base) and zero the step tally; the caller then restarts the device counters.
+int fold_counters(mcg_ctx* ctx) {
+  if (ctx->N < 1 || !ctx->d_nacc.p || ctx->nsteps_total == 0) {
+    ctx->nsteps_total = 0;
+    return MCG_OK;
+  }
+  std::vector<uint64_t> h((size_t)ctx->N);
+  int rc = hip_check(ctx, hipMemcpy(h.data(), ctx->d_nacc.p, h.size() * 8, hipMemcpyDeviceToHost), "copy counters");
+  if (rc) return rc;
+  uint64_t s = 0;
+  for (uint64_t v : h) s += v;
+  ctx->acc_base += s;
+  ctx->rej_base += (uint64_t)ctx->nsteps_total * (uint64_t)ctx->N - s;
+  ctx->nsteps_total = 0;
+  return MCG_OK;
+}
+
 DevBuf::~DevBuf() { release(); }
 void DevBuf::release() {
   if (p) (void)hipFree(p);
@@ -311,6 +336,7 @@ extern "C" {
 
 int mcg_set_likelihood(mcg_ctx* ctx, int32_t kind, int32_t ndim, const double* params, size_t n) {
   if (!ctx) return MCG_EINVAL;
+  if (int qrc = quiesce(ctx)) return qrc;
   std::vector<double> dev;
   const int D = ndim;
   int32_t is_cauchy = 0;
@@ -374,6 +400,7 @@ extern "C" {
 
 int mcg_set_prior(mcg_ctx* ctx, int32_t kind, const double* params, size_t n) {
   if (!ctx) return MCG_EINVAL;
+  if (int qrc = quiesce(ctx)) return qrc;
   int D = ctx->D;
   if (D < 1) return set_error(ctx, MCG_ESTATE, "set the likelihood (ndim) first");
   std::vector<double> dev;
@@ -388,6 +415,7 @@ int mcg_set_prior(mcg_ctx* ctx, int32_t kind, const double* params, size_t n) {
 
 int mcg_set_proposal(mcg_ctx* ctx, int32_t kind, const double* params, size_t n) {
   if (!ctx) return MCG_EINVAL;
+  if (int qrc = quiesce(ctx)) return qrc;
   int D = ctx->D;
   if (D < 1) return set_error(ctx, MCG_ESTATE, "set the likelihood (ndim) first");
   std::vector<double> dev;
@@ -417,6 +445,7 @@ int mcg_set_proposal(mcg_ctx* ctx, int32_t kind, const double* params, size_t n)
 int mcg_set_kd_proposal(mcg_ctx* ctx, const double* pts, int64_t M, const double* low,
                         const double* high) {
   if (!ctx || !pts || !low || !high) return MCG_EINVAL;
+  if (int qrc = quiesce(ctx)) return qrc;
   int D = ctx->D;
   if (D < 1) return set_error(ctx, MCG_ESTATE, "set the likelihood (ndim) first");
   if (M < 1) return set_error(ctx, MCG_EINVAL, "Interpolate_pdf.make: no points");
@@ -435,6 +464,12 @@ int mcg_init(mcg_ctx* ctx, int64_t nchains, const double* x_soa, const double* l
   const int D = ctx->D;
   const size_t N = (size_t)nchains;
   int rc;
+  // the uploads below are blocking copies on the null stream, which does not order against the
+  // context's non-blocking stream: let every kernel in flight finish first
+  if ((rc = quiesce(ctx))) return rc;
+  // Mcmc's counters are global until reset_counters (mcmc.ml:27-35): fold this set of chains'
+  // tallies into the context totals before the per-chain device counters restart
+  if ((rc = mcg::fold_counters(ctx))) return rc;
   if ((rc = hip_check(ctx, ctx->d_x.ensure(N * D * 8), "alloc x"))) return rc;
   if ((rc = hip_check(ctx, ctx->d_ll.ensure(N * 8), "alloc ll"))) return rc;
   if ((rc = hip_check(ctx, ctx->d_lp.ensure(N * 8), "alloc lp"))) return rc;
@@ -442,8 +477,8 @@ int mcg_init(mcg_ctx* ctx, int64_t nchains, const double* x_soa, const double* l
   if ((rc = hip_check(ctx, hipMemcpy(ctx->d_x.p, x_soa, N * D * 8, hipMemcpyHostToDevice), "copy x"))) return rc;
   if ((rc = hip_check(ctx, hipMemset(ctx->d_nacc.p, 0, N * 8), "zero counters"))) return rc;
   ctx->N = nchains;
-  ctx->steps_done = 0;
-  ctx->nsteps_total = 0;
+  // steps_done is NOT reset: the Philox step counter runs on across inits like the reference's
+  // global Random state (a re-init must not replay the previous draws); mcg_reseed restarts it
   ctx->last_nsteps = 0;
   ctx->nrec_total = 0;
   ctx->rec_stored = 0;
@@ -706,8 +741,8 @@ int mcg_get_records(mcg_ctx* ctx, double* rec_x, double* rec_ll, double* rec_lp,
 int mcg_get_counters(mcg_ctx* ctx, uint64_t* naccept, uint64_t* nreject) {
   if (!ctx) return MCG_EINVAL;
   if (ctx->N < 1) {
-    if (naccept) *naccept = 0;
-    if (nreject) *nreject = 0;
+    if (naccept) *naccept = ctx->acc_base;
+    if (nreject) *nreject = ctx->rej_base;
     return MCG_OK;
   }
   std::vector<uint64_t> h((size_t)ctx->N);
@@ -717,14 +752,15 @@ int mcg_get_counters(mcg_ctx* ctx, uint64_t* naccept, uint64_t* nreject) {
   uint64_t s = 0;
   for (uint64_t v : h) s += v;
   const uint64_t total = (uint64_t)ctx->nsteps_total * (uint64_t)ctx->N;
-  if (naccept) *naccept = s;
-  if (nreject) *nreject = total - s;
+  if (naccept) *naccept = ctx->acc_base + s;
+  if (nreject) *nreject = ctx->rej_base + (total - s);
   return MCG_OK;
 }
 
 int mcg_reset_counters(mcg_ctx* ctx) {
   if (!ctx) return MCG_EINVAL;
   ctx->nsteps_total = 0;
+  ctx->acc_base = ctx->rej_base = 0;
   if (ctx->N < 1) return MCG_OK;
   return hip_check(ctx, hipMemsetAsync(ctx->d_nacc.p, 0, (size_t)ctx->N * 8, ctx->stream), "reset counters");
 }
@@ -840,6 +876,16 @@ int mcg_get_kernel_timing(mcg_ctx* ctx, const char* kernel, mcg_kernel_timing* o
   }
   return set_error(ctx, MCG_EINVAL, "unknown kernel '%s'", k.c_str());
 }
+
+int mcg_reseed(mcg_ctx* ctx, uint64_t seed) {
+  if (!ctx) return MCG_EINVAL;
+  if (int rc = quiesce(ctx)) return rc;
+  ctx->opts.seed = seed;
+  ctx->steps_done = 0;
+  return MCG_OK;
+}
+
+uint64_t mcg_rng_step(const mcg_ctx* ctx) { return ctx ? ctx->steps_done : 0; }
 
 int mcg_sync(mcg_ctx* ctx) {
   if (!ctx) return MCG_EINVAL;

@@ -39,6 +39,7 @@ struct NestedState {
   std::vector<double> ll, lp, wts;
   int64_t n_total = 0, n_dead = 0, n_gen = 0, nlive = 0, ndim = 0;
   double log_ev = 0.0, log_dev = 0.0;
+  bool converged = false;       // the stop test fired (false: max_dead reached first)
 };
 
 }  // namespace mcg
@@ -65,7 +66,8 @@ struct mcg_ctx {
   int64_t N = 0;
   mcg::DevBuf d_x, d_ll, d_lp, d_nacc;
   uint64_t steps_done = 0;      // global RNG step counter (all runs)
-  int64_t nsteps_total = 0;     // steps since the last counter reset
+  int64_t nsteps_total = 0;     // steps of the current chains since init / the last counter reset
+  uint64_t acc_base = 0, rej_base = 0;  // tallies of earlier chain sets (folded at mcg_init)
   int64_t last_nsteps = 0;
   int lanes = 1;
   // records and statistics
@@ -97,6 +99,8 @@ struct mcg_ctx {
 namespace mcg {
 int set_error(mcg_ctx* ctx, int code, const char* fmt, ...);
 int hip_check(mcg_ctx* ctx, hipError_t e, const char* what);
+int quiesce(mcg_ctx* ctx);
+int fold_counters(mcg_ctx* ctx);
 MhArgs base_args(mcg_ctx* ctx);
 int choose_lanes(mcg_ctx* ctx);
 double host_pexp(double x);

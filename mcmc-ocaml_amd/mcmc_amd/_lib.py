@@ -43,7 +43,7 @@ class McgNestedOpts(C.Structure):
 
 class McgNestedResult(C.Structure):
     _fields_ = [("log_ev", C.c_double), ("log_dev", C.c_double), ("n_dead", C.c_int64),
-                ("n_total", C.c_int64), ("n_gen", C.c_int64)]
+                ("n_total", C.c_int64), ("n_gen", C.c_int64), ("converged", C.c_int32)]
 
 
 class McgRjModel(C.Structure):
@@ -104,6 +104,8 @@ SIGNATURES = {
     "mcg_get_kernel_timing": ([C.c_void_p, C.c_char_p, C.POINTER(McgKernelTiming)], C.c_int),
     "mcg_set_timing": ([C.c_void_p, C.c_int32], C.c_int),
     "mcg_sync": ([C.c_void_p], C.c_int),
+    "mcg_reseed": ([C.c_void_p, C.c_uint64], C.c_int),
+    "mcg_rng_step": ([C.c_void_p], C.c_uint64),
 }
 
 

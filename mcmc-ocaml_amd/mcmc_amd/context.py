@@ -142,6 +142,15 @@ class Context:
         self._check(L.lib().mcg_get_kernel_timing(self._p, kernel.encode(), C.byref(t)))
         return dict(launches=t.launches, total_ms=t.total_ms, last_ms=t.last_ms)
 
+    def reseed(self, seed):
+        """Random.init seed: new Philox key, step counter back to 0 (include/mcg.h mcg_reseed)."""
+        self._check(L.lib().mcg_reseed(self._p, seed))
+        self.seed = seed
+
+    def rng_step(self):
+        """Philox step index of the next MH step."""
+        return int(L.lib().mcg_rng_step(self._p))
+
     def sync(self):
         self._check(L.lib().mcg_sync(self._p))
 

@@ -56,7 +56,10 @@ def mcmc_array(n, log_likelihood, log_prior, jump_proposal, start, nbin=0, nskip
 def make_mcmc_sampler(log_likelihood, log_prior, jump_proposal, ctx=None):
     """Mcmc.make_mcmc_sampler (mcmc.ml:37-56): returns step(state) -> next state for a batch.
 
-    state = (x (D, N), ll (N,), lp (N,)); each call is one MH step of every chain on the device."""
+    state = (x (D, N), ll (N,), lp (N,)); each call is one MH step of every chain on the device.
+    Successive calls draw at successive Philox steps (the context's step counter is never
+    rewound, as the reference's global Random state is not), and the accept / reject tallies
+    add up across calls until reset_counters (mcmc.ml:27-35)."""
     ctx = ctx or default_context()
     ctx.set_model(log_likelihood, log_prior, jump_proposal)
 

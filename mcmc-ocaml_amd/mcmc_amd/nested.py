@@ -1,5 +1,6 @@
 """Mirror of the reference's Nested module (nested.mli) over the HIP sampler."""
 import ctypes as C
+import warnings
 
 import numpy as np
 
@@ -35,13 +36,23 @@ def nested_evidence(log_likelihood, log_prior, epsrel=0.01, nmcmc=1000, nlive=10
     pts = np.zeros((n, D)); ll = np.zeros(n); lp = np.zeros(n); w = np.zeros(n)
     L.check(L.lib().mcg_nested_get(ctx.ptr, L.dptr(pts), L.dptr(ll), L.dptr(lp), L.dptr(w)),
             ctx.ptr)
-    return NestedOutput(r.log_ev, r.log_dev, pts, w, ll, lp, r.n_dead, r.n_gen)
+    if not r.converged:
+        warnings.warn("nested_evidence: max_dead (%d dead points) reached before the stop test "
+                      "(nested.ml:45-48) fired; log Z comes from an unconverged run" % r.n_dead,
+                      UnconvergedWarning, stacklevel=2)
+    return NestedOutput(r.log_ev, r.log_dev, pts, w, ll, lp, r.n_dead, r.n_gen, bool(r.converged))
+
+
+class UnconvergedWarning(RuntimeWarning):
+    """A nested run stopped at its max_dead safety cap instead of the reference's stop test."""
 
 
 class NestedOutput(tuple):
-    def __new__(cls, log_ev, log_dev, pts, log_wts, ll, lp, n_dead, n_gen):
+    """nested_output (nested.ml:20) plus ll / lp per point, counts and `converged` (False when
+    the max_dead cap ended the run before remaining_integral_negligable fired)."""
+    def __new__(cls, log_ev, log_dev, pts, log_wts, ll, lp, n_dead, n_gen, converged=True):
         t = super().__new__(cls, (log_ev, log_dev, pts, log_wts))
-        t.ll, t.lp, t.n_dead, t.n_gen = ll, lp, n_dead, n_gen
+        t.ll, t.lp, t.n_dead, t.n_gen, t.converged = ll, lp, n_dead, n_gen, converged
         return t
 
 
@@ -67,8 +78,9 @@ def merge_runs(runs):
                                      L.dptr(w)))
     n_dead = int(n - nlive.sum())
     n_gen = int(sum(getattr(o, "n_gen", 0) for o, _, _ in runs))
+    conv = all(getattr(o, "converged", True) for o, _, _ in runs)
     return NestedOutput(le.value, ld.value, None if pts is None else pts[order], w, ll[order], lp[order],
-                        n_dead, n_gen)
+                        n_dead, n_gen, conv)
 
 
 def _ll(o):

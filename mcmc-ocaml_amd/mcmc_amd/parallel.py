@@ -16,6 +16,8 @@ import numpy as np
 from . import nested as _nested
 from .context import Context, combine_tiles
 
+MAX_K = 16384          # mcg_nested's cap on points retired per generation (include/mcg.h)
+
 GOLDEN64 = 0x9E3779B97F4A7C15
 
 
@@ -82,6 +84,17 @@ def allgather_runs(output, nlive, k, device=None, group=None, points=True):
     return runs
 
 
+def replica_sizes(nlive, k, world):
+    """(live points, points retired per generation) of one of `world` replicas: nlive / world
+    live points, k clamped to what mcg_nested accepts (1 <= k < nlive, k <= MAX_K)."""
+    if nlive % world:
+        raise ValueError("nlive (%d) must be a multiple of the number of ranks (%d)" % (nlive, world))
+    nl = nlive // world
+    if nl < 2:
+        raise ValueError("nlive / ranks = %d: every replica needs at least 2 live points" % nl)
+    return nl, max(1, min(k, nl - 1, MAX_K))
+
+
 def nested_evidence_replicas(log_likelihood, log_prior, epsrel=0.01, nmcmc=1000, nlive=1000,
                              mode_hopping_frac=0.1, k=1, seed=0, device=0, group=None,
                              comm_device=None, points=True):
@@ -91,10 +104,7 @@ def nested_evidence_replicas(log_likelihood, log_prior, epsrel=0.01, nmcmc=1000,
     rank returns the same merged NestedOutput (points=False: gather ll / lp only; the merged
     output then has no points)."""
     rank, world = _world(group)
-    if nlive % world:
-        raise ValueError("nlive (%d) must be a multiple of the number of ranks (%d)" % (nlive, world))
-    nl = nlive // world
-    kk = min(k, nl)
+    nl, kk = replica_sizes(nlive, k, world)
     with Context(seed=replica_seed(seed, rank), device=device) as ctx:
         out = _nested.nested_evidence(log_likelihood, log_prior, epsrel=epsrel, nmcmc=nmcmc,
                                       nlive=nl, mode_hopping_frac=mode_hopping_frac, k=kk, ctx=ctx)

@@ -1262,14 +1262,13 @@ void or_evidence_weights(int64_t n, int64_t nlive, int64_t k, const double* ll,
     wts[i + 1] = or_log_sum_logs(wts[i + 1], log_half + dhigh);
     last_dv = log_dv;
   }
+  /* the final live points reuse the log_dv of the last dead iteration (nested.ml:104: the
+     reference's i = ilive - 1 volume element, for every k); with no dead point at all, k = 1
+     keeps the reference's formula at i = -1 and k > 1 shares the whole prior volume */
   double log_dv;
   if (k == 1) log_dv = log(1.0 / (double)nlive) + (double)(ilive - 1) * log1p(-1.0 / (double)nlive);
-  else {
-    /* remaining volume X_final shared by the nlive final points */
-    int64_t g = ilive / k, j = ilive % k;
-    log_dv = ((double)g * prefix[k] + prefix[j]) + log(1.0 / (double)nlive);
-    (void)last_dv;
-  }
+  else if (ilive > 0) log_dv = last_dv;
+  else log_dv = log(1.0 / (double)nlive);
   for (int64_t i = ilive; i < n; ++i) {
     double dlow = log_dv + ll[i - 1], dhigh = log_dv + ll[i];
     OR_EV_FOLD(dlow, dhigh);

@@ -75,3 +75,18 @@ def test_two_rank_gloo_reduction_matches_single_rank():
         np.testing.assert_array_equal(mean, ref[0])
         np.testing.assert_array_equal(sd, ref[1])
         assert lz == ref[2]
+
+
+def test_replica_sizes_keep_k_below_nlive():
+    """Per-replica (nlive, k) stay inside mcg_nested's bounds at any rank count (1 <= k < nlive,
+    k <= 16384): nlive 32768 with k 2048 on 16 ranks gives 2048 live points and k 2047."""
+    from mcmc_amd.parallel import MAX_K, replica_sizes
+    assert replica_sizes(32768, 2048, 1) == (32768, 2048)
+    assert replica_sizes(32768, 2048, 8) == (4096, 2048)
+    assert replica_sizes(32768, 2048, 16) == (2048, 2047)
+    assert replica_sizes(2 ** 20, 2 ** 15, 2) == (2 ** 19, MAX_K)
+    assert replica_sizes(8, 1, 4) == (2, 1)
+    with pytest.raises(ValueError):
+        replica_sizes(100, 1, 3)          # not a multiple of the rank count
+    with pytest.raises(ValueError):
+        replica_sizes(4, 1, 4)            # one live point per replica

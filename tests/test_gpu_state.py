@@ -1,0 +1,168 @@
+"""GPU tests of a context's state across calls: the Philox step counter and the accept / reject
+tallies run on across mcg_init (as the reference's global Random state and its global counters,
+mcmc.ml:27-35, do), host uploads are ordered after in-flight kernels, and a nested run's result
+reports whether the stop test fired.  Every draw is checked bit for bit against the oracle at
+the step index it must have used."""
+import math
+import warnings
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def T():
+    from mcmc_amd import targets
+    return targets
+
+
+def c2_model(T, D=8, seed=42):
+    rng = np.random.default_rng(seed)
+    mu, sg = rng.uniform(-1, 1, D), rng.uniform(0.5, 2, D)
+    s = 2.38 / math.sqrt(D) * float(np.median(sg))
+    return T.diag_gauss(mu, sg), T.box(-10 * np.ones(D), 10 * np.ones(D)), T.gauss(s), mu, sg
+
+
+def oracle_model(O, lik, pri, prop):
+    return O.Model(lik.ndim, lik.kind, lik.params, pri.kind, pri.params, prop.kind, prop.params)
+
+
+def oracle_start(m, x0):
+    N = x0.shape[1]
+    return (np.array([m.loglik(x0[:, i]) for i in range(N)]),
+            np.array([m.logprior(x0[:, i]) for i in range(N)]))
+
+
+def test_make_mcmc_sampler_successive_steps_draw_successive_indices(oracle, T):
+    """Two step() calls of Mcmc.make_mcmc_sampler (mcmc.ml:37-56) from the returned state are the
+    oracle's steps 0 and 1, not step 0 twice; the counters add up over both calls."""
+    from mcmc_amd import Context, mcmc
+    lik, pri, prop, mu, sg = c2_model(T)
+    N = 256
+    x0 = np.random.default_rng(3).normal(mu[:, None], sg[:, None], size=(8, N))
+    m = oracle_model(oracle, lik, pri, prop)
+    ll0, lp0 = oracle_start(m, x0)
+    ctx = Context(seed=5)
+    step = mcmc.make_mcmc_sampler(lik, pri, prop, ctx=ctx)
+    s1 = step((x0, ll0, lp0))
+    s2 = step(s1)
+    o1 = oracle.mh_run(m, 5, x0, ll0, lp0, nbin=1, n_rec=0, record_x=False, record_llp=False,
+                       record_accept=False, accumulate=False, step0=0)
+    o2 = oracle.mh_run(m, 5, o1["x"], o1["ll"], o1["lp"], nbin=1, n_rec=0, record_x=False,
+                       record_llp=False, record_accept=False, accumulate=False, step0=1)
+    for s, o in ((s1, o1), (s2, o2)):
+        np.testing.assert_array_equal(s[0], o["x"])
+        np.testing.assert_array_equal(s[1], o["ll"])
+        np.testing.assert_array_equal(s[2], o["lp"])
+    # the same draw twice would move an accepted chain by the same vector again
+    d1, d2 = s1[0] - x0, s2[0] - s1[0]
+    both = np.all(d1 != 0, axis=0) & np.all(d2 != 0, axis=0)
+    assert both.any()
+    assert not np.any(np.all(d1[:, both] == d2[:, both], axis=0))
+    acc, rej = ctx.counters()
+    assert acc == int(o1["nacc"].sum() + o2["nacc"].sum()) and acc + rej == 2 * N
+    assert ctx.rng_step() == 2
+    ctx.close()
+
+
+def test_run_then_reinit_without_sync_matches_oracle(oracle, T):
+    """mcg_run returns without a sync; an immediate init() of new chains must wait for the
+    in-flight MH kernel (no torn state), and the second run continues the Philox step counter."""
+    from mcmc_amd import Context
+    lik, pri, prop, mu, sg = c2_model(T)
+    N = 4096
+    rng = np.random.default_rng(7)
+    xa = rng.normal(mu[:, None], sg[:, None], size=(8, N))
+    xb = rng.normal(mu[:, None], sg[:, None], size=(8, N))
+    m = oracle_model(oracle, lik, pri, prop)
+    ctx = Context(seed=9)
+    ctx.set_model(lik, pri, prop)
+    ctx.init(xa)
+    ctx.run(nbin=2000, n_rec=0, record_x=False, record_llp=False)   # long, left in flight
+    ctx.init(xb)
+    ctx.run(nbin=30, n_rec=0, record_x=False, record_llp=False)
+    x, ll, lp = ctx.state()
+    acc, rej = ctx.counters()
+    lla, lpa = oracle_start(m, xa)
+    oa = oracle.mh_run(m, 9, xa, lla, lpa, nbin=2000, n_rec=0, record_x=False, record_llp=False,
+                       record_accept=False, accumulate=False, nthreads=8)
+    llb, lpb = oracle_start(m, xb)
+    ob = oracle.mh_run(m, 9, xb, llb, lpb, nbin=30, n_rec=0, record_x=False, record_llp=False,
+                       record_accept=False, accumulate=False, step0=2000, nthreads=8)
+    np.testing.assert_array_equal(x, ob["x"])
+    np.testing.assert_array_equal(ll, ob["ll"])
+    np.testing.assert_array_equal(lp, ob["lp"])
+    # Mcmc's counters are global until reset_counters: both chain sets count
+    assert acc == int(oa["nacc"].sum() + ob["nacc"].sum())
+    assert acc + rej == 2030 * N
+    ctx.reset_counters()
+    assert ctx.counters() == (0, 0)
+    ctx.close()
+
+
+def test_set_model_after_run_waits_for_the_kernel(oracle, T):
+    """A new likelihood uploaded right after an unsynchronised run must not reach that run."""
+    from mcmc_amd import Context
+    lik, pri, prop, mu, sg = c2_model(T)
+    lik2 = T.diag_gauss(mu + 0.5, sg * 1.5)
+    N = 4096
+    x0 = np.random.default_rng(8).normal(mu[:, None], sg[:, None], size=(8, N))
+    m = oracle_model(oracle, lik, pri, prop)
+    ctx = Context(seed=4)
+    ctx.set_model(lik, pri, prop)
+    ctx.init(x0)
+    ctx.run(nbin=2000, n_rec=0, record_x=False, record_llp=False)
+    ctx.set_model(lik2, pri, prop)           # would race the kernel without the drain
+    x, ll, _ = ctx.state()
+    ll0, lp0 = oracle_start(m, x0)
+    o = oracle.mh_run(m, 4, x0, ll0, lp0, nbin=2000, n_rec=0, record_x=False, record_llp=False,
+                      record_accept=False, accumulate=False, nthreads=8)
+    np.testing.assert_array_equal(x, o["x"])
+    np.testing.assert_array_equal(ll, o["ll"])
+    ctx.close()
+
+
+def test_reseed_restarts_the_stream(oracle, T):
+    """Context.reseed (Random.init): the step counter returns to 0, so a run after a reseed to
+    the same seed repeats a fresh context's run exactly; without it a repeated run differs."""
+    from mcmc_amd import Context
+    lik, pri, prop, mu, sg = c2_model(T)
+    x0 = np.random.default_rng(11).normal(mu[:, None], sg[:, None], size=(8, 512))
+    ctx = Context(seed=21)
+    ctx.set_model(lik, pri, prop)
+    outs = []
+    for reseed in (False, False, True):
+        if reseed:
+            ctx.reseed(21)
+        ctx.init(x0)
+        ctx.run(nbin=20, n_rec=0, record_x=False, record_llp=False)
+        outs.append(ctx.state()[0])
+    assert not np.array_equal(outs[0], outs[1])
+    np.testing.assert_array_equal(outs[0], outs[2])
+    ctx.close()
+
+
+def test_nested_cap_reports_unconverged_and_failed_run_clears_result(T):
+    """max_dead reached before the stop test: the result says converged = False (with a
+    warning); a later run that fails leaves no stale result for mcg_nested_get."""
+    from mcmc_amd import Context, nested
+    from mcmc_amd._lib import McgError
+    lik = T.diag_gauss([0.5, 0.5], [0.1, 0.1])
+    pri = T.box([0, 0], [1, 1], 0.0, open_=True)
+    ctx = Context(seed=2)
+    with pytest.warns(nested.UnconvergedWarning):
+        out = nested.nested_evidence(lik, pri, ctx=ctx, nlive=200, nmcmc=10, k=10, max_dead=100)
+    assert not out.converged and out.n_dead == 100
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        full = nested.nested_evidence(lik, pri, ctx=ctx, nlive=200, nmcmc=10, k=10)
+    assert full.converged and full.n_dead > 100
+    with pytest.raises(McgError):          # max_dead below one generation: fails mid-setup
+        nested.nested_evidence(lik, pri, ctx=ctx, nlive=200, nmcmc=10, k=10, max_dead=5)
+    from mcmc_amd import _lib as L
+    p = np.zeros((full.ll.size, 2)); a = np.zeros(full.ll.size)
+    rc = L.lib().mcg_nested_get(ctx.ptr, L.dptr(p), L.dptr(a), L.dptr(a), L.dptr(a))
+    assert rc == L.MCG_ESTATE
+    ctx.close()

@@ -299,6 +299,51 @@ def test_evidence_weights_k1_matches_reference_formula(oracle):
     np.testing.assert_array_equal(w, np.array(wts) - lev)
 
 
+@pytest.mark.parametrize("k", [2, 5])
+def test_evidence_weights_k_generations_restated(oracle, k):
+    """k > 1 generalisation of nested.ml:81-120, restated in Python: dead point i was retired
+    with nlive - (i mod k) live points from volume X_i = (i div k) L_k + prefix[i mod k]; the
+    final live points reuse the last dead iteration's log_dv, as the reference does at k = 1
+    (nested.ml:104)."""
+    rng = np.random.default_rng(9 + k)
+    nlive = 12
+    ll = np.sort(rng.normal(size=61))
+    le, ld, w = oracle.evidence_weights(ll, nlive, k)
+
+    def lse(a, b):
+        if a == -math.inf and b == -math.inf:
+            return -math.inf
+        if b > a:
+            a, b = b, a
+        return a + math.log1p(math.exp(b - a))
+
+    prefix = [0.0]
+    for j in range(k):
+        prefix.append(prefix[-1] + math.log1p(-1.0 / (nlive - j)))
+    lh = -0.69314718055994530942
+    n = len(ll); ilive = n - nlive
+    wts = [-math.inf] * n; low = high = -math.inf
+
+    def ldv_dead(i):
+        j, g = i % k, i // k
+        return math.log(1.0 / (nlive - j)) + (g * prefix[k] + prefix[j])
+
+    for i in range(ilive):
+        ldv = ldv_dead(i)
+        dl, dh = ldv + ll[i], ldv + ll[i + 1]
+        low, high = lse(low, dl), lse(high, dh)
+        wts[i] = lse(wts[i], lh + dl); wts[i + 1] = lse(wts[i + 1], lh + dh)
+    ldv = ldv_dead(ilive - 1)
+    for i in range(ilive, n):
+        dl, dh = ldv + ll[i - 1], ldv + ll[i]
+        low, high = lse(low, dl), lse(high, dh)
+        wts[i - 1] = lse(wts[i - 1], lh + dl); wts[i] = lse(wts[i], lh + dh)
+    lev = lh + lse(low, high)
+    ldev = high + math.log1p(-math.exp(low - high))
+    assert le == lev and ld == ldev
+    np.testing.assert_array_equal(w, np.array(wts) - lev)
+
+
 # ---------------------------------------------------------------- kD tree (kd_tree_test.ml)
 def test_kd_tree_invariants(oracle):
     rng = np.random.default_rng(6)
