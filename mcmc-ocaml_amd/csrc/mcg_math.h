@@ -41,6 +41,46 @@ __device__ __forceinline__ u32x4 philox(uint32_t c0, uint32_t c1, uint32_t c2, u
   return u32x4{c0, c1, c2, c3};
 }
 
+// N Philox4x32-10 calls that differ only in the third counter word (the MH step's per-dim
+// calls: same chain, step and tag), advanced round by round together: N independent chains of
+// (v_mad_u64_u32 -> v_bitop3) instead of one serial 10-round chain after another, so one wave
+// keeps its SIMD issuing; the shared first-round product of c0 is computed once.
+template <int N>
+__device__ __forceinline__ void philox_multi(u32x4* out, uint32_t c0, uint32_t c1, const uint32_t* c2,
+                                             uint32_t c3, uint32_t k0, uint32_t k1) {
+  asm volatile("" : "+s"(k0), "+s"(k1));
+  uint32_t a[N], b[N], c[N], d[N];
+  {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2[n];
+      a[n] = xor3((uint32_t)(p1 >> 32), c1, k0);
+      b[n] = (uint32_t)p1;
+      c[n] = xor3((uint32_t)(p0 >> 32), c3, k1);
+      d[n] = (uint32_t)p0;
+    }
+  }
+#pragma unroll
+  for (int r = 1; r < 10; ++r) {
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      const uint64_t p0 = (uint64_t)0xD2511F53u * a[n];
+      const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[n];
+      const uint32_t n0 = xor3((uint32_t)(p1 >> 32), b[n], k0);
+      const uint32_t n2 = xor3((uint32_t)(p0 >> 32), d[n], k1);
+      b[n] = (uint32_t)p1;
+      d[n] = (uint32_t)p0;
+      a[n] = n0;
+      c[n] = n2;
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) out[n] = u32x4{a[n], b[n], c[n], d[n]};
+}
+
 // counter layout (c0, c1, c2, (tag << 16) | hi16), key = seed
 enum : uint32_t {
   TAG_MH = 1u, TAG_NEST_WALK = 3u, TAG_NEST_PRIOR = 4u,
@@ -149,59 +189,64 @@ __device__ __forceinline__ double psqrt(double a) {
   return a * y;
 }
 
-// standard normal from one 32-bit word (spec v5): the sign is bit 31; the other
+// standard normal from one 32-bit word (spec v6): the sign is bit 31; the other
 // 31 bits give v = 2w + 1 (odd), u = v 2^-33 in (0, 1/2).  double(v) = 2^E (1 + f) is exact; the
-// segment is (E, top kNrmS bits of f) = (high word >> 15) - (1023 << 5); the rest of f, put under
+// segment is (E, top kNrmS bits of f), its row bits 15..24 of the high word; the rest of f, put under
 // the exponent of 1.0, gives 1 + t/32 exactly, so x = t/32 with one exact subtraction, and
-// z = -+ p_seg(x): the segment's degree-5 polynomial in t (oracle/gen_tables.py), stored scaled by
-// 32^k so that Horner in x rounds exactly like the oracle's Horner in t.  Exactly symmetric:
-// flipping bit 31 negates z.  `tab` points at kNrmTab or at a copy staged in LDS (3 x 16-B gathers).
-static_assert(kNrmS == 5 && kNrmDeg == 5, "pnormal is written for 32 segments per octave, degree 5");
-__device__ __forceinline__ double pnormal(uint32_t w, const double2* tab) {
-  const uint32_t v = (w << 1) | 1u;
-  const double dv = (double)v;                                   // exact
-  const uint32_t hi = (uint32_t)__double2hiint(dv);
-  const uint32_t lo = (uint32_t)__double2loint(dv);
-  const double2* c = tab + 3u * ((hi >> 15) - (1023u << kNrmS));
-  const double x = __hiloint2double((int)((hi & 0x7FFFu) | 0x3FF00000u), (int)lo) - 1.0;
-  const double2 c0 = c[0], c1 = c[1], c2 = c[2];
-  double p = fma(c0.x, x, c0.y);
-  p = fma(p, x, c1.x);
-  p = fma(p, x, c1.y);
-  p = fma(p, x, c2.x);
-  p = fma(p, x, c2.y);
-  return __hiloint2double(__double2hiint(p) ^ (int)(w & 0x80000000u), __double2loint(p));
+// z = -+ p_seg(x): the segment's cubic in t (oracle/gen_tables.py), stored scaled by 32^k so that
+// Horner in x rounds exactly like the oracle's Horner in t.  Exactly symmetric: flipping bit 31
+// negates z.  `tab` points at kNrmTab or at a copy staged in LDS: (d3, d2) of the segment at row
+// r, (d1, d0) at row kNrmSeg + r -- two 16-B gathers from one address (constant offset), each on
+// LDS slot r mod 16.
+static_assert(kNrmS == 5 && kNrmDeg == 3, "pnormal is written for 32 segments per octave, degree 3");
+constexpr int kNrmSeg = 32 << kNrmS;
+static_assert(kNrmTabN == 2 * kNrmSeg, "normal table: two rows per segment");
+
+// (w << 1) | 1 and (hi & 0x7FFF) | 0x3FF00000 as single VALU ops (hipcc emits shift + or pairs)
+__device__ __forceinline__ uint32_t nrm_odd(uint32_t w) {
+  uint32_t r;
+  asm("v_lshl_or_b32 %0, %1, 1, 1" : "=v"(r) : "v"(w));
+  return r;
+}
+__device__ __forceinline__ uint32_t nrm_frac_hi(uint32_t hi) {
+  uint32_t r;
+  // gfx9 VOP3: no literal operand and one scalar operand, so the mask comes in a VGPR
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(hi), "v"(0x7FFFu), "s"(0x3FF00000u));
+  return r;
 }
 
-// pnormal in two halves, for callers that issue the table gather early and finish later (the
-// nested walker: a gather issued after its prefetched rows would make the in-order vmcnt wait
-// for every row).  Same operations as pnormal.
 struct NrmPending {
   double x;
-  double2 c0, c1, c2;
+  double2 c32, c10;
   uint32_t sign;
 };
 __device__ __forceinline__ NrmPending pnormal_issue(uint32_t w, const double2* tab) {
-  const uint32_t v = (w << 1) | 1u;
-  const double dv = (double)v;
+  const uint32_t v = nrm_odd(w);
+  const double dv = (double)v;                                   // exact
   const uint32_t hi = (uint32_t)__double2hiint(dv);
   const uint32_t lo = (uint32_t)__double2loint(dv);
-  const double2* c = tab + 3u * ((hi >> 15) - (1023u << kNrmS));
+  // row = bits 15..24 of hi: the low 5 bits of the biased exponent 1023 + E, then j (the table
+  // is stored rotated by one octave, oracle/gen_tables.py dev_row), so no bias subtraction and
+  // both gathers take the table base as an immediate offset
+  const double2* c = tab + ((hi >> 15) & (uint32_t)(kNrmSeg - 1));
   NrmPending r;
-  r.x = __hiloint2double((int)((hi & 0x7FFFu) | 0x3FF00000u), (int)lo) - 1.0;
-  r.c0 = c[0];
-  r.c1 = c[1];
-  r.c2 = c[2];
-  r.sign = w & 0x80000000u;
+  r.x = __hiloint2double((int)nrm_frac_hi(hi), (int)lo) - 1.0;
+  r.c32 = c[0];
+  r.c10 = c[kNrmSeg];
+  r.sign = w;
   return r;
 }
 __device__ __forceinline__ double pnormal_finish(const NrmPending& q) {
-  double p = fma(q.c0.x, q.x, q.c0.y);
-  p = fma(p, q.x, q.c1.x);
-  p = fma(p, q.x, q.c1.y);
-  p = fma(p, q.x, q.c2.x);
-  p = fma(p, q.x, q.c2.y);
-  return __hiloint2double(__double2hiint(p) ^ (int)q.sign, __double2loint(p));
+  double p = fma(q.c32.x, q.x, q.c32.y);
+  p = fma(p, q.x, q.c10.x);
+  p = fma(p, q.x, q.c10.y);
+  // p_hi ^ (w & 0x80000000): the sign of the word flips z
+  uint32_t h;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x6c" : "=v"(h) : "v"(q.sign), "v"(__double2hiint(p)), "s"(0x80000000u));
+  return __hiloint2double((int)h, __double2loint(p));
+}
+__device__ __forceinline__ double pnormal(uint32_t w, const double2* tab) {
+  return pnormal_finish(pnormal_issue(w, tab));
 }
 
 // log1p(r), r in [0,1] (Goldberg: r * log(1+r) / ((1+r)-1)); log-sum-exp on the portable

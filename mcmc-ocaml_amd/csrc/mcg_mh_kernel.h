@@ -444,7 +444,13 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
   // UNI (isotropic proposal scale, one box for every dim): the scale and the box are kernel
   // arguments (SGPRs), so the lane's likelihood constants fit in registers for the whole launch
   double rc_m[UNI ? L::NL : 1], rc_i[UNI ? L::NL : 1];
+  // UNI: the likelihood normaliser and the box's log density in VGPRs too (a per-step cached
+  // load of each put a vector-memory wait on every step's critical path)
+  double rc_c = 0.0, rc_lp = 0.0;
   if constexpr (UNI) {
+    rc_c = LIK == MCG_LIK_DIAG_GAUSS ? a.lik[2 * D] : LIK == MCG_LIK_GAUSS_SHELL ? a.lik[D + 2] : 0.0;
+    rc_lp = a.prior_kind != MCG_PRIOR_FLAT ? a.pri[2 * D] : 0.0;
+    asm volatile("" : "+v"(rc_c), "+v"(rc_lp));
 #pragma unroll
     for (int i = 0; i < L::NCL; ++i)
 #pragma unroll
@@ -490,12 +496,18 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
       for (int j = 0; j < L::NA; ++j) A[j] = 0.0;
       int inb = 1;
       const bool box = a.prior_kind != MCG_PRIOR_FLAT;
+      // the lane's Philox calls of this step (c2 = call index sub + P i) advanced together
+      u32x4 wl[L::NCL];
+      {
+        uint32_t cidx[L::NCL];
+#pragma unroll
+        for (int i = 0; i < L::NCL; ++i) cidx[i] = (uint32_t)(sub + P * i);
+        philox_multi<L::NCL>(wl, gid, tlo, cidx, (TAG_MH << 16) | (thi & 0xFFFFu), rng.k0, rng.k1);
+      }
 #pragma unroll
       for (int i = 0; i < L::NCL; ++i) {
-        if (P == 1 && 4 * i >= D) continue;
-        asm volatile("" ::: "memory");
         const int cc = sub + P * i;
-        const u32x4 w = rng(gid, tlo, (uint32_t)cc, TAG_MH, thi);
+        const u32x4 w = wl[i];
         double z[4];
         z[0] = pnormal(w.x, s_nt);
         z[1] = pnormal(w.y, s_nt);
@@ -528,15 +540,15 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
       } else {
         const double S = reduce_canon<P>(A);
         if constexpr (LIK == MCG_LIK_DIAG_GAUSS) {
-          lly = qlik[2 * D] - 0.5 * S;
+          lly = (UNI ? rc_c : qlik[2 * D]) - 0.5 * S;
         } else {
           const double rr = psqrt(S);
           const double qq = (rr - qlik[D]) * qlik[D + 1];
-          lly = qlik[D + 2] - 0.5 * qq * qq;
+          lly = (UNI ? rc_c : qlik[D + 2]) - 0.5 * qq * qq;
         }
       }
       inb = and_lanes<P>(inb);
-      lpy = !box ? 0.0 : (inb ? qpri[2 * D] : -__builtin_inf());
+      lpy = !box ? 0.0 : (inb ? (UNI ? rc_lp : qpri[2 * D]) : -__builtin_inf());
     } else {
       // ---- proposal (jump_proposal, mcmc.ml:41) ----
       if constexpr (PROP == MCG_PROP_GAUSS) {

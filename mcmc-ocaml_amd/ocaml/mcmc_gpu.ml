@@ -47,6 +47,7 @@ let nr_log_dev = field nested_result "log_dev" double
 let nr_n_dead = field nested_result "n_dead" int64_t
 let nr_n_total = field nested_result "n_total" int64_t
 let nr_n_gen = field nested_result "n_gen" int64_t
+let nr_converged = field nested_result "converged" int32_t
 let () = seal nested_result
 
 let c_ctx_create = fn "mcg_ctx_create" (ptr (ptr void) @-> ptr opts @-> returning int)
@@ -61,6 +62,7 @@ let c_run = fn "mcg_run" (ptr void @-> ptr run_opts @-> returning int)
 let c_get_records = fn "mcg_get_records" (ptr void @-> ptr double @-> ptr double @-> ptr double @-> ptr uint64_t @-> returning int)
 let c_get_counters = fn "mcg_get_counters" (ptr void @-> ptr uint64_t @-> ptr uint64_t @-> returning int)
 let c_reset_counters = fn "mcg_reset_counters" (ptr void @-> returning int)
+let c_reseed = fn "mcg_reseed" (ptr void @-> uint64_t @-> returning int)
 let c_stats = fn "mcg_stats" (ptr void @-> ptr double @-> ptr double @-> ptr double @-> returning int)
 let c_nested = fn "mcg_nested" (ptr void @-> ptr nested_opts @-> ptr nested_result @-> ptr void @-> ptr void @-> returning int)
 let c_nested_get = fn "mcg_nested_get" (ptr void @-> ptr double @-> ptr double @-> ptr double @-> ptr double @-> returning int)
@@ -164,6 +166,8 @@ let set_model ctx lik pri prop =
 
 let reset_counters ctx = check ctx (c_reset_counters ctx)
 
+let reseed ctx seed = check ctx (c_reseed ctx (Unsigned.UInt64.of_int64 seed))
+
 let get_counters ctx =
   let a = allocate uint64_t Unsigned.UInt64.zero and r = allocate uint64_t Unsigned.UInt64.zero in
   check ctx (c_get_counters ctx a r);
@@ -201,6 +205,8 @@ let nested_evidence ?(epsrel = 0.01) ?(nmcmc = 1000) ?(nlive = 1000) ?(mode_hopp
   setf o n_epsrel epsrel; setf o n_mode_hop mode_hopping_frac; setf o n_max_dead 0L;
   let r = make nested_result in
   check ctx (c_nested ctx (addr o) (addr r) null null);
+  if getf r nr_converged = 0l then
+    prerr_endline "Mcmc_gpu.nested_evidence: max_dead cap reached before the stop test (unconverged)";
   let n = Int64.to_int (getf r nr_n_total) in
   let pts = CArray.make double (n * d) and ll = CArray.make double n
   and lp = CArray.make double n and w = CArray.make double n in

@@ -53,6 +53,10 @@ val set_model : ctx -> likelihood -> prior -> proposal option -> unit
 
 (** Mcmc.reset_counters / get_counters (mcmc.mli:29-30) for this context. *)
 val reset_counters : ctx -> unit
+
+(** Random.init: new Philox key and the step counter back to 0.  Without it the counter runs
+    on across [mcmc_array] calls on one context, as the reference's global Random state does. *)
+val reseed : ctx -> int64 -> unit
 val get_counters : ctx -> int * int
 
 (** Batched Mcmc.mcmc_array ?nbin ?nskip n (mcmc.mli:70-72): [start] is D x N; returns the

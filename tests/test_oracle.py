@@ -47,10 +47,11 @@ def test_portable_math_accuracy(oracle):
 
 
 def test_normal_accuracy_and_exact_symmetry(oracle):
-    """Spec v5 normal: within 5e-14 of the exact quantile -sqrt(2) erfinv(1 - 2u) of
-    u = (2 (w mod 2^31) + 1) 2^-33 (sign from bit 31), across every octave of u including the
-    extreme words, and exactly antisymmetric under w -> w ^ 2^31, which makes the proposal
-    exactly symmetric."""
+    """Spec v6 normal: within 7.5e-10 of the exact quantile -sqrt(2) erfinv(1 - 2u) of
+    u = (2 (w mod 2^31) + 1) 2^-33 (sign from bit 31) -- about one step of the grid the
+    quantisation of u puts on z (>= 5.8e-10) -- across every octave of u including the extreme
+    words, and exactly antisymmetric under w -> w ^ 2^31, which makes the proposal exactly
+    symmetric."""
     mp = pytest.importorskip("mpmath")
     mp.mp.dps = 40
     rng = np.random.default_rng(3)
@@ -65,7 +66,7 @@ def test_normal_accuracy_and_exact_symmetry(oracle):
         u = (2 * mp.mpf(w & 0x7FFFFFFF) + 1) / mp.mpf(2) ** 33
         q = mp.sqrt(2) * mp.erfinv(2 * u - 1)
         ref = -q if (w >> 31) else q
-        assert abs(mp.mpf(z) - ref) <= 5e-14, (w, z, ref)
+        assert abs(mp.mpf(z) - ref) <= 7.5e-10, (w, z, ref)
         assert oracle.normal(w ^ 0x80000000) == -z
 
 
@@ -406,9 +407,9 @@ def test_evidence_weights_blocked_fold_close_to_sequential(oracle):
 
 
 def test_device_normal_formulation_matches_oracle(oracle):
-    """The kernels' pnormal (mcg_math.h) reaches the same spec by bit tricks: segment from the high
-    word of double(v), x = t/32 from the low fraction bits, Horner in x with the 32^k-scaled
-    table of mcg_tables.h.  Restated here in exact rational arithmetic (one rounding per fma) and
+    """The kernels' pnormal (mcg_math.h) reaches the same spec by bit tricks: table row from bits
+    15..24 of the high word of double(v) (the table is stored rotated by one octave), x = t/32
+    from the low fraction bits, Horner in x with the 32^k-scaled table of mcg_tables.h.  Restated here in exact rational arithmetic (one rounding per fma) and
     compared with the oracle's Horner in t, word for word, over every octave of v."""
     import re
     import struct
@@ -426,11 +427,11 @@ def test_device_normal_formulation_matches_oracle(oracle):
         v = ((w << 1) | 1) & 0xFFFFFFFF
         bits = struct.unpack("<Q", struct.pack("<d", float(v)))[0]
         hi, lo = bits >> 32, bits & 0xFFFFFFFF
-        seg = (hi >> 15) - (1023 << 5)
+        seg = (hi >> 15) & 1023                       # row: exponent low bits, then j
         x = struct.unpack("<d", struct.pack("<Q", (((hi & 0x7FFF) | 0x3FF00000) << 32) | lo))[0] - 1.0
-        c = tab[3 * seg:3 * seg + 3]
-        p = fma(c[0][0], x, c[0][1])
-        for a in (c[1][0], c[1][1], c[2][0], c[2][1]):
+        c32, c10 = tab[seg], tab[1024 + seg]          # structure-of-arrays rows
+        p = fma(c32[0], x, c32[1])
+        for a in (c10[0], c10[1]):
             p = fma(p, x, a)
         return -p if w >> 31 else p
 
