@@ -189,15 +189,14 @@ __device__ __forceinline__ double psqrt(double a) {
   return a * y;
 }
 
-// standard normal from one 32-bit word (spec v6): the sign is bit 31; the other
+// standard normal from one 32-bit word (spec v7): the sign is bit 31; the other
 // 31 bits give v = 2w + 1 (odd), u = v 2^-33 in (0, 1/2).  double(v) = 2^E (1 + f) is exact; the
-// segment is (E, top kNrmS bits of f), its row bits 15..24 of the high word; the rest of f, put under
-// the exponent of 1.0, gives 1 + t/32 exactly, so x = t/32 with one exact subtraction, and
-// z = -+ p_seg(x): the segment's cubic in t (oracle/gen_tables.py), stored scaled by 32^k so that
-// Horner in x rounds exactly like the oracle's Horner in t.  Exactly symmetric: flipping bit 31
-// negates z.  `tab` points at kNrmTab or at a copy staged in LDS: (d3, d2) of the segment at row
-// r, (d1, d0) at row kNrmSeg + r -- two 16-B gathers from one address (constant offset), each on
-// LDS slot r mod 16.
+// segment is (E, top kNrmS bits of f), its row bits 15..24 of the high word; the rest of f, put
+// under the exponent of 1.0, is x' = 1 + t/32 exactly, and z = -+ p_seg(x'): the segment's cubic
+// in x' (oracle/gen_tables.py), the same coefficients and Horner as the oracle's.  Exactly
+// symmetric: flipping bit 31 negates z.  `tab` points at kNrmTab or at a copy staged in LDS:
+// (e3, e2) of the segment at row r, (e1, e0) at row kNrmSeg + r -- two 16-B gathers from one
+// address (constant offset), each on LDS slot r mod 16.
 static_assert(kNrmS == 5 && kNrmDeg == 3, "pnormal is written for 32 segments per octave, degree 3");
 constexpr int kNrmSeg = 32 << kNrmS;
 static_assert(kNrmTabN == 2 * kNrmSeg, "normal table: two rows per segment");
@@ -230,7 +229,7 @@ __device__ __forceinline__ NrmPending pnormal_issue(uint32_t w, const double2* t
   // both gathers take the table base as an immediate offset
   const double2* c = tab + ((hi >> 15) & (uint32_t)(kNrmSeg - 1));
   NrmPending r;
-  r.x = __hiloint2double((int)nrm_frac_hi(hi), (int)lo) - 1.0;
+  r.x = __hiloint2double((int)nrm_frac_hi(hi), (int)lo);        // x' = 1 + t/32, exact
   r.c32 = c[0];
   r.c10 = c[kNrmSeg];
   r.sign = w;

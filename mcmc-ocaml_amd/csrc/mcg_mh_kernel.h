@@ -298,7 +298,10 @@ struct AccumCfg {
 #define MCG_MH_MIN_WAVES 1
 #endif
 
-template <int D, int P, int LIK, int PROP, bool UNI>
+// UNI: 0 = constants through pointers; 1 = isotropic proposal scale and one box [lo, hi] for
+// every dim as kernel arguments; 2 = the same with a symmetric box [-h, h], tested as |y| <= h
+// (one compare per dim; the same predicate as lo <= y <= hi for every double, NaN included)
+template <int D, int P, int LIK, int PROP, int UNI>
 __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs a) {
   using L = Layout<D, P>;
   constexpr bool kSeparable = separable<LIK, PROP>();
@@ -494,7 +497,8 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
       double A[L::NA];
 #pragma unroll
       for (int j = 0; j < L::NA; ++j) A[j] = 0.0;
-      int inb = 1;
+      // box test as a lane predicate (SGPR masks), one VGPR bit for the cross-lane AND
+      bool ok = true;
       const bool box = a.prior_kind != MCG_PRIOR_FLAT;
       // the lane's Philox calls of this step (c2 = call index sub + P i) advanced together
       u32x4 wl[L::NCL];
@@ -527,11 +531,13 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
             const double e = yv - (UNI ? rc_m[4 * i + k] : qlik[d]);
             A[i % L::NA] = fma(e, e, A[i % L::NA]);
           }
-          {
-            // branch-free closed-box test: the host stores an OPEN box as its closed equivalent
-            // [nextafter(lo, +inf), nextafter(hi, -inf)] and pads FLAT priors with (-inf, inf)
+          // branch-free closed-box test: the host stores an OPEN box as its closed equivalent
+          // [nextafter(lo, +inf), nextafter(hi, -inf)] and pads FLAT priors with (-inf, inf)
+          if constexpr (UNI == 2) {
+            ok = ok & (__builtin_fabs(yv) <= a.uni_hi);
+          } else {
             const double lo = UNI ? a.uni_lo : qpri[d], hi = UNI ? a.uni_hi : qpri[D + d];
-            inb &= (int)(yv >= lo) & (int)(yv <= hi);
+            ok = ok & (yv >= lo) & (yv <= hi);
           }
         }
       }
@@ -547,7 +553,7 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
           lly = (UNI ? rc_c : qlik[D + 2]) - 0.5 * qq * qq;
         }
       }
-      inb = and_lanes<P>(inb);
+      const int inb = and_lanes<P>(ok ? 1 : 0);
       lpy = !box ? 0.0 : (inb ? (UNI ? rc_lp : qpri[2 * D]) : -__builtin_inf());
     } else {
       // ---- proposal (jump_proposal, mcmc.ml:41) ----
@@ -782,12 +788,16 @@ hipError_t launch_mh(const MhArgs& a, int64_t nthreads, hipStream_t s) {
   const int64_t grid = (nthreads + block - 1) / block;
   constexpr int lds = AccumCfg<D, P>::kLdsBytes;
   if constexpr (separable<LIK, PROP>()) {
+    if (a.uni && a.uni_lo == -a.uni_hi) {
+      hipLaunchKernelGGL((mh_kernel<D, P, LIK, PROP, 2>), dim3((unsigned)grid), dim3(block), lds, s, a);
+      return hipGetLastError();
+    }
     if (a.uni) {
-      hipLaunchKernelGGL((mh_kernel<D, P, LIK, PROP, true>), dim3((unsigned)grid), dim3(block), lds, s, a);
+      hipLaunchKernelGGL((mh_kernel<D, P, LIK, PROP, 1>), dim3((unsigned)grid), dim3(block), lds, s, a);
       return hipGetLastError();
     }
   }
-  hipLaunchKernelGGL((mh_kernel<D, P, LIK, PROP, false>), dim3((unsigned)grid), dim3(block), lds, s, a);
+  hipLaunchKernelGGL((mh_kernel<D, P, LIK, PROP, 0>), dim3((unsigned)grid), dim3(block), lds, s, a);
   return hipGetLastError();
 }
 

@@ -147,24 +147,23 @@ double or_sqrt(double a) {
   return a * y;
 }
 
-/* standard normal from one 32-bit word (spec v6): z = -+ q(u), the sign from bit 31, u = v 2^-33
+/* standard normal from one 32-bit word (spec v7): z = -+ q(u), the sign from bit 31, u = v 2^-33
    with v = 2 (w mod 2^31) + 1, and q the spec's piecewise-polynomial normal quantile on (0, 1/2):
-   for v = 2^E (1 + f), segment (E, j = floor(32 f)), t = 32 f - j in [0, 1), Horner in t of the
-   segment's four coefficients (or_tables.h, highest first) with fma.  Replaces Leva's
-   ratio-of-uniforms Stats.draw_gaussian (stats.ml:113-124): any exactly symmetric proposal keeps
-   MH exact, and the table is within 7.5e-10 of the exact quantile (about one step of the grid
-   the 2^-32 quantisation of u puts on z). */
+   for v = 2^E (1 + f), segment (E, j = floor(32 f)), t = 32 f - j in [0, 1), Horner (fma) in
+   x' = 1 + t/32 of the segment's four coefficients (or_tables.h, highest first).  Replaces
+   Leva's ratio-of-uniforms Stats.draw_gaussian (stats.ml:113-124): any exactly symmetric
+   proposal keeps MH exact, and the table is within 7.5e-10 of the exact quantile (about one
+   step of the grid the 2^-32 quantisation of u puts on z). */
 double or_normal(uint32_t w) {
   uint32_t v = 2u * (w & 0x7FFFFFFFu) + 1u;
   int E = 31 - __builtin_clz(v);
   double fv = ldexp((double)v, -E);                /* exact, in [1, 2) */
-  double s32 = (fv - 1.0) * 32.0;                  /* exact */
-  int j = (int)s32;
-  double t = s32 - (double)j;                      /* exact, in [0, 1) */
+  int j = (int)((fv - 1.0) * 32.0);                /* exact product, then floor */
+  double xp = fv - ldexp((double)j, -5);           /* exact: 1 + t/32 */
   const double(*c)[2] = &or_nrmtab[2 * (E * 32 + j)];
-  double p = fma(c[0][0], t, c[0][1]);
-  p = fma(p, t, c[1][0]);
-  p = fma(p, t, c[1][1]);
+  double p = fma(c[0][0], xp, c[0][1]);
+  p = fma(p, xp, c[1][0]);
+  p = fma(p, xp, c[1][1]);
   return (w >> 31) ? -p : p;
 }
 

@@ -84,11 +84,12 @@ def test_c2_mini_bit_exact(oracle, T, lanes):
 
 
 @pytest.mark.parametrize("lanes", [1, 4])
-@pytest.mark.parametrize("case", ["per_dim", "flat", "open_box"])
+@pytest.mark.parametrize("case", ["per_dim", "flat", "open_box", "asym_box"])
 def test_fused_step_constant_forms_bit_exact(oracle, T, lanes, case):
-    """The fused step's two constant forms: per-dim proposal scales / per-dim box bounds (loaded
-    every step) and one scale + one box for all dims (kernel arguments, register-resident
-    likelihood constants), with FLAT and OPEN_BOX priors."""
+    """The fused step's constant forms: per-dim proposal scales / per-dim box bounds (loaded
+    every step); one scale + one box [lo, hi] for all dims (kernel arguments, register-resident
+    likelihood constants); and the symmetric box [-h, h] tested as |y| <= h -- with FLAT,
+    OPEN_BOX and asymmetric priors, and chains started near the faces so the box rejects."""
     lik, pri, prop, mu, sg = c2_model(T)
     D, N = 32, 128
     if case == "per_dim":
@@ -96,8 +97,10 @@ def test_fused_step_constant_forms_bit_exact(oracle, T, lanes, case):
         pri = T.box(-3.0 - np.arange(D) / D, 3.0 + np.arange(D) / D)
     elif case == "flat":
         pri = T.flat_prior()
-    else:
+    elif case == "open_box":
         pri = T.box(-2.5 * np.ones(D), 2.5 * np.ones(D), open_=True)
+    else:
+        pri = T.box(-2.5 * np.ones(D), 2.45 * np.ones(D))
     x0 = np.clip(np.random.default_rng(6).normal(mu[:, None], sg[:, None], size=(D, N)), -2.4, 2.4)
     g = run_gpu(lik, pri, prop, x0, 9, nbin=5, nskip=1, n_rec=120, lanes=lanes)
     o = run_oracle(oracle, lik, pri, prop, x0, 9, 5, 1, 120)

@@ -47,7 +47,7 @@ def test_portable_math_accuracy(oracle):
 
 
 def test_normal_accuracy_and_exact_symmetry(oracle):
-    """Spec v6 normal: within 7.5e-10 of the exact quantile -sqrt(2) erfinv(1 - 2u) of
+    """Spec v7 normal: within 7.5e-10 of the exact quantile -sqrt(2) erfinv(1 - 2u) of
     u = (2 (w mod 2^31) + 1) 2^-33 (sign from bit 31) -- about one step of the grid the
     quantisation of u puts on z (>= 5.8e-10) -- across every octave of u including the extreme
     words, and exactly antisymmetric under w -> w ^ 2^31, which makes the proposal exactly
@@ -408,9 +408,11 @@ def test_evidence_weights_blocked_fold_close_to_sequential(oracle):
 
 def test_device_normal_formulation_matches_oracle(oracle):
     """The kernels' pnormal (mcg_math.h) reaches the same spec by bit tricks: table row from bits
-    15..24 of the high word of double(v) (the table is stored rotated by one octave), x = t/32
-    from the low fraction bits, Horner in x with the 32^k-scaled table of mcg_tables.h.  Restated here in exact rational arithmetic (one rounding per fma) and
-    compared with the oracle's Horner in t, word for word, over every octave of v."""
+    15..24 of the high word of double(v) (the table is stored rotated by one octave), x' = 1 + t/32
+    from the low fraction bits under the exponent of 1.0 (no subtraction), Horner in x' with the
+    structure-of-arrays table of mcg_tables.h.  Restated here in exact rational arithmetic (one
+    rounding per fma) and compared with the oracle's Horner in x' (computed there as
+    fv - j/32), word for word, over every octave of v."""
     import re
     import struct
     from fractions import Fraction as Fr
@@ -428,7 +430,7 @@ def test_device_normal_formulation_matches_oracle(oracle):
         bits = struct.unpack("<Q", struct.pack("<d", float(v)))[0]
         hi, lo = bits >> 32, bits & 0xFFFFFFFF
         seg = (hi >> 15) & 1023                       # row: exponent low bits, then j
-        x = struct.unpack("<d", struct.pack("<Q", (((hi & 0x7FFF) | 0x3FF00000) << 32) | lo))[0] - 1.0
+        x = struct.unpack("<d", struct.pack("<Q", (((hi & 0x7FFF) | 0x3FF00000) << 32) | lo))[0]
         c32, c10 = tab[seg], tab[1024 + seg]          # structure-of-arrays rows
         p = fma(c32[0], x, c32[1])
         for a in (c10[0], c10[1]):
