@@ -64,8 +64,15 @@ __device__ __forceinline__ void transpose_quadrants(double* v) {
 #ifndef MCG_FC_MIN_WAVES
 #define MCG_FC_MIN_WAVES 2   // occupancy 2 with a few spills beats occupancy 1 (+50%, C5)
 #endif
-// UNI: one proposal scale and one box for every dim (MhArgs::uni): scalars, no per-step loads
-template <int D, bool UNI>
+#ifndef MCG_FC_NRM_BATCH
+// the MH kernel's batched gathers (MCG_NRM_BATCH) cost this kernel 5 % (C5 4.86e9 -> 4.63e9, A/B
+// on one box): at 256 VGPRs the 32 extra in-flight registers spill
+#define MCG_FC_NRM_BATCH 0
+#endif
+
+// UNI: one proposal scale and one box for every dim (MhArgs::uni): scalars, no per-step loads;
+// UNI == 2: the box is symmetric, [-h, h], tested as |y| <= h (mcg_mh_kernel.h)
+template <int D, int UNI>
 __global__ void __launch_bounds__(256, MCG_FC_MIN_WAVES) mh_fullcov_kernel(const MhArgs a) {
   using F = FcLayout<D>;
   constexpr int NL = F::NKB;
@@ -177,16 +184,20 @@ __global__ void __launch_bounds__(256, MCG_FC_MIN_WAVES) mh_fullcov_kernel(const
     gdouble* qprop = (gdouble*)a.prop;
     asm volatile("" : "+s"(qlik), "+s"(qpri), "+s"(qprop));
     // ---- proposal: y = x + s z (mcmc.ml:41); calls 4m + q, transposed to the lane's dims ----
-    int inb = 1;
+    bool ok = true;
 #pragma unroll
     for (int m = 0; m < F::NM; ++m) {
       asm volatile("" ::: "memory");
       const u32x4 w = rng(gid, tlo, (uint32_t)(4 * m + q), TAG_MH, thi);
       double v[4];
+#if MCG_FC_NRM_BATCH
+      pnormal4_lds(w, s_nt, v);
+#else
       v[0] = pnormal(w.x, s_nt);
       v[1] = pnormal(w.y, s_nt);
       v[2] = pnormal(w.z, s_nt);
       v[3] = pnormal(w.w, s_nt);
+#endif
       transpose_quadrants(v);                 // v[k'] = z[16 m + 4 k' + q]
 #pragma unroll
       for (int k2 = 0; k2 < 4; ++k2) {
@@ -194,7 +205,8 @@ __global__ void __launch_bounds__(256, MCG_FC_MIN_WAVES) mh_fullcov_kernel(const
         const int d = dim(kb);
         const double yv = fma(UNI ? a.uni_s : qprop[d], v[k2], x[kb]);
         y[kb] = yv;
-        inb &= (int)(yv >= (UNI ? a.uni_lo : qpri[d])) & (int)(yv <= (UNI ? a.uni_hi : qpri[D + d]));
+        if constexpr (UNI == 2) ok = ok & (__builtin_fabs(yv) <= a.uni_hi);
+        else ok = ok & (yv >= (UNI ? a.uni_lo : qpri[d])) & (yv <= (UNI ? a.uni_hi : qpri[D + d]));
       }
     }
     // ---- log-likelihood: e = U (y - mu) on the matrix cores, S = sum e_i^2 ----
@@ -218,6 +230,7 @@ __global__ void __launch_bounds__(256, MCG_FC_MIN_WAVES) mh_fullcov_kernel(const
     const double cs = b + __shfl_xor(b, 32, 64);
     const double S = cs + __shfl_xor(cs, 16, 64);
     const double lly = qlik[D] - 0.5 * S;
+    int inb = ok ? 1 : 0;
     inb &= __shfl_xor(inb, 32, 64);
     inb &= __shfl_xor(inb, 16, 64);
     const double lpy = a.prior_kind == MCG_PRIOR_FLAT ? 0.0 : (inb ? qpri[2 * D] : -__builtin_inf());
@@ -279,8 +292,9 @@ __global__ void __launch_bounds__(256, MCG_FC_MIN_WAVES) mh_fullcov_kernel(const
 template <int D>
 hipError_t launch_mh_fullcov(const MhArgs& a, int64_t nthreads, hipStream_t s) {
   const int64_t grid = (nthreads + 255) / 256;          // nthreads = 4 N: 64 chains per block
-  if (a.uni) hipLaunchKernelGGL((mh_fullcov_kernel<D, true>), dim3((unsigned)grid), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((mh_fullcov_kernel<D, false>), dim3((unsigned)grid), dim3(256), 0, s, a);
+  if (a.uni && a.uni_lo == -a.uni_hi) hipLaunchKernelGGL((mh_fullcov_kernel<D, 2>), dim3((unsigned)grid), dim3(256), 0, s, a);
+  else if (a.uni) hipLaunchKernelGGL((mh_fullcov_kernel<D, 1>), dim3((unsigned)grid), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((mh_fullcov_kernel<D, 0>), dim3((unsigned)grid), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

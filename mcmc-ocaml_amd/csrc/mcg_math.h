@@ -248,6 +248,49 @@ __device__ __forceinline__ double pnormal(uint32_t w, const double2* tab) {
   return pnormal_finish(pnormal_issue(w, tab));
 }
 
+// The four normals of one Philox call with their eight table gathers issued back to back and
+// one LDS wait (the compiler, short of registers, otherwise issues two gathers, waits, and
+// evaluates one normal at a time).  `tab` must be the LDS copy of kNrmTab.  The same operations
+// as pnormal, so the same values.
+__device__ __forceinline__ void pnormal4_lds(const u32x4 w, const double2* tab, double z[4]) {
+  const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+  uint32_t ad[4];
+  double xp[4];
+  const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) double2*)tab;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const double dv = (double)nrm_odd(ww[k]);
+    const uint32_t hi = (uint32_t)__double2hiint(dv);
+    ad[k] = base + ((hi >> 15) & (uint32_t)(kNrmSeg - 1)) * 16u;
+    xp[k] = __hiloint2double((int)nrm_frac_hi(hi), __double2loint(dv));
+  }
+  double2 a0, a1, a2, a3, b0, b1, b2, b3;
+  static_assert(kNrmSeg * 16 == 16384, "second half of the table at offset 16384");
+  asm volatile(
+      "ds_read_b128 %0, %8\n\t"
+      "ds_read_b128 %4, %8 offset:16384\n\t"
+      "ds_read_b128 %1, %9\n\t"
+      "ds_read_b128 %5, %9 offset:16384\n\t"
+      "ds_read_b128 %2, %10\n\t"
+      "ds_read_b128 %6, %10 offset:16384\n\t"
+      "ds_read_b128 %3, %11\n\t"
+      "ds_read_b128 %7, %11 offset:16384\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3), "=&v"(b0), "=&v"(b1), "=&v"(b2), "=&v"(b3)
+      : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3])
+      : "memory");
+  const double2 A[4] = {a0, a1, a2, a3}, B[4] = {b0, b1, b2, b3};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    NrmPending q;
+    q.x = xp[k];
+    q.c32 = A[k];
+    q.c10 = B[k];
+    q.sign = ww[k];
+    z[k] = pnormal_finish(q);
+  }
+}
+
 // log1p(r), r in [0,1] (Goldberg: r * log(1+r) / ((1+r)-1)); log-sum-exp on the portable
 // exp/log.  Drives the running nested-sampling estimate (nested.ml:139-142).
 __device__ __forceinline__ double plog1p(double r, const double2* tab = kLogTab) {

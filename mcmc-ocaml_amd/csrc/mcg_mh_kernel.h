@@ -294,6 +294,10 @@ struct AccumCfg {
 #define MCG_CONST_MODE 1   // model constants of the fused step: 0 generic loads, 1 global, 2 LDS
 #endif
 
+#ifndef MCG_NRM_BATCH
+#define MCG_NRM_BATCH 1    // 1: the four normals of a Philox call gather together (one LDS wait)
+#endif
+
 #ifndef MCG_MH_MIN_WAVES
 #define MCG_MH_MIN_WAVES 1
 #endif
@@ -513,10 +517,14 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
         const int cc = sub + P * i;
         const u32x4 w = wl[i];
         double z[4];
+#if MCG_NRM_BATCH
+        pnormal4_lds(w, s_nt, z);
+#else
         z[0] = pnormal(w.x, s_nt);
         z[1] = pnormal(w.y, s_nt);
         z[2] = pnormal(w.z, s_nt);
         z[3] = pnormal(w.w, s_nt);
+#endif
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           if (!L::valid(sub, i, k)) continue;
