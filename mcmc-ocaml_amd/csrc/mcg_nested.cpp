@@ -137,11 +137,18 @@ class EvFold {
     const int64_t ilive = ntot - n_;
     View v{this, ll, ilive, 0.0};
     v.ntot = ntot;
-    // the final live points reuse the last dead iteration's log_dv (nested.ml:104), for every k
+    // the final live points each get 1/nlive of the volume that remained before the last
+    // retirement: nested.ml:104 is log_vol_fraction + log X_(ilive-1), X_(ilive-1) the product
+    // of the first ilive-1 volume reductions.  For k > 1 the same X is the generation prefix
+    // (not the last dead point's own element, which divides by its live count nlive - k + 1
+    // and so would over-weight the live points by nlive / (nlive - k + 1))
     if (k_ == 1) {
       v.ldv_live = std::log(1.0 / (double)n_) + (double)(ilive - 1) * std::log1p(-1.0 / (double)n_);
+    } else if (ilive > 0) {
+      const int64_t m = ilive - 1, j = m % k_, g = m / k_;
+      v.ldv_live = std::log(1.0 / (double)n_) + ((double)g * prefix_[(size_t)k_] + prefix_[(size_t)j]);
     } else {
-      v.ldv_live = ilive > 0 ? v.ldv_dead(ilive - 1) : std::log(1.0 / (double)n_);
+      v.ldv_live = std::log(1.0 / (double)n_);
     }
     fold_blocks(v, (ntot + kEvBlock - 1) / kEvBlock, threads_);
     parallel_for(wdone_, ntot, threads_, [&](int64_t m) { wts[m] = v.weight(m); });

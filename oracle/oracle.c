@@ -1248,7 +1248,6 @@ void or_evidence_weights(int64_t n, int64_t nlive, int64_t k, const double* ll,
     if (++it % OR_EV_BLOCK == 0 || it == n) { \
       low = or_log_sum_logs(low, blow); high = or_log_sum_logs(high, bhigh); \
       blow = -INFINITY; bhigh = -INFINITY; } } while (0)
-  double last_dv = 0.0;
   for (int64_t i = 0; i < ilive; ++i) {
     int64_t j = i % k, g = i / k;
     double logx = (double)g * prefix[k] + prefix[j];
@@ -1258,15 +1257,18 @@ void or_evidence_weights(int64_t n, int64_t nlive, int64_t k, const double* ll,
     OR_EV_FOLD(dlow, dhigh);
     wts[i] = or_log_sum_logs(wts[i], log_half + dlow);
     wts[i + 1] = or_log_sum_logs(wts[i + 1], log_half + dhigh);
-    last_dv = log_dv;
   }
-  /* the final live points reuse the log_dv of the last dead iteration (nested.ml:104: the
-     reference's i = ilive - 1 volume element, for every k); with no dead point at all, k = 1
-     keeps the reference's formula at i = -1 and k > 1 shares the whole prior volume */
+  /* the final live points each get 1/nlive of the volume that remained before the last
+     retirement (nested.ml:104: log_vol_fraction + log X_(ilive-1)); for k > 1 that X is the
+     generation prefix of the first ilive - 1 retirements (not the last dead point's own element,
+     which divides by its live count nlive - k + 1); with no dead point at all, k = 1 keeps the
+     reference's formula at i = -1 and k > 1 shares the whole prior volume */
   double log_dv;
   if (k == 1) log_dv = log(1.0 / (double)nlive) + (double)(ilive - 1) * log1p(-1.0 / (double)nlive);
-  else if (ilive > 0) log_dv = last_dv;
-  else log_dv = log(1.0 / (double)nlive);
+  else if (ilive > 0) {
+    int64_t m = ilive - 1, j = m % k, g = m / k;
+    log_dv = log(1.0 / (double)nlive) + ((double)g * prefix[k] + prefix[j]);
+  } else log_dv = log(1.0 / (double)nlive);
   for (int64_t i = ilive; i < n; ++i) {
     double dlow = log_dv + ll[i - 1], dhigh = log_dv + ll[i];
     OR_EV_FOLD(dlow, dhigh);

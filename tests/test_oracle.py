@@ -303,9 +303,9 @@ def test_evidence_weights_k1_matches_reference_formula(oracle):
 @pytest.mark.parametrize("k", [2, 5])
 def test_evidence_weights_k_generations_restated(oracle, k):
     """k > 1 generalisation of nested.ml:81-120, restated in Python: dead point i was retired
-    with nlive - (i mod k) live points from volume X_i = (i div k) L_k + prefix[i mod k]; the
-    final live points reuse the last dead iteration's log_dv, as the reference does at k = 1
-    (nested.ml:104)."""
+    with nlive - (i mod k) live points from volume X_i = (i div k) L_k + prefix[i mod k]; each
+    final live point gets 1/nlive of X_(ilive-1), the volume before the last retirement, as the
+    reference's log_vol_fraction + (ilive - 1) log_reduction_frac does at k = 1 (nested.ml:104)."""
     rng = np.random.default_rng(9 + k)
     nlive = 12
     ll = np.sort(rng.normal(size=61))
@@ -334,7 +334,8 @@ def test_evidence_weights_k_generations_restated(oracle, k):
         dl, dh = ldv + ll[i], ldv + ll[i + 1]
         low, high = lse(low, dl), lse(high, dh)
         wts[i] = lse(wts[i], lh + dl); wts[i + 1] = lse(wts[i + 1], lh + dh)
-    ldv = ldv_dead(ilive - 1)
+    m = ilive - 1
+    ldv = math.log(1.0 / nlive) + ((m // k) * prefix[k] + prefix[m % k])
     for i in range(ilive, n):
         dl, dh = ldv + ll[i - 1], ldv + ll[i]
         low, high = lse(low, dl), lse(high, dh)
