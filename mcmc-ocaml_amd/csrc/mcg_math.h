@@ -119,6 +119,11 @@ __device__ __forceinline__ uint32_t randint(uint32_t w0, uint32_t w1, uint32_t n
   return (uint32_t)__umul64hi(u, (uint64_t)n);
 }
 
+// A 64-bit constant materialised in an SGPR pair at its point of use (two s_mov): left to the
+// compiler, a kernel whose loop calls plog / pexp keeps every polynomial coefficient in a VGPR
+// pair for its whole life (~30 VGPRs in the MH kernel), which costs occupancy.  Same values.
+#define MCG_SCONST(c) ([&] { double v_ = (c); asm volatile("" : "+s"(v_)); return v_; }())
+
 // log (spec v4): mantissa rounded to 8 bits, j = round(256 (m - 1)) in [0, 256];
 // cells j >= kLogSplit are halved (m/2, k+1); d = m - m_j exact, r = d RN(1/m_j), |r| <= 2^-9,
 // degree-6 log1p.  All reduction steps are 32-bit integer ops on the high word.
@@ -138,13 +143,13 @@ __device__ __forceinline__ double plog(double x, const double2* tab) {
   const double d = m - mj;
   const double r = d * cl.x;
   const double z = r * r;
-  double q = fma(r, -0x1.5555555555555p-3, 0x1.999999999999ap-3);
+  double q = fma(r, MCG_SCONST(-0x1.5555555555555p-3), MCG_SCONST(0x1.999999999999ap-3));
   q = fma(r, q, -0.25);
-  q = fma(r, q, 0x1.5555555555555p-2);
+  q = fma(r, q, MCG_SCONST(0x1.5555555555555p-2));
   q = fma(r, q, -0.5);
   const double p = fma(z, q, r);
   const double dk = (double)k;
-  return fma(dk, ln2_hi, cl.y) + fma(dk, ln2_lo, p);
+  return fma(dk, MCG_SCONST(ln2_hi), cl.y) + fma(dk, MCG_SCONST(ln2_lo), p);
 }
 
 __device__ __forceinline__ double plog(double x) { return plog(x, kLogTab); }
@@ -155,19 +160,19 @@ __device__ __forceinline__ double pexp(double x) {
   const double ln2_hi = 0x1.62e42fee00000p-1, ln2_lo = 0x1.a39ef35793c76p-33;
   bool tiny = !(x > -708.0);
   x = tiny ? 0.0 : x;
-  double kd = floor(fma(x, inv_ln2, 0.5));
-  double r = fma(-kd, ln2_hi, x);
-  r = fma(-kd, ln2_lo, r);
-  double p = 0x1.1eed8eff8d898p-29;
-  p = fma(p, r, 0x1.ae64567f544e4p-26);
-  p = fma(p, r, 0x1.27e4fb7789f5cp-22);
-  p = fma(p, r, 0x1.71de3a556c734p-19);
-  p = fma(p, r, 0x1.a01a01a01a01ap-16);
-  p = fma(p, r, 0x1.a01a01a01a01ap-13);
-  p = fma(p, r, 0x1.6c16c16c16c17p-10);
-  p = fma(p, r, 0x1.1111111111111p-7);
-  p = fma(p, r, 0x1.5555555555555p-5);
-  p = fma(p, r, 0x1.5555555555555p-3);
+  double kd = floor(fma(x, MCG_SCONST(inv_ln2), 0.5));
+  double r = fma(-kd, MCG_SCONST(ln2_hi), x);
+  r = fma(-kd, MCG_SCONST(ln2_lo), r);
+  double p = MCG_SCONST(0x1.1eed8eff8d898p-29);
+  p = fma(p, r, MCG_SCONST(0x1.ae64567f544e4p-26));
+  p = fma(p, r, MCG_SCONST(0x1.27e4fb7789f5cp-22));
+  p = fma(p, r, MCG_SCONST(0x1.71de3a556c734p-19));
+  p = fma(p, r, MCG_SCONST(0x1.a01a01a01a01ap-16));
+  p = fma(p, r, MCG_SCONST(0x1.a01a01a01a01ap-13));
+  p = fma(p, r, MCG_SCONST(0x1.6c16c16c16c17p-10));
+  p = fma(p, r, MCG_SCONST(0x1.1111111111111p-7));
+  p = fma(p, r, MCG_SCONST(0x1.5555555555555p-5));
+  p = fma(p, r, MCG_SCONST(0x1.5555555555555p-3));
   p = fma(p, r, 0.5);
   p = fma(p, r, 1.0);
   p = fma(p, r, 1.0);

@@ -531,12 +531,13 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
           const int d = 4 * cc + k;
           const double yv = fma(UNI ? a.uni_s : qprop[d], z[k], x[4 * i + k]);
           y[4 * i + k] = yv;
+          const double rcm = UNI ? rc_m[4 * i + k] : 0.0, rci = UNI ? rc_i[4 * i + k] : 0.0;
           if constexpr (LIK == MCG_LIK_DIAG_GAUSS) {
-            const double e = UNI ? fma(yv, rc_i[4 * i + k], -rc_m[4 * i + k])
+            const double e = UNI ? fma(yv, rci, -rcm)
                                  : fma(yv, qlik[D + d], -qlik[d]);   // (y - mu)/sigma
             A[i % L::NA] = fma(e, e, A[i % L::NA]);
           } else if constexpr (LIK == MCG_LIK_GAUSS_SHELL) {
-            const double e = yv - (UNI ? rc_m[4 * i + k] : qlik[d]);
+            const double e = yv - (UNI ? rcm : qlik[d]);
             A[i % L::NA] = fma(e, e, A[i % L::NA]);
           }
           // branch-free closed-box test: the host stores an OPEN box as its closed equivalent
