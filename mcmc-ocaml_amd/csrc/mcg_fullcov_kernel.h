@@ -61,26 +61,40 @@ __device__ __forceinline__ void transpose_quadrants(double* v) {
   swap16(v[2], v[3]);
 }
 
-#ifndef MCG_FC_MIN_WAVES
-#define MCG_FC_MIN_WAVES 2   // occupancy 2 with a few spills beats occupancy 1 (+50%, C5)
-#endif
 #ifndef MCG_FC_NRM_BATCH
-// the MH kernel's batched gathers (MCG_NRM_BATCH) cost this kernel 5 % (C5 4.86e9 -> 4.63e9, A/B
-// on one box): at 256 VGPRs the 32 extra in-flight registers spill
-#define MCG_FC_NRM_BATCH 0
+#define MCG_FC_NRM_BATCH 1   // the four normals of a Philox call gather together (one LDS wait)
 #endif
 
+// 512-thread workgroups, one per CU: eight waves = two per SIMD, sharing one copy of the tables
+// (the proposed point's 64 KB LDS park, below, leaves no room for two workgroups per CU)
+constexpr int kFcBlock = 512;
+
+// Per step: the lane's four Philox calls one at a time -> 4 normals -> quadrant
+// transpose -> 4 proposed coordinates; each coordinate's residual r = y - mu goes straight into
+// the matrix core (row blocks ib with 4 ib <= kb, four accumulators, kb ascending per block, so
+// every e_i is still the oracle's fma chain), and y itself is parked in LDS until the accept
+// test.  The proposed point thus never occupies registers: chain state, Welford accumulators
+// and the four MFMA accumulators fit the 256 registers of two waves per SIMD without spilling.
 // UNI: one proposal scale and one box for every dim (MhArgs::uni): scalars, no per-step loads;
 // UNI == 2: the box is symmetric, [-h, h], tested as |y| <= h (mcg_mh_kernel.h)
 template <int D, int UNI>
-__global__ void __launch_bounds__(256, MCG_FC_MIN_WAVES) mh_fullcov_kernel(const MhArgs a) {
+__global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a) {
   using F = FcLayout<D>;
   constexpr int NL = F::NKB;
   __shared__ double2 s_lt[kLogTabN];
   __shared__ double2 s_nt[kNrmTabN];
   __shared__ double s_u[F::NFRAG * 64];
+  // mu by lane quadrant, [q][kb] = mu[4 kb + q], then the likelihood normaliser C and the prior
+  // box's log density (per-step global loads of these were in-order vmcnt waits on every step)
+  __shared__ double s_mu[D + 2];
+  __shared__ double s_y[NL * kFcBlock];                  // proposed point, [kb][thread]
   for (int i = threadIdx.x; i < kLogTabN; i += blockDim.x) s_lt[i] = kLogTab[i];
   for (int i = threadIdx.x; i < kNrmTabN; i += blockDim.x) s_nt[i] = kNrmTab[i];
+  for (int i = threadIdx.x; i < D; i += blockDim.x) s_mu[(i & 3) * (D / 4) + (i >> 2)] = a.lik[i];
+  if (threadIdx.x == 0) {
+    s_mu[D] = a.lik[D];
+    s_mu[D + 1] = a.prior_kind == MCG_PRIOR_FLAT ? 0.0 : a.pri[2 * D];
+  }
   {
     // U fragments in lane order: frag (ib, kb), lane l -> U[16 ib + (l & 15)][4 kb + (l >> 4)],
     // zero below the diagonal (the oracle's chains start at j = i)
@@ -104,8 +118,9 @@ __global__ void __launch_bounds__(256, MCG_FC_MIN_WAVES) mh_fullcov_kernel(const
   const Rng rng{a.k0, a.k1};
   const uint32_t gid = a.chain_offset + (uint32_t)c;
   auto dim = [&](int kb) { return 4 * kb + q; };
+  double* const ypark = s_y + threadIdx.x;              // ypark[kb * kFcBlock]
 
-  double x[NL], y[NL];
+  double x[NL];
 #pragma unroll
   for (int kb = 0; kb < NL; ++kb) x[kb] = a.x[(int64_t)dim(kb) * N + c];
   double ll = a.ll[c], lp = a.lp[c];
@@ -113,7 +128,9 @@ __global__ void __launch_bounds__(256, MCG_FC_MIN_WAVES) mh_fullcov_kernel(const
 
   const bool accum = (a.flags & RUNF_ACCUMULATE) != 0;
   constexpr int P = 4, NH = 2;
-  double hcm[NH], hcs[NH];
+  __shared__ double s_hm[2 * NH * kFcBlock];             // harmonic-mean partials [2 NH][block]
+  auto hcm = [&](int l) -> double& { return s_hm[(2 * l) * kFcBlock + threadIdx.x]; };
+  auto hcs = [&](int l) -> double& { return s_hm[(2 * l + 1) * kFcBlock + threadIdx.x]; };
   double hm_pv = 0.0;
   bool hm_pok = false;
   double rmean[NL], rm2[NL];
@@ -125,33 +142,37 @@ __global__ void __launch_bounds__(256, MCG_FC_MIN_WAVES) mh_fullcov_kernel(const
     }
 #pragma unroll
     for (int l = 0; l < NH; ++l) {
-      hcm[l] = a.hm_m[(int64_t)(q + P * l) * N + c];
-      hcs[l] = a.hm_s[(int64_t)(q + P * l) * N + c];
+      hcm(l) = a.hm_m[(int64_t)(q + P * l) * N + c];
+      hcs(l) = a.hm_s[(int64_t)(q + P * l) * N + c];
     }
   }
   auto hm_flush = [&](int64_t R0) {
     const int li = (int)((R0 & 7) / P);
-    if (hm_pok) {
-#pragma unroll
-      for (int l = 0; l < NH; ++l)
-        if (l == li) hm_update(hcm[l], hcs[l], hm_pv);
-    }
+    if (hm_pok) hm_update(hcm(li), hcs(li), hm_pv);        // li: wave-uniform
     hm_pok = false;
   };
 
   int64_t next_rec = a.next_rec, r = a.next_r;
+  double inv_pf = 0.0;                                   // Welford weight, one record ahead
+  if (accum) inv_pf = a.inv_n[r - a.next_r0];
   auto record = [&](int64_t R) {
     const int64_t s = R - a.rec_base;
     if ((a.flags & RUNF_RECORD_X) && active) {
+      // opaque row pitch: left visible, the compiler hoists the 16 per-dim record addresses out
+      // of the step loop (32 registers, spilled) for this rarely taken path
+      int64_t n = N;
+      asm volatile("" : "+s"(n));
+      double* px = a.rec_x + (s * D + q) * n + c;
 #pragma unroll
-      for (int kb = 0; kb < NL; ++kb) a.rec_x[(s * D + dim(kb)) * N + c] = x[kb];
+      for (int kb = 0; kb < NL; ++kb) px[4 * kb * n] = x[kb];
     }
     if ((a.flags & RUNF_RECORD_LLP) && active && q == 0) {
       a.rec_ll[s * N + c] = ll;
       a.rec_lp[s * N + c] = lp;
     }
     if (accum) {
-      const double inv = a.inv_n[R - a.next_r0];
+      const double inv = inv_pf;
+      inv_pf = a.inv_n[R + 1 - a.next_r0];
 #pragma unroll
       for (int kb = 0; kb < NL; ++kb) {
         const double delta = x[kb] - rmean[kb];
@@ -179,14 +200,18 @@ __global__ void __launch_bounds__(256, MCG_FC_MIN_WAVES) mh_fullcov_kernel(const
     // model constants through global (not flat) pointers: a flat load counts against the LDS
     // counter too, so every wait for one would also drain the table gathers and U fragments
     typedef const __attribute__((address_space(1))) double gdouble;
-    gdouble* qlik = (gdouble*)a.lik;
     gdouble* qpri = (gdouble*)a.pri;
     gdouble* qprop = (gdouble*)a.prop;
-    asm volatile("" : "+s"(qlik), "+s"(qpri), "+s"(qprop));
-    // ---- proposal: y = x + s z (mcmc.ml:41); calls 4m + q, transposed to the lane's dims ----
+    asm volatile("" : "+s"(qpri), "+s"(qprop));
+    // ---- proposal y = x + s z (mcmc.ml:41) fused with e = U (y - mu) on the matrix cores ----
     bool ok = true;
+    dbl4 e[F::NIB];
+#pragma unroll
+    for (int ib = 0; ib < F::NIB; ++ib) e[ib] = dbl4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int m = 0; m < F::NM; ++m) {
+      // U fragments and mu are loop-invariant LDS reads: without a barrier the compiler hoists
+      // all of them out of the step loop into ~110 registers
       asm volatile("" ::: "memory");
       const u32x4 w = rng(gid, tlo, (uint32_t)(4 * m + q), TAG_MH, thi);
       double v[4];
@@ -204,36 +229,33 @@ __global__ void __launch_bounds__(256, MCG_FC_MIN_WAVES) mh_fullcov_kernel(const
         const int kb = 4 * m + k2;
         const int d = dim(kb);
         const double yv = fma(UNI ? a.uni_s : qprop[d], v[k2], x[kb]);
-        y[kb] = yv;
+        ypark[kb * kFcBlock] = yv;
         if constexpr (UNI == 2) ok = ok & (__builtin_fabs(yv) <= a.uni_hi);
         else ok = ok & (yv >= (UNI ? a.uni_lo : qpri[d])) & (yv <= (UNI ? a.uni_hi : qpri[D + d]));
+        const double rv = yv - s_mu[q * NL + kb];
+#pragma unroll
+        for (int ib = 0; ib < F::NIB; ++ib)
+          if (4 * ib <= kb)
+            e[ib] = __builtin_amdgcn_mfma_f64_16x16x4f64(s_u[F::frag(ib, kb) * 64 + lane], rv, e[ib], 0, 0, 0);
       }
     }
-    // ---- log-likelihood: e = U (y - mu) on the matrix cores, S = sum e_i^2 ----
-    double A0 = 0.0, A1 = 0.0;     // accumulators k = q (even ib) and k = q + 4 (odd ib)
+    // ---- log-likelihood: S = sum e_i^2 (accumulators k = q for even ib, k = q + 4 for odd ib) --
+    double A0 = 0.0, A1 = 0.0;
 #pragma unroll
-    for (int ib = 0; ib < F::NIB; ++ib) {
-      asm volatile("" ::: "memory");        // keep one row block's fragment reads in flight
-      dbl4 e = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int kb = 4 * ib; kb < F::NKB; ++kb) {
-        const double rv = y[kb] - qlik[dim(kb)];
-        e = __builtin_amdgcn_mfma_f64_16x16x4f64(s_u[F::frag(ib, kb) * 64 + lane], rv, e, 0, 0, 0);
-      }
+    for (int ib = 0; ib < F::NIB; ++ib)
 #pragma unroll
       for (int ri = 0; ri < 4; ++ri) {
-        if (ib & 1) A1 = fma(e[ri], e[ri], A1);
-        else A0 = fma(e[ri], e[ri], A0);
+        if (ib & 1) A1 = fma(e[ib][ri], e[ib][ri], A1);
+        else A0 = fma(e[ib][ri], e[ib][ri], A0);
       }
-    }
     const double b = A0 + A1;
     const double cs = b + __shfl_xor(b, 32, 64);
     const double S = cs + __shfl_xor(cs, 16, 64);
-    const double lly = qlik[D] - 0.5 * S;
+    const double lly = s_mu[D] - 0.5 * S;
     int inb = ok ? 1 : 0;
     inb &= __shfl_xor(inb, 32, 64);
     inb &= __shfl_xor(inb, 16, 64);
-    const double lpy = a.prior_kind == MCG_PRIOR_FLAT ? 0.0 : (inb ? qpri[2 * D] : -__builtin_inf());
+    const double lpy = a.prior_kind == MCG_PRIOR_FLAT ? 0.0 : (inb ? s_mu[D + 1] : -__builtin_inf());
     // ---- Hastings ratio and accept test (mcmc.ml:42-56); staggered accept uniforms ----
     const double ratio = (lly + lpy) - (ll + lp);
     const int qq = (int)(t & (P - 1));
@@ -244,9 +266,12 @@ __global__ void __launch_bounds__(256, MCG_FC_MIN_WAVES) mh_fullcov_kernel(const
     }
     const double lu = __shfl(lu_own, (lane & 15) | (qq << 4), 64);
     const bool acc = lu < ratio;
-    if (acc) {
 #pragma unroll
-      for (int kb = 0; kb < NL; ++kb) x[kb] = y[kb];
+    for (int kb = 0; kb < NL; ++kb) {
+      const double yv = ypark[kb * kFcBlock];
+      x[kb] = acc ? yv : x[kb];
+    }
+    if (acc) {
       ll = lly;
       lp = lpy;
       ++na;
@@ -267,8 +292,13 @@ __global__ void __launch_bounds__(256, MCG_FC_MIN_WAVES) mh_fullcov_kernel(const
   }
 
   if (!active) return;
+  // opaque row pitch: the prologue's per-dim addresses would otherwise be kept live through the
+  // step loop for these stores (two registers per address, spilled)
+  int64_t n = N;
+  asm volatile("" : "+s"(n));
+  const int64_t o = (int64_t)q * n + c;
 #pragma unroll
-  for (int kb = 0; kb < NL; ++kb) a.x[(int64_t)dim(kb) * N + c] = x[kb];
+  for (int kb = 0; kb < NL; ++kb) a.x[o + 4 * kb * n] = x[kb];
   if (q == 0) {
     a.ll[c] = ll;
     a.lp[c] = lp;
@@ -277,24 +307,25 @@ __global__ void __launch_bounds__(256, MCG_FC_MIN_WAVES) mh_fullcov_kernel(const
   if (accum) {
 #pragma unroll
     for (int kb = 0; kb < NL; ++kb) {
-      a.mean[(int64_t)dim(kb) * N + c] = rmean[kb];
-      a.m2[(int64_t)dim(kb) * N + c] = rm2[kb];
+      a.mean[o + 4 * kb * n] = rmean[kb];
+      a.m2[o + 4 * kb * n] = rm2[kb];
     }
     hm_flush((r - 1) & ~(int64_t)(P - 1));
 #pragma unroll
     for (int l = 0; l < NH; ++l) {
-      a.hm_m[(int64_t)(q + P * l) * N + c] = hcm[l];
-      a.hm_s[(int64_t)(q + P * l) * N + c] = hcs[l];
+      a.hm_m[o + P * l * n] = hcm(l);
+      a.hm_s[o + P * l * n] = hcs(l);
     }
   }
 }
 
 template <int D>
 hipError_t launch_mh_fullcov(const MhArgs& a, int64_t nthreads, hipStream_t s) {
-  const int64_t grid = (nthreads + 255) / 256;          // nthreads = 4 N: 64 chains per block
-  if (a.uni && a.uni_lo == -a.uni_hi) hipLaunchKernelGGL((mh_fullcov_kernel<D, 2>), dim3((unsigned)grid), dim3(256), 0, s, a);
-  else if (a.uni) hipLaunchKernelGGL((mh_fullcov_kernel<D, 1>), dim3((unsigned)grid), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((mh_fullcov_kernel<D, 0>), dim3((unsigned)grid), dim3(256), 0, s, a);
+  const int64_t grid = (nthreads + kFcBlock - 1) / kFcBlock;   // nthreads = 4 N: 128 chains per block
+  const dim3 g((unsigned)grid), b(kFcBlock);
+  if (a.uni && a.uni_lo == -a.uni_hi) hipLaunchKernelGGL((mh_fullcov_kernel<D, 2>), g, b, 0, s, a);
+  else if (a.uni) hipLaunchKernelGGL((mh_fullcov_kernel<D, 1>), g, b, 0, s, a);
+  else hipLaunchKernelGGL((mh_fullcov_kernel<D, 0>), g, b, 0, s, a);
   return hipGetLastError();
 }
 

@@ -295,18 +295,35 @@ struct AccumCfg {
 #endif
 
 #ifndef MCG_NRM_BATCH
-#define MCG_NRM_BATCH 1    // 1: the four normals of a Philox call gather together (one LDS wait)
+#define MCG_NRM_BATCH 1    // 1: the four normals of a Philox call gather together (one LDS wait);
+                           // 2: two calls' gathers in flight together (the second hides behind the first)
+#endif
+
+#ifndef MCG_HM_LDS
+#define MCG_HM_LDS 1       // harmonic-mean partials of the record classes in LDS (not VGPRs)
 #endif
 
 #ifndef MCG_MH_MIN_WAVES
 #define MCG_MH_MIN_WAVES 1
 #endif
 
+// Waves per SIMD the kernel is built for.  The fused Gaussian step with at most 8 dims per lane
+// (C2: D 32 on 4 lanes) fits 168 registers -- three waves per SIMD -- when its normals are
+// evaluated one at a time (no batched gathers: their 32 in-flight registers would spill);
+// C2 1.87e10 -> 1.96e10 MH steps/s against two waves with batched gathers (A/B on one box).
+// Everything else is left to the compiler's register budget (two waves where it fits).
+template <int D, int P, int LIK, int PROP>
+struct MhShape {
+  static constexpr bool kThree = separable<LIK, PROP>() && Layout<D, P>::NL <= 8 && MCG_MH_MIN_WAVES <= 3;
+  static constexpr int kWaves = kThree ? 3 : MCG_MH_MIN_WAVES;
+  static constexpr bool kBatchNormals = MCG_NRM_BATCH != 0 && !kThree;
+};
+
 // UNI: 0 = constants through pointers; 1 = isotropic proposal scale and one box [lo, hi] for
 // every dim as kernel arguments; 2 = the same with a symmetric box [-h, h], tested as |y| <= h
 // (one compare per dim; the same predicate as lo <= y <= hi for every double, NaN included)
 template <int D, int P, int LIK, int PROP, int UNI>
-__global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs a) {
+__global__ void __launch_bounds__(256, (MhShape<D, P, LIK, PROP>::kWaves)) mh_kernel(const MhArgs a) {
   using L = Layout<D, P>;
   constexpr bool kSeparable = separable<LIK, PROP>();
   static_assert(kSeparable || !UNI, "UNI applies to the fused separable step");
@@ -359,7 +376,18 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
   // classes c = sub + P l.  The -ll of record R is parked in lane R mod P and folded when the
   // group of P records is complete, so each lane evaluates one exp per P records.
   constexpr int NH = P >= 8 ? 1 : 8 / P;
-  double hcm[NH], hcs[NH];
+  // the partials live in LDS ([2 NH][256], conflict-free): touched once per P records, they
+  // would otherwise hold 4 NH VGPRs through the whole step
+  __shared__ double s_hm[MCG_HM_LDS ? 2 * NH * 256 : 1];
+  double hcm_r[MCG_HM_LDS ? 1 : NH], hcs_r[MCG_HM_LDS ? 1 : NH];
+  auto hcm = [&](int l) -> double& {
+    if constexpr (MCG_HM_LDS) return s_hm[(2 * l) * 256 + threadIdx.x];
+    else return hcm_r[l];
+  };
+  auto hcs = [&](int l) -> double& {
+    if constexpr (MCG_HM_LDS) return s_hm[(2 * l + 1) * 256 + threadIdx.x];
+    else return hcs_r[l];
+  };
   double hm_pv = 0.0;
   bool hm_pok = false;
   // accumulator slot j of this lane: VGPR, LDS [j][threadIdx] or HBM [dim][chain]
@@ -388,37 +416,51 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
     }
 #pragma unroll
     for (int l = 0; l < NH; ++l) {
-      hcm[l] = a.hm_m[(int64_t)(sub + P * l) * N + c];
-      hcs[l] = a.hm_s[(int64_t)(sub + P * l) * N + c];
+      hcm(l) = a.hm_m[(int64_t)(sub + P * l) * N + c];
+      hcs(l) = a.hm_s[(int64_t)(sub + P * l) * N + c];
     }
   }
   // fold the parked record of the group starting at record R0 (R0 % P == 0)
   auto hm_flush = [&](int64_t R0) {
     const int li = (int)((R0 & 7) / P);
     if (hm_pok) {
+      if constexpr (MCG_HM_LDS) {
+        hm_update(hcm(li), hcs(li), hm_pv);             // li is wave-uniform (record index)
+      } else {
 #pragma unroll
-      for (int l = 0; l < NH; ++l)
-        if (l == li) hm_update(hcm[l], hcs[l], hm_pv);
+        for (int l = 0; l < NH; ++l)
+          if (l == li) hm_update(hcm(l), hcs(l), hm_pv);
+      }
     }
     hm_pok = false;
   };
 
   int64_t next_rec = a.next_rec, r = a.next_r;
+  // the Welford weight of the next record is loaded one record ahead: loaded where it is used,
+  // its L2 latency sat exposed in every step (the table holds one entry past rec_end)
+  double inv_pf = 0.0;
+  if (accum) inv_pf = a.inv_n[r - a.next_r0];
   auto record = [&](int64_t R) {
     int64_t s = R - a.rec_base;
     if ((a.flags & RUNF_RECORD_X) && active) {
+      // opaque row pitch: left visible, the compiler hoists the per-dim record addresses out of
+      // the step loop (two registers per dim) for this rarely taken path
+      int64_t n = N;
+      asm volatile("" : "+s"(n));
+      double* px = a.rec_x + s * D * n + c;
 #pragma unroll
       for (int i = 0; i < L::NCL; ++i)
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-          if (L::valid(sub, i, k)) a.rec_x[(s * D + L::dim(sub, i, k)) * N + c] = x[4 * i + k];
+          if (L::valid(sub, i, k)) px[L::dim(sub, i, k) * n] = x[4 * i + k];
     }
     if ((a.flags & RUNF_RECORD_LLP) && active && sub == 0) {
       a.rec_ll[s * N + c] = ll;
       a.rec_lp[s * N + c] = lp;
     }
     if (accum) {
-      const double inv = a.inv_n[R - a.next_r0];      // 1/(R+1), host IEEE division
+      const double inv = inv_pf;                      // 1/(R+1), host IEEE division
+      inv_pf = a.inv_n[R + 1 - a.next_r0];
 #pragma unroll
       for (int i = 0; i < L::NCL; ++i)
 #pragma unroll
@@ -512,19 +554,9 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
         for (int i = 0; i < L::NCL; ++i) cidx[i] = (uint32_t)(sub + P * i);
         philox_multi<L::NCL>(wl, gid, tlo, cidx, (TAG_MH << 16) | (thi & 0xFFFFu), rng.k0, rng.k1);
       }
-#pragma unroll
-      for (int i = 0; i < L::NCL; ++i) {
+      // the coordinates and terms of call i from its four normals
+      auto dims = [&](const int i, const double* z) {
         const int cc = sub + P * i;
-        const u32x4 w = wl[i];
-        double z[4];
-#if MCG_NRM_BATCH
-        pnormal4_lds(w, s_nt, z);
-#else
-        z[0] = pnormal(w.x, s_nt);
-        z[1] = pnormal(w.y, s_nt);
-        z[2] = pnormal(w.z, s_nt);
-        z[3] = pnormal(w.w, s_nt);
-#endif
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           if (!L::valid(sub, i, k)) continue;
@@ -549,6 +581,34 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
             ok = ok & (yv >= lo) & (yv <= hi);
           }
         }
+      };
+      constexpr int kStride = MCG_NRM_BATCH == 2 ? 2 : 1;
+#pragma unroll
+      for (int i = 0; i < L::NCL; i += kStride) {
+        double z[4];
+        if constexpr (kStride == 2) {
+          if (i + 1 < L::NCL) {
+            // calls i and i + 1: sixteen gathers in flight, call i's arithmetic hides call i+1's
+            Nrm4Rows r0, r1;
+            nrm8_issue(wl[i], wl[i + 1], s_nt, r0, r1);
+            nrm4_finish<true>(r0, z);
+            dims(i, z);
+            nrm8_wait(r1);
+            nrm4_finish<MCG_NRM_XP1>(r1, z);
+            dims(i + 1, z);
+            continue;
+          }
+        }
+        if constexpr (MhShape<D, P, LIK, PROP>::kBatchNormals) {
+          pnormal4_lds(wl[i], s_nt, z);
+        } else {
+          const u32x4 w = wl[i];
+          z[0] = pnormal(w.x, s_nt);
+          z[1] = pnormal(w.y, s_nt);
+          z[2] = pnormal(w.z, s_nt);
+          z[3] = pnormal(w.w, s_nt);
+        }
+        dims(i, z);
       }
       if constexpr (LIK == MCG_LIK_FLAT) {
         lly = 0.0;
@@ -740,11 +800,15 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
   }
 
   if (!active) return;
+  // opaque row pitch: the prologue's per-dim addresses would otherwise be kept live through the
+  // step loop for these stores (two registers per address)
+  int64_t n = N;
+  asm volatile("" : "+s"(n));
 #pragma unroll
   for (int i = 0; i < L::NCL; ++i)
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      if (L::valid(sub, i, k)) a.x[(int64_t)L::dim(sub, i, k) * N + c] = x[4 * i + k];
+      if (L::valid(sub, i, k)) a.x[(int64_t)L::dim(sub, i, k) * n + c] = x[4 * i + k];
   if (sub == 0) {
     a.ll[c] = ll;
     a.lp[c] = lp;
@@ -757,7 +821,7 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
 #pragma unroll
         for (int k = 0; k < 4; ++k)
           if (L::valid(sub, i, k)) {
-            int64_t o = (int64_t)L::dim(sub, i, k) * N + c;
+            int64_t o = (int64_t)L::dim(sub, i, k) * n + c;
             a.mean[o] = acc_mean(i, k);
             a.m2[o] = acc_m2(i, k);
           }
@@ -766,8 +830,8 @@ __global__ void __launch_bounds__(256, MCG_MH_MIN_WAVES) mh_kernel(const MhArgs 
     hm_flush((r - 1) & ~(int64_t)(P - 1));
 #pragma unroll
     for (int l = 0; l < NH; ++l) {
-      a.hm_m[(int64_t)(sub + P * l) * N + c] = hcm[l];
-      a.hm_s[(int64_t)(sub + P * l) * N + c] = hcs[l];
+      a.hm_m[(int64_t)(sub + P * l) * n + c] = hcm(l);
+      a.hm_s[(int64_t)(sub + P * l) * n + c] = hcs(l);
     }
   }
 }

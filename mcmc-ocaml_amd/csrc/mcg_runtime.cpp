@@ -654,7 +654,7 @@ int mcg_run(mcg_ctx* ctx, const mcg_run_opts* o) {
   // per-step division): one device table inv[R] for every absolute record index R, grown rarely.
   // (A per-run upload put a copy between consecutive MH kernels: two engine hand-offs per run.)
   {
-    const int64_t need = rec_base + std::max<int64_t>(n_rec, 1);
+    const int64_t need = rec_base + std::max<int64_t>(n_rec, 1) + 1;   // + the prefetch of record rec_end
     if (need > ctx->inv_cap) {
       const int64_t cap = std::max<int64_t>(need, std::max<int64_t>(2 * ctx->inv_cap, (int64_t)1 << 20));
       std::vector<double> ih((size_t)cap);
