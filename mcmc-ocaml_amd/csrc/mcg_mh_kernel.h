@@ -312,10 +312,16 @@ struct AccumCfg {
 // evaluated one at a time (no batched gathers: their 32 in-flight registers would spill);
 // C2 1.87e10 -> 1.96e10 MH steps/s against two waves with batched gathers (A/B on one box).
 // Everything else is left to the compiler's register budget (two waves where it fits).
+#ifndef MCG_MH_FOUR
+#define MCG_MH_FOUR 0      // experiment: four waves per SIMD, UNI likelihood constants read from LDS
+#endif
 template <int D, int P, int LIK, int PROP>
 struct MhShape {
   static constexpr bool kThree = separable<LIK, PROP>() && Layout<D, P>::NL <= 8 && MCG_MH_MIN_WAVES <= 3;
-  static constexpr int kWaves = kThree ? 3 : MCG_MH_MIN_WAVES;
+  static constexpr bool kFour = kThree && MCG_MH_FOUR;
+  static constexpr int kWaves = kFour ? 4 : kThree ? 3 : MCG_MH_MIN_WAVES;
+  // four waves per SIMD need two workgroups per CU within the LDS: 512 threads share the tables
+  static constexpr int kBlock = kFour ? 512 : 256;
   static constexpr bool kBatchNormals = MCG_NRM_BATCH != 0 && !kThree;
 };
 
@@ -323,7 +329,8 @@ struct MhShape {
 // every dim as kernel arguments; 2 = the same with a symmetric box [-h, h], tested as |y| <= h
 // (one compare per dim; the same predicate as lo <= y <= hi for every double, NaN included)
 template <int D, int P, int LIK, int PROP, int UNI>
-__global__ void __launch_bounds__(256, (MhShape<D, P, LIK, PROP>::kWaves)) mh_kernel(const MhArgs a) {
+__global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D, P, LIK, PROP>::kWaves)) mh_kernel(const MhArgs a) {
+  constexpr int kBlk = MhShape<D, P, LIK, PROP>::kBlock;
   using L = Layout<D, P>;
   constexpr bool kSeparable = separable<LIK, PROP>();
   static_assert(kSeparable || !UNI, "UNI applies to the fused separable step");
@@ -378,14 +385,14 @@ __global__ void __launch_bounds__(256, (MhShape<D, P, LIK, PROP>::kWaves)) mh_ke
   constexpr int NH = P >= 8 ? 1 : 8 / P;
   // the partials live in LDS ([2 NH][256], conflict-free): touched once per P records, they
   // would otherwise hold 4 NH VGPRs through the whole step
-  __shared__ double s_hm[MCG_HM_LDS ? 2 * NH * 256 : 1];
+  __shared__ double s_hm[MCG_HM_LDS ? 2 * NH * kBlk : 1];
   double hcm_r[MCG_HM_LDS ? 1 : NH], hcs_r[MCG_HM_LDS ? 1 : NH];
   auto hcm = [&](int l) -> double& {
-    if constexpr (MCG_HM_LDS) return s_hm[(2 * l) * 256 + threadIdx.x];
+    if constexpr (MCG_HM_LDS) return s_hm[(2 * l) * kBlk + threadIdx.x];
     else return hcm_r[l];
   };
   auto hcs = [&](int l) -> double& {
-    if constexpr (MCG_HM_LDS) return s_hm[(2 * l + 1) * 256 + threadIdx.x];
+    if constexpr (MCG_HM_LDS) return s_hm[(2 * l + 1) * kBlk + threadIdx.x];
     else return hcs_r[l];
   };
   double hm_pv = 0.0;
@@ -492,7 +499,17 @@ __global__ void __launch_bounds__(256, (MhShape<D, P, LIK, PROP>::kWaves)) mh_ke
   double lu_own = 0.0;
   // UNI (isotropic proposal scale, one box for every dim): the scale and the box are kernel
   // arguments (SGPRs), so the lane's likelihood constants fit in registers for the whole launch
-  double rc_m[UNI ? L::NL : 1], rc_i[UNI ? L::NL : 1];
+  constexpr bool kRcLds = MhShape<D, P, LIK, PROP>::kFour && UNI;
+  double rc_m[UNI && !kRcLds ? L::NL : 1], rc_i[UNI && !kRcLds ? L::NL : 1];
+  // kRcLds: (1/sigma, mu/sigma) of every dim staged in LDS, read per step (lanes of one `sub`
+  // read one address: a broadcast, conflict-free)
+  __shared__ double2 s_rc[kRcLds ? D : 1];
+  if constexpr (kRcLds) {
+    __syncthreads();
+    for (int d = threadIdx.x; d < D; d += blockDim.x)
+      s_rc[d] = double2(LIK == MCG_LIK_DIAG_GAUSS ? a.lik[D + d] : 0.0, LIK == MCG_LIK_FLAT ? 0.0 : a.lik[d]);
+    __syncthreads();
+  }
   // UNI: the likelihood normaliser and the box's log density in VGPRs too (a per-step cached
   // load of each put a vector-memory wait on every step's critical path)
   double rc_c = 0.0, rc_lp = 0.0;
@@ -501,7 +518,7 @@ __global__ void __launch_bounds__(256, (MhShape<D, P, LIK, PROP>::kWaves)) mh_ke
     rc_lp = a.prior_kind != MCG_PRIOR_FLAT ? a.pri[2 * D] : 0.0;
     asm volatile("" : "+v"(rc_c), "+v"(rc_lp));
 #pragma unroll
-    for (int i = 0; i < L::NCL; ++i)
+    for (int i = 0; i < (kRcLds ? 0 : L::NCL); ++i)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int d = L::valid(sub, i, k) ? L::dim(sub, i, k) : 0;
@@ -563,7 +580,15 @@ __global__ void __launch_bounds__(256, (MhShape<D, P, LIK, PROP>::kWaves)) mh_ke
           const int d = 4 * cc + k;
           const double yv = fma(UNI ? a.uni_s : qprop[d], z[k], x[4 * i + k]);
           y[4 * i + k] = yv;
-          const double rcm = UNI ? rc_m[4 * i + k] : 0.0, rci = UNI ? rc_i[4 * i + k] : 0.0;
+          double rcm = 0.0, rci = 0.0;
+          if constexpr (kRcLds) {
+            const double2 rc = s_rc[d];
+            rci = rc.x;
+            rcm = rc.y;
+          } else if constexpr (UNI) {
+            rcm = rc_m[4 * i + k];
+            rci = rc_i[4 * i + k];
+          }
           if constexpr (LIK == MCG_LIK_DIAG_GAUSS) {
             const double e = UNI ? fma(yv, rci, -rcm)
                                  : fma(yv, qlik[D + d], -qlik[d]);   // (y - mu)/sigma
@@ -857,7 +882,7 @@ hipError_t launch_eval(const MhArgs& a, hipStream_t s) {
 
 template <int D, int P, int LIK, int PROP>
 hipError_t launch_mh(const MhArgs& a, int64_t nthreads, hipStream_t s) {
-  const int block = 256;
+  const int block = MhShape<D, P, LIK, PROP>::kBlock;
   const int64_t grid = (nthreads + block - 1) / block;
   constexpr int lds = AccumCfg<D, P>::kLdsBytes;
   if constexpr (separable<LIK, PROP>()) {

@@ -288,6 +288,17 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
 
   NestArgs a{};
   a.m = base_args(ctx);
+  {
+    // a box prior symmetric in every dim (closed form lo[d] == -hi[d], bitwise): the walkers
+    // test it as |y| <= hi, one compare per dim
+    const auto& bx = ctx->pri_host;
+    bool sym = ctx->prior_kind != MCG_PRIOR_FLAT && (int64_t)bx.size() >= 2 * D;
+    for (int64_t d = 0; d < D && sym; ++d) {
+      const double nhi = -bx[(size_t)(D + d)];
+      sym = !std::memcmp(&bx[(size_t)d], &nhi, 8);
+    }
+    a.sym_box = sym ? 1 : 0;
+  }
   a.x = (double*)B.x.p;
   a.ll = (double*)B.ll.p;
   a.lp = (double*)B.lp.p;
@@ -302,7 +313,11 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   // the walkers' draws of a generation in a table the previous merge fills (when it fits)
   a.rt_ix = nullptr;
   a.rt_sc = nullptr;
-  if (2 * k * nmcmc * 24 <= ((int64_t)512 << 20) && std::getenv("MCG_NESTED_NO_TABLE") == nullptr) {
+  // (its DE pairs are stored as row byte offsets i D 8 | j D 8 << 32, so the live set must span
+  // less than 4 GiB)
+  a.row_bytes = (uint32_t)(D * 8);
+  if (2 * k * nmcmc * 24 <= ((int64_t)512 << 20) && (uint64_t)n * (uint64_t)D * 8u < ((uint64_t)1 << 32) &&
+      std::getenv("MCG_NESTED_NO_TABLE") == nullptr) {
     HC(B.rt_ix.ensure(2 * k * nmcmc * 8), "alloc draw table");
     HC(B.rt_sc.ensure(2 * k * nmcmc * 16), "alloc draw table");
     a.rt_ix = (unsigned long long*)B.rt_ix.p;

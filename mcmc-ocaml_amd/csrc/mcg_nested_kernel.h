@@ -67,11 +67,13 @@ struct NestArgs {
   uint32_t* sync;           // [2][kSyncUse] hand-off counters: retire -> estimate, rank count -> scatter
   unsigned long long* trace;  // MCG_NEST_TRACE builds: per-workgroup phase stamps of one generation
   // the walkers' draws of a generation, [2][nmcmc][k] (null: the walk draws them itself): DE
-  // indices i | j << 32 and (DE scale, log accept uniform).  The walk of generation g reads half
+  // pair as row byte offsets (i | j << 32) * row_bytes and (DE scale, log accept uniform).  The walk of generation g reads half
   // g & 1 while its spare waves fill the other half for generation g + 1.
   unsigned long long* rt_ix;
   double2* rt_sc;
   int32_t est_in_rank;      // the estimate is folded by an extra rank_count workgroup (k <= 4096)
+  int32_t sym_box;          // box prior with lo[d] == -hi[d] for every d: tested as |y| <= hi
+  uint32_t row_bytes;       // D * 8: the draw table holds DE pairs as row byte offsets
   double* tv;               // ll + log dv of this generation's dead points (padded pow2)
   const double* prefix;     // [k+1] sum_{j'<j} log1p(-1/(n-j'))
   const double* qadd;       // [k] 1/(n-j) (nested.ml:140 quirk) or log(1/(n-j))
@@ -136,6 +138,9 @@ __device__ __forceinline__ void walk_draws_fill(const NestArgs& a, int64_t mrep,
     unsigned long long ix;
     double2 sc;
     walk_draw(a, (uint32_t)(mrep + w), (uint32_t)s, kNrmTab, lt, ix, sc);
+    // byte offsets of the two rows: the walker adds them to the live set's base with no 64-bit
+    // address arithmetic
+    ix = (unsigned long long)((uint32_t)ix * a.row_bytes) | ((unsigned long long)((uint32_t)(ix >> 32) * a.row_bytes) << 32);
     a.rt_ix[base + e] = ix;
     a.rt_sc[base + e] = sc;
   }
@@ -145,7 +150,7 @@ __device__ __forceinline__ void walk_draws_fill(const NestArgs& a, int64_t mrep,
 // bounds), loaded into registers once per launch.  Loaded per step through the parameter
 // pointers they would queue behind the prefetched DE rows in the in-order vector-memory counter
 // and expose the full load latency every step.  Same operations as eval_lik / eval_prior.
-template <int D, int P, int LIK>
+template <int D, int P, int LIK, bool SYM = false>
 struct WalkTarget {
   using Lay = Layout<D, P>;
   static constexpr int NL = Lay::NL;
@@ -272,10 +277,14 @@ struct WalkTarget {
     if constexpr (!kReg) {
       return eval_prior<D, P>(y, sub, a, a.pri);
     } else {
-      if (!box) return 0.0;
+      if (!SYM && !box) return 0.0;                   // SYM implies a box prior
       int inb = 1;
 #pragma unroll
-      for (int j = 0; j < NL; ++j) inb &= (int)(y[j] >= lo[j]) & (int)(y[j] <= hi[j]);
+      for (int j = 0; j < NL; ++j) {
+        // SYM: |y| <= h is the same predicate as -h <= y <= h for every double, NaN included
+        if constexpr (SYM) inb &= (int)(__builtin_fabs(y[j]) <= hi[j]);
+        else inb &= (int)(y[j] >= lo[j]) & (int)(y[j] <= hi[j]);
+      }
       inb = and_lanes<P>(inb);
       return inb ? lp_in : -__builtin_inf();
     }
@@ -288,7 +297,7 @@ struct WalkTarget {
 // scale, accept decision and start point agree without communication; the log-target is the
 // canonical sum reduced across the P lanes (reduce_canon).  The DE partner rows of step s + 1
 // depend only on the RNG, so they are loaded while step s computes (one step of prefetch).
-template <int D, int LIK, int P, bool TAB>
+template <int D, int LIK, int P, bool TAB, bool SYM>
 __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   using Lay = Layout<D, P>;
   constexpr int NL = Lay::NL;
@@ -342,6 +351,18 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   }
   if (start < 0) start = a.key_slot[a.k - 1];
   double cur[NL], y[NL];
+  auto load_row_at = [&](double* dst, const double* __restrict__ src) {
+#pragma unroll
+    for (int i = 0; i < Lay::NCL; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        dst[4 * i + q] = Lay::valid(sub, i, q) ? src[Lay::dim(sub, i, q)] : 0.0;
+  };
+  // TAB: the table holds row byte offsets (32-bit: the live set is below 4 GiB)
+  auto row_ptr = [&](uint32_t v) -> const double* {
+    if constexpr (TAB) return (const double*)((const char*)a.x + v);
+    else return a.x + (int64_t)v * D;
+  };
   auto load_row = [&](double* dst, int64_t row) {
     const double* __restrict__ src = a.x + row * D;
 #pragma unroll
@@ -357,7 +378,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
     const uint32_t jj = randint(ri.z, ri.w, n - 1);
     j = jj + (jj >= i ? 1u : 0u);
   };
-  WalkTarget<D, P, LIK> tgt;
+  WalkTarget<D, P, LIK, SYM> tgt;
   tgt.load(a.m, sub);
   tgt.setup_constraint(thr);
   load_row(cur, start);
@@ -396,14 +417,24 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   // loaded one group ahead like the rows: (scale, log u) of steps s0 + u and the refill indices
   // of steps s0 + PD + u
   const int64_t tbase = TAB ? walk_tab_base(a, a.mrep) : 0;
-  auto tab_at = [&](int64_t st) { return tbase + (st < a.nmcmc ? st : a.nmcmc - 1) * a.k + wc; };
+  // per-lane entry pointers; step st (clamped to the last step) is at [st * k].  32-bit offsets
+  // (the table is skipped beyond 512 MB, so k nmcmc < 2^25): as 64-bit products with the clamp
+  // compare in VALU the eight entry addresses of a group cost ~80 SALU/VALU per group, issued by
+  // the walker's single wave on its SIMD
+  const double2* const tsc_lane = a.rt_sc + tbase + wc;
+  const unsigned long long* const tix_lane = a.rt_ix + tbase + wc;
+  const uint32_t tk = (uint32_t)a.k, tlast = (uint32_t)(a.nmcmc - 1);
+  auto tab_off = [&](int64_t st) -> uint32_t {
+    const uint32_t s32 = (uint32_t)st;
+    return (s32 < tlast ? s32 : tlast) * tk;
+  };
   unsigned long long tix_cur[PD], tix_next[PD];
   double2 tsc_cur[PD], tsc_next[PD];
   if constexpr (TAB) {
 #pragma unroll
     for (int u = 0; u < PD; ++u) {
-      tsc_cur[u] = a.rt_sc[tab_at(u)];
-      tix_cur[u] = a.rt_ix[tab_at(PD + u)];
+      tsc_cur[u] = tsc_lane[tab_off(u)];
+      tix_cur[u] = tix_lane[tab_off(PD + u)];
     }
   }
   // partner rows of steps s .. s + PD - 1 in flight: ring slot u holds step s0 + u
@@ -412,14 +443,14 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   for (int u = 0; u < PD; ++u) {
     uint32_t i0, j0;
     if constexpr (TAB) {
-      const unsigned long long ix = a.rt_ix[tab_at(u)];
+      const unsigned long long ix = tix_lane[tab_off(u)];
       i0 = (uint32_t)ix;
       j0 = (uint32_t)(ix >> 32);
     } else {
       pick(u, i0, j0);
     }
-    load_row(bi[u], i0);
-    load_row(bj[u], j0);
+    load_row_at(bi[u], row_ptr(i0));
+    load_row_at(bj[u], row_ptr(j0));
   }
   // whole groups of PD steps with no data-dependent branches around the loads, so the compiler
   // can count the in-flight loads (vmcnt) across iterations; steps past nmcmc only compute
@@ -436,8 +467,8 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
       }
 #pragma unroll
       for (int u = 0; u < PD; ++u) {                  // the next group's draws go out first
-        tsc_next[u] = a.rt_sc[tab_at(s0 + PD + u)];
-        tix_next[u] = a.rt_ix[tab_at(s0 + 2 * PD + u)];
+        tsc_next[u] = tsc_lane[tab_off(s0 + PD + u)];
+        tix_next[u] = tix_lane[tab_off(s0 + 2 * PD + u)];
       }
     } else if constexpr (P == 4 && PD % 4 == 0) {
       // finish this group's draws and hand step u's values from lane u % 4 to the quad (DPP)
@@ -498,8 +529,8 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
       const bool live = s0 + u < a.nmcmc;
 #pragma unroll
       for (int d = 0; d < NL; ++d) y[d] = cur[d] + dsc_g[u] * (bj[u][d] - bi[u][d]);
-      load_row(bi[u], ip_g[u]);                        // refill slot u with step s + PD's rows
-      load_row(bj[u], jp_g[u]);
+      load_row_at(bi[u], row_ptr(ip_g[u]));            // refill slot u with step s + PD's rows
+      load_row_at(bj[u], row_ptr(jp_g[u]));
       const bool ok = tgt.constraint(y, sub, a.m, thr);
       const double lpy = tgt.prior(y, sub, a.m);
       const double ml = ok ? lpy : -__builtin_inf();
@@ -574,8 +605,11 @@ hipError_t launch_nest_walk(const NestArgs& a, hipStream_t st) {
   const int block = kNestWalkBlock;
   const int64_t grid = (a.k * P + block - 1) / block;
   // with the draw table: the same walker waves, each with three table-filling waves beside it
-  if (a.rt_ix) hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true>), dim3((unsigned)((a.k * P + 63) / 64)), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, false>), dim3((unsigned)grid), dim3(block), 0, st, a);
+  const dim3 gt((unsigned)((a.k * P + 63) / 64)), bt(256);
+  constexpr bool kSym = WalkTarget<D, P, LIK>::kReg;   // the |y| <= h form needs the register target
+  if (a.rt_ix && kSym && a.sym_box) hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, kSym>), gt, bt, 0, st, a);
+  else if (a.rt_ix) hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, false>), gt, bt, 0, st, a);
+  else hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, false, false>), dim3((unsigned)grid), dim3(block), 0, st, a);
   return hipGetLastError();
 }
 

@@ -198,6 +198,22 @@ def test_nested_multilane_walkers_bit_exact(oracle, T, D, k):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("D,sym,diag", [(16, False, False), (16, False, True), (16, True, True)])
+def test_nested_walker_box_forms_bit_exact(oracle, T, D, sym, diag):
+    """The walker's two box tests: a box symmetric in every dim is tested as |y| <= h (one
+    compare per dim), any other as lo <= y <= hi; both give the oracle's dead points bit for
+    bit (4-lane walkers, draw table with row byte offsets)."""
+    lo = -2.0 * np.ones(D) if sym else np.linspace(-2.5, -1.5, D)
+    hi = 2.0 * np.ones(D) if sym else np.linspace(1.75, 2.25, D)
+    lik = (T.diag_gauss(np.linspace(-0.3, 0.3, D), np.linspace(0.4, 0.8, D)) if diag
+           else T.gauss_shell(np.zeros(D), 1.0, 0.2))
+    pri = T.box(lo, hi)
+    g = gpu_nested(lik, pri, 12, nlive=400, nmcmc=15, mode_hopping_frac=0.1, k=40, max_dead=40 * 30)
+    o = oracle_nested(oracle, lik, pri, 12, nlive=400, nmcmc=15, mode_hop=0.1, k=40, max_iter=40 * 30)
+    assert_nested_same(g, o)
+
+
+@pytest.mark.gpu
 def test_nested_rank_count_sort_ties_and_partial_runs(oracle, T):
     """k = 1000 new keys per generation: three full 256-key runs and a partial one in the
     counted-rank sort, and walks of 2 steps on a thin shell, so many walkers reject every step and
