@@ -316,10 +316,14 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   // (its DE pairs are stored as row byte offsets i D 8 | j D 8 << 32, so the live set must span
   // less than 4 GiB)
   a.row_bytes = (uint32_t)(D * 8);
-  if (2 * k * nmcmc * 24 <= ((int64_t)512 << 20) && (uint64_t)n * (uint64_t)D * 8u < ((uint64_t)1 << 32) &&
+  if (2 * k * (nmcmc + kWalkTabPad) * 24 <= ((int64_t)512 << 20) && (uint64_t)n * (uint64_t)D * 8u < ((uint64_t)1 << 32) &&
       std::getenv("MCG_NESTED_NO_TABLE") == nullptr) {
-    HC(B.rt_ix.ensure(2 * k * nmcmc * 8), "alloc draw table");
-    HC(B.rt_sc.ensure(2 * k * nmcmc * 16), "alloc draw table");
+    // two halves of nmcmc + kWalkTabPad rows; the pad rows stay zero (walk_tab_base)
+    const int64_t ent = 2 * k * (nmcmc + kWalkTabPad);
+    HC(B.rt_ix.ensure(ent * 8), "alloc draw table");
+    HC(B.rt_sc.ensure(ent * 16), "alloc draw table");
+    HC(hipMemsetAsync(B.rt_ix.p, 0, ent * 8, s), "clear draw table");
+    HC(hipMemsetAsync(B.rt_sc.p, 0, ent * 16, s), "clear draw table");
     a.rt_ix = (unsigned long long*)B.rt_ix.p;
     a.rt_sc = (double2*)B.rt_sc.p;
   }

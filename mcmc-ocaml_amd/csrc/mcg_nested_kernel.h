@@ -100,6 +100,8 @@ struct NestArgs {
 #define MCG_NEST_PREFETCH 4
 #endif
 constexpr int kNestPrefetch = MCG_NEST_PREFETCH;    // DE steps whose partner rows are in flight
+// pad rows per draw-table half: the walker loads entries up to 3 prefetch groups past its step
+constexpr int kWalkTabPad = 3 * kNestPrefetch;
 #ifndef MCG_NEST_WALK_BLOCK
 #define MCG_NEST_WALK_BLOCK 64
 #endif
@@ -126,9 +128,12 @@ __device__ __forceinline__ void walk_draw(const NestArgs& a, uint32_t wid, uint3
 
 // the draws of every walker step of the generation that starts at replacement mrep, entries
 // [e0, k nmcmc) with stride `stride` (layout [step][walker])
-// Generation g = mrep / k uses half g & 1 of the double-buffered table.
+// Generation g = mrep / k uses half g & 1 of the double-buffered table.  Each half has
+// nmcmc + kWalkTabPad rows of k entries: the pad rows (zero: DE pair (0, 0), scale 0, log u 0,
+// written once at allocation) serve the walker's look-ahead loads past the last step, which
+// therefore need no clamp.
 __device__ __forceinline__ int64_t walk_tab_base(const NestArgs& a, int64_t mrep) {
-  return ((mrep / a.k) & 1) * a.k * a.nmcmc;
+  return ((mrep / a.k) & 1) * a.k * (a.nmcmc + kWalkTabPad);
 }
 __device__ __forceinline__ void walk_draws_fill(const NestArgs& a, int64_t mrep, int64_t e0, int64_t stride,
                                                 const double2* lt) {
@@ -358,10 +363,22 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
       for (int q = 0; q < 4; ++q)
         dst[4 * i + q] = Lay::valid(sub, i, q) ? src[Lay::dim(sub, i, q)] : 0.0;
   };
-  // TAB: the table holds row byte offsets (32-bit: the live set is below 4 GiB)
-  auto row_ptr = [&](uint32_t v) -> const double* {
-    if constexpr (TAB) return (const double*)((const char*)a.x + v);
-    else return a.x + (int64_t)v * D;
+  // TAB: the table holds row byte offsets (32-bit: the live set is below 4 GiB); the lane's
+  // first dim joins the offset, so a row load is the live set's base (SGPRs) plus one 32-bit
+  // VGPR (global_load ... saddr) and one 32-bit add per row
+  const char* const xb = (const char*)a.x;
+  const uint32_t lane_b = 32u * (uint32_t)sub;
+  auto load_row_off = [&](double* dst, uint32_t v) {
+    const char* src = xb + (v + lane_b);
+#pragma unroll
+    for (int i = 0; i < Lay::NCL; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        dst[4 * i + q] = Lay::valid(sub, i, q) ? *(const double*)(src + 8 * (4 * P * i + q)) : 0.0;
+  };
+  auto refill = [&](double* dst, uint32_t v) {
+    if constexpr (TAB) load_row_off(dst, v);
+    else load_row_at(dst, a.x + (int64_t)v * D);
   };
   auto load_row = [&](double* dst, int64_t row) {
     const double* __restrict__ src = a.x + row * D;
@@ -423,11 +440,8 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   // the walker's single wave on its SIMD
   const double2* const tsc_lane = a.rt_sc + tbase + wc;
   const unsigned long long* const tix_lane = a.rt_ix + tbase + wc;
-  const uint32_t tk = (uint32_t)a.k, tlast = (uint32_t)(a.nmcmc - 1);
-  auto tab_off = [&](int64_t st) -> uint32_t {
-    const uint32_t s32 = (uint32_t)st;
-    return (s32 < tlast ? s32 : tlast) * tk;
-  };
+  const uint32_t tk = (uint32_t)a.k;
+  auto tab_off = [&](int64_t st) -> uint32_t { return (uint32_t)st * tk; };   // pad rows: no clamp
   unsigned long long tix_cur[PD], tix_next[PD];
   double2 tsc_cur[PD], tsc_next[PD];
   if constexpr (TAB) {
@@ -449,8 +463,8 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
     } else {
       pick(u, i0, j0);
     }
-    load_row_at(bi[u], row_ptr(i0));
-    load_row_at(bj[u], row_ptr(j0));
+    refill(bi[u], i0);
+    refill(bj[u], j0);
   }
   // whole groups of PD steps with no data-dependent branches around the loads, so the compiler
   // can count the in-flight loads (vmcnt) across iterations; steps past nmcmc only compute
@@ -529,8 +543,8 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
       const bool live = s0 + u < a.nmcmc;
 #pragma unroll
       for (int d = 0; d < NL; ++d) y[d] = cur[d] + dsc_g[u] * (bj[u][d] - bi[u][d]);
-      load_row_at(bi[u], row_ptr(ip_g[u]));            // refill slot u with step s + PD's rows
-      load_row_at(bj[u], row_ptr(jp_g[u]));
+      refill(bi[u], ip_g[u]);                          // refill slot u with step s + PD's rows
+      refill(bj[u], jp_g[u]);
       const bool ok = tgt.constraint(y, sub, a.m, thr);
       const double lpy = tgt.prior(y, sub, a.m);
       const double ml = ok ? lpy : -__builtin_inf();
