@@ -310,6 +310,7 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   a.newk_slot = B.newk.s();
   a.rank = (int*)B.rank.p;
   a.est_in_rank = k <= 4096 ? 1 : 0;                  // the counted-rank sort path
+  a.fuse_retire = a.est_in_rank && std::getenv("MCG_NESTED_RETIRE_KERNEL") == nullptr;
   // the walkers' draws of a generation in a table the previous merge fills (when it fits)
   a.rt_ix = nullptr;
   a.rt_sc = nullptr;
@@ -436,7 +437,7 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
       if (ctx->timing) timing_begin(ctx, &e0, &e1);
       HC(walk(a, s), "nested walk");
       if (ctx->timing) timing_end(ctx, e0, e1, 1);
-      HC(launch_retire(a, D, s), "nested retire");
+      if (!a.fuse_retire) HC(launch_retire(a, D, s), "nested retire");
       bool nk_tmp = false;
       if (k <= 4096) {
         HC(launch_sort_new_small(a, B.newk_tmp.l(), B.newk_tmp.t(), B.newk_tmp.s(), s), "sort new keys");

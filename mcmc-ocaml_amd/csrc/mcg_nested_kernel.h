@@ -72,6 +72,9 @@ struct NestArgs {
   unsigned long long* rt_ix;
   double2* rt_sc;
   int32_t est_in_rank;      // the estimate is folded by an extra rank_count workgroup (k <= 4096)
+  int32_t fuse_retire;      // (k <= 4096) no retire kernel: each walker retires its own dead point
+                            // at its start and emits its key at its end; the rank-count workgroups
+                            // put the new points into the freed slots
   int32_t sym_box;          // box prior with lo[d] == -hi[d] for every d: tested as |y| <= hi
   uint32_t row_bytes;       // D * 8: the draw table holds DE pairs as row byte offsets
   double* tv;               // ll + log dv of this generation's dead points (padded pow2)
@@ -329,6 +332,27 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
     // generation's table and leave
     if (threadIdx.x >= 64) {
       const int64_t nf = blockDim.x - 64;
+      if (a.fuse_retire) {
+        // retire the dead points of this workgroup's walkers (see below): element e of the
+        // (64 / P) x D block, the scalars with d == 0
+        const int64_t w0 = (int64_t)blockIdx.x * (64 / P);
+        for (int64_t e = threadIdx.x - 64; e < (64 / P) * D; e += nf) {
+          const int64_t wj = w0 + e / D;
+          const int d = (int)(e % D);
+          if (wj >= a.k) break;
+          const int rs = a.key_slot[wj];
+          const int64_t m = a.mrep + wj;
+          a.dead_x[m * D + d] = a.x[(int64_t)rs * D + d];
+          if (d == 0) {
+            const double lls = a.ll[rs];
+            a.dead_ll[m] = lls;
+            a.dead_lp[m] = a.lp[rs];
+            const double lv = a.st->log_vol + a.prefix[wj];
+            __hip_atomic_store(a.tv + wj, lls + (lv + a.qadd[wj]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            a.rank[wj] = 0;
+          }
+        }
+      }
       walk_draws_fill(a, a.mrep + a.k, (int64_t)blockIdx.x * nf + (threadIdx.x - 64), (int64_t)gridDim.x * nf, s_lt);
       return;
     }
@@ -342,6 +366,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   const Rng rng{a.k0, a.k1};
   const uint32_t wid = (uint32_t)(a.mrep + wc);
   const double thr = a.key_ll[a.k - 1];
+  const int ret_slot = a.key_slot[wc];               // the live slot walker w's point replaces
   const uint32_t n = (uint32_t)a.n;
   // start: a uniformly random live point satisfying the constraint (nested.ml:63); with k = 1
   // every live point does, so this is Random.int nlive
@@ -466,6 +491,27 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
     refill(bi[u], i0);
     refill(bj[u], j0);
   }
+  if (!TAB && a.fuse_retire && active) {
+    // replace_live_point's retirement (nested.ml:26-43, slot form) of the w-th lowest point: the
+    // live set stays frozen during the walk, so its row can go to the dead buffer now -- after
+    // the first DE rows are in flight, so that their wait is not queued behind these loads (with
+    // the draw table the workgroup's spare waves do this, off the walker's SIMD)
+    const int64_t m = a.mrep + w;
+    const double* __restrict__ src = a.x + (int64_t)ret_slot * D;
+#pragma unroll
+    for (int i = 0; i < Lay::NCL; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (Lay::valid(sub, i, q)) a.dead_x[m * D + Lay::dim(sub, i, q)] = src[Lay::dim(sub, i, q)];
+    if (sub == 0) {
+      const double lls = a.ll[ret_slot];
+      a.dead_ll[m] = lls;
+      a.dead_lp[m] = a.lp[ret_slot];
+      const double lv = a.st->log_vol + a.prefix[w];
+      __hip_atomic_store(a.tv + w, lls + (lv + a.qadd[w]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // nested.ml:138-141
+      a.rank[w] = 0;
+    }
+  }
   // whole groups of PD steps with no data-dependent branches around the loads, so the compiler
   // can count the in-flight loads (vmcnt) across iterations; steps past nmcmc only compute
   for (int64_t s0 = 0; s0 < a.nmcmc; s0 += PD) {
@@ -578,6 +624,11 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   if (sub == 0) {
     a.nll[w] = nl;
     a.nlp[w] = np;
+    if (a.fuse_retire) {                               // the new point's key
+      a.newk_ll[w] = nl;
+      a.newk_tie[w] = -(long long)(a.mrep + w + 1);
+      a.newk_slot[w] = ret_slot;
+    }
     if (!(nl >= thr)) nest_set(&a.st->error);        // nested.ml:70-72 -> Failure
   }
 }

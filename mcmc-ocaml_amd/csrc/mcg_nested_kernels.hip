@@ -264,6 +264,21 @@ __global__ void __launch_bounds__(256) rank_count_kernel(const NestArgs a, int n
     return;
   }
   const uint32_t ncount = gridDim.x - (a.est_in_rank ? 1u : 0u);
+  if (a.fuse_retire) {
+    // the retire kernel's slot writes (the walkers moved the dead rows and emitted the keys):
+    // walker j's point into the slot it replaces, spread over the counting workgroups
+    const int64_t kD = a.k * a.row_bytes / 8, D = a.row_bytes / 8;
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < kD; g += (int64_t)ncount * blockDim.x) {
+      const int64_t j = g / D;
+      const int64_t d = g - j * D;
+      const int sj = a.newk_slot[j];
+      a.x[(int64_t)sj * D + d] = a.nx[g];
+      if (d == 0) {
+        a.ll[sj] = a.nll[j];
+        a.lp[sj] = a.nlp[j];
+      }
+    }
+  }
   __shared__ double sl[kSub];
   __shared__ double s_ll[kSmallSort];                // last block: keys placed at their ranks
   __shared__ short s_j[kSmallSort];

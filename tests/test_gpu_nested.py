@@ -214,6 +214,22 @@ def test_nested_walker_box_forms_bit_exact(oracle, T, D, sym, diag):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("env", ["MCG_NESTED_NO_TABLE", "MCG_NESTED_RETIRE_KERNEL", "both"])
+@pytest.mark.parametrize("D", [3, 16])
+def test_nested_alternate_paths_bit_exact(oracle, T, monkeypatch, env, D):
+    """The paths the default run does not take: walkers drawing their own random numbers (no
+    draw table: what a generation too big for the table uses) and the separate retire kernel
+    (k > 4096 uses it) -- the same dead points as the oracle, bit for bit."""
+    for var in (["MCG_NESTED_NO_TABLE", "MCG_NESTED_RETIRE_KERNEL"] if env == "both" else [env]):
+        monkeypatch.setenv(var, "1")
+    lik = T.gauss_shell(np.zeros(D), 1.0, 0.2)
+    pri = T.box(-2 * np.ones(D), 2 * np.ones(D))
+    g = gpu_nested(lik, pri, 14, nlive=300, nmcmc=15, mode_hopping_frac=0.1, k=30, max_dead=30 * 30)
+    o = oracle_nested(oracle, lik, pri, 14, nlive=300, nmcmc=15, mode_hop=0.1, k=30, max_iter=30 * 30)
+    assert_nested_same(g, o)
+
+
+@pytest.mark.gpu
 def test_nested_rank_count_sort_ties_and_partial_runs(oracle, T):
     """k = 1000 new keys per generation: three full 256-key runs and a partial one in the
     counted-rank sort, and walks of 2 steps on a thin shell, so many walkers reject every step and
