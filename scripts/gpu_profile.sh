@@ -8,3 +8,4 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof/fetch -o run --o
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof/write -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/prof/write.log 2>&1 || exit $?
 echo profile-ok
 python3 scripts/pmc_traffic.py gpurun_out/prof gpurun_out/prof/pmc_traffic.json
+python3 scripts/trace_summary.py gpurun_out/prof/trace/run_kernel_trace.csv gpurun_out/prof/trace_summary.json
