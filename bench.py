@@ -6,9 +6,12 @@
 Workload (BASELINE.json configs[1]): D=32 diagonal-Gaussian log-target, isotropic Gaussian
 proposal s = 2.38/sqrt(D) * median(sigma), flat box prior [-10, 10]^32, 65,536 independent chains
 per GPU (weak scaling), starts drawn from the target.  One bench "step" = one fused kernel launch
-of --sweeps MH sweeps over every chain (default 100), so the default --warmup 10 --steps 100 is
-the C2 job: nbin = 1,000 burn-in sweeps, then 10,000 recorded sweeps whose samples are folded on
-the device into Welford moments and harmonic-mean partials.  The timed region covers the K steps
+of --sweeps MH sweeps over every chain (default 1,000: one launch at the runtime's own launch
+length, which caps a launch at min(4096, 2^26/N) = 1,024 sweeps for 65,536 chains), so the default
+--warmup 1 --steps 10 is the C2 job: nbin = 1,000 burn-in sweeps, then 10,000 recorded sweeps
+whose samples are folded on the device into Welford moments and harmonic-mean partials.  (Each
+launch also pays a fixed ~47 us: the chain state and accumulators round-trip through HBM; at 100
+sweeps per launch that was 14 % of the launch, at 1,000 it is 1.7 %.  DESIGN.md §6.)  The timed region covers the K steps
 plus the end-of-run reduction (tile kernel, RCCL all-gather of tile partials, host combine).
 After it (outside `value`), the |delta log-evidence| half of the metric: Nested.nested_evidence on
 the same target, one replica per GPU merged over the ranks (--nested-nlive per GPU).
@@ -101,9 +104,9 @@ def pmc_traffic(D, N, S):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--sweeps", type=int, default=100, help="MH sweeps per bench step (one launch)")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--sweeps", type=int, default=1000, help="MH sweeps per bench step (one launch, <= 1024)")
     ap.add_argument("--chains", type=int, default=65536, help="chains per GPU")
     ap.add_argument("--ndim", type=int, default=32)
     ap.add_argument("--lanes", type=int, default=0, help="lanes per chain (0 = auto)")

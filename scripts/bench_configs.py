@@ -136,14 +136,14 @@ def c3(args):
 def c4(args):
     """Interpolate_pdf kD-tree independence proposal, D=8 N(0,1) target, M=32,768 exact draws,
     32,768 chains."""
-    D, N, M, S, K = 8, 32768, 32768, 100, args.launches
+    D, N, M, S, K = 8, 32768, 32768, 1000, args.launches // 10
     rng = np.random.default_rng(4)
     pts = rng.normal(size=(M, D))
     lo, hi = -10 * np.ones(D), 10 * np.ones(D)
     ctx = Context(seed=args.seed)
     ctx.set_model(T.diag_gauss(np.zeros(D), np.ones(D)), T.box(lo, hi), T.KdInterp(pts, lo, hi))
     ctx.init(rng.normal(size=(D, N)))
-    ctx.run(nbin=10 * S, nskip=1, n_rec=1, record_x=False, record_llp=False, accumulate=True)
+    ctx.run(nbin=S, nskip=1, n_rec=1, record_x=False, record_llp=False, accumulate=True)
     ctx.sync()
     ctx.set_timing(True)
     t0 = time.perf_counter()
@@ -169,7 +169,7 @@ def c4(args):
 def c5(args):
     """D=64 full-covariance Gaussian, Sigma = Q diag(lambda) Q^T, lambda log-uniform [0.1, 10],
     131,072 chains (one GPU's share of 1,048,576 over 8)."""
-    D, N, S, K = 64, args.c5_chains, 100, args.launches
+    D, N, S, K = 64, args.c5_chains, 500, args.launches // 5
     rng = np.random.default_rng(5)
     Q, _ = np.linalg.qr(rng.normal(size=(D, D)))
     lam = np.exp(rng.uniform(math.log(0.1), math.log(10.0), D))
@@ -210,7 +210,8 @@ def main():
     ap.add_argument("--nlive", type=int, default=131072)
     ap.add_argument("--k", type=int, default=4096)
     ap.add_argument("--nmcmc", type=int, default=100)
-    ap.add_argument("--launches", type=int, default=100, help="C4/C5: timed launches of 100 sweeps")
+    ap.add_argument("--launches", type=int, default=100,
+                    help="C4/C5: timed sweeps / 100 (C4: launches of 1,000 sweeps, C5: of 500 -- at or under\n                    the runtime's own launch length min(4096, 2^26/N))")
     ap.add_argument("--reps", type=int, default=3, help="C3: timed nested runs (median reported)")
     ap.add_argument("--c5-chains", type=int, default=131072)
     args = ap.parse_args()

@@ -2,7 +2,7 @@
 # rocprofv3 kernel-trace stats of the bench, then two separate PMC passes (FETCH_SIZE, WRITE_SIZE).
 mkdir -p gpurun_out/prof
 export TMPDIR=/tmp
-ARGS="--steps 50 --warmup 5 --no-cpu-baseline $*"
+ARGS="--steps 10 --warmup 1 --no-cpu-baseline $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/trace -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/prof/trace.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof/fetch -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/prof/fetch.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof/write -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/prof/write.log 2>&1 || exit $?

@@ -5,7 +5,7 @@ scripts/gpu_profile.sh (FETCH_SIZE and WRITE_SIZE in separate runs, values in KB
 gfx950 correction (MI355X_MICROARCH.md, HBM/rocprofv3 section): FETCH_SIZE reports half the bytes
 of wide coalesced streaming reads -> doubled; WRITE_SIZE is exact for 16-B/lane stores.
 
-  python scripts/pmc_traffic.py gpurun_out/prof profiles/r01/pmc_traffic.json [--ndim 32 --chains 65536 --sweeps 100]
+  python scripts/pmc_traffic.py gpurun_out/prof profiles/r01/pmc_traffic.json [--ndim 32 --chains 65536 --sweeps 1000]
 """
 import argparse
 import collections
@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--kernel", default="mcg::mh_kernel<")
     ap.add_argument("--ndim", type=int, default=32)
     ap.add_argument("--chains", type=int, default=65536)
-    ap.add_argument("--sweeps", type=int, default=100)
+    ap.add_argument("--sweeps", type=int, default=1000)
     a = ap.parse_args()
     fetch = per_kernel(os.path.join(a.prof_dir, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(a.prof_dir, "write", "run_counter_collection.csv"), "WRITE_SIZE")
