@@ -438,11 +438,17 @@ __device__ __forceinline__ int xor_lane_i(int v) {
   if constexpr (!MCG_DPP_XLANE) return __shfl_xor(v, M, 64);
   else if constexpr (M == 1) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);   // [1,0,3,2]
   else if constexpr (M == 2) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+  else if constexpr (M == 4) {
+    // two row shifts, each writing one half of every 8-lane group (bank_mask: banks of 4 lanes):
+    // lanes 0-3 (banks 0, 2) take lane + 4 (row_shl:4), lanes 4-7 (banks 1, 3) lane - 4 (row_shr:4)
+    const int t = __builtin_amdgcn_update_dpp(0, v, 0x104, 0xF, 0x5, false);
+    return __builtin_amdgcn_update_dpp(t, v, 0x114, 0xF, 0xA, false);
+  }
   else return __shfl_xor(v, M, 64);
 }
 template <int M>
 __device__ __forceinline__ double xor_lane_d(double v) {
-  if constexpr (MCG_DPP_XLANE && (M == 1 || M == 2)) {
+  if constexpr (MCG_DPP_XLANE && (M == 1 || M == 2 || M == 4)) {
     return __hiloint2double(xor_lane_i<M>(__double2hiint(v)), xor_lane_i<M>(__double2loint(v)));
   } else {
     return __shfl_xor(v, M, 64);

@@ -310,6 +310,10 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   a.newk_slot = B.newk.s();
   a.rank = (int*)B.rank.p;
   a.est_in_rank = k <= 4096 ? 1 : 0;                  // the counted-rank sort path
+  // MCG_NEST_LANES: lanes per walker (8 for D % 32 == 0; 4 at D = 8, 8 at D = 16: two dims per
+  // lane), "wide" for that wider split, "narrow" for the one-block-per-call split
+  if (const char* e = std::getenv("MCG_NEST_LANES"))
+    a.lanes_hint = !std::strcmp(e, "wide") ? -1 : !std::strcmp(e, "narrow") ? -2 : std::atoi(e);
   a.fuse_retire = a.est_in_rank && std::getenv("MCG_NESTED_RETIRE_KERNEL") == nullptr;
   // the walkers' draws of a generation in a table the previous merge fills (when it fits)
   a.rt_ix = nullptr;

@@ -76,6 +76,7 @@ struct NestArgs {
                             // at its start and emits its key at its end; the rank-count workgroups
                             // put the new points into the freed slots
   int32_t sym_box;          // box prior with lo[d] == -hi[d] for every d: tested as |y| <= hi
+  int32_t lanes_hint;       // lanes per walker requested by MCG_NEST_LANES (0: the default)
   uint32_t row_bytes;       // D * 8: the draw table holds DE pairs as row byte offsets
   double* tv;               // ll + log dv of this generation's dead points (padded pow2)
   const double* prefix;     // [k+1] sum_{j'<j} log1p(-1/(n-j'))
@@ -154,13 +155,60 @@ __device__ __forceinline__ void walk_draws_fill(const NestArgs& a, int64_t mrep,
   }
 }
 
+// Lane layout of a walker on P lanes: lane `sub` owns the W-dim blocks c = sub, sub + P, ...
+// (dims W c .. W c + W - 1).  W = 4 is the MH kernel's Layout (Philox blocks); W = 2 when D = 2P
+// (D = 8 on 4 lanes, D = 16 on 8), whose lanes each hold two dims: the two lanes of a canonical
+// accumulator (dims 4j .. 4j + 3, DESIGN.md §Canonical sums) then chain their fmas in dim order
+// (reduce_canon_w2).  The walker's DE proposal draws no per-dim random numbers, so any split of
+// the dims is the same computation.
+template <int D, int P>
+struct WalkLayout {
+  static constexpr int W = (P > 1 && D == 2 * P) ? 2 : 4;
+  static constexpr int NC = (D + W - 1) / W;               // blocks
+  static constexpr int NCL = (NC + P - 1) / P;             // blocks owned by one lane
+  static constexpr int NL = NCL * W;                       // local dims
+  static constexpr int NA = W == 2 ? 1 : 8 / P;            // local accumulators (W = 4)
+  static_assert(P == 1 || P == 2 || P == 4 || P == 8, "P must divide 8");
+  static_assert(P == 1 || D % (W * P) == 0, "P > 1 needs D % WP == 0");
+  __device__ static __forceinline__ int dim(int sub, int i, int q) { return W * (sub + P * i) + q; }
+  __device__ static __forceinline__ bool valid(int sub, int i, int q) {
+    return q < W && (P > 1 || (W * i + q) < D);
+  }
+};
+
+// the canonical sum for W = 2 (D = 2P): lane sub holds the terms of dims 2 sub, 2 sub + 1, which
+// belong to accumulator A_j, j = sub / 2.  The even lane of the pair folds dims 4j, 4j + 1 from
+// zero, the odd lane continues from that partial with dims 4j + 2, 4j + 3 (the sequential fma
+// chain of A_j), and the odd lanes (A_0 .. A_{P/2-1}) meet in the canonical tree
+// ((A0 + A4) + (A2 + A6)) + ((A1 + A5) + (A3 + A7)), whose A_4 .. A_7 are zero here (x + 0 = x
+// for the sums of squares): (A0 + A2) + (A1 + A3) at P = 8, A0 + A1 at P = 4.  Even lanes take
+// their odd neighbour's value.  Additions are commutative, so every lane of the tree holds the
+// same bits.
+template <int P>
+__device__ __forceinline__ double reduce_canon_w2(double e0, double e1, int sub) {
+  static_assert(P == 4 || P == 8, "W = 2 walkers run on 4 or 8 lanes");
+  const double t = fma(e1, e1, fma(e0, e0, 0.0));
+  const double tp = xor_lane_d<1>(t);
+  const double a = fma(e1, e1, fma(e0, e0, tp));
+  double c;
+  if constexpr (P == 8) {
+    const double b = a + xor_lane_d<4>(a);
+    c = b + xor_lane_d<2>(b);
+  } else {
+    c = a + xor_lane_d<2>(a);
+  }
+  const double o = xor_lane_d<1>(c);
+  return (sub & 1) ? c : o;
+}
+
 // The log-target constants of one walker lane (its dims of mu/sigma or the shell centre, the box
 // bounds), loaded into registers once per launch.  Loaded per step through the parameter
 // pointers they would queue behind the prefetched DE rows in the in-order vector-memory counter
 // and expose the full load latency every step.  Same operations as eval_lik / eval_prior.
 template <int D, int P, int LIK, bool SYM = false>
 struct WalkTarget {
-  using Lay = Layout<D, P>;
+  using Lay = WalkLayout<D, P>;
+  static constexpr int W = Lay::W;
   static constexpr int NL = Lay::NL;
   static constexpr bool kReg =
       (LIK == MCG_LIK_DIAG_GAUSS || LIK == MCG_LIK_GAUSS_SHELL || LIK == MCG_LIK_FLAT) && NL <= 8;
@@ -177,8 +225,8 @@ struct WalkTarget {
 #pragma unroll
       for (int i = 0; i < Lay::NCL; ++i)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int j = 4 * i + k;
+        for (int k = 0; k < W; ++k) {
+          const int j = W * i + k;
           const bool v = Lay::valid(sub, i, k);
           const int d = v ? Lay::dim(sub, i, k) : 0;
           m0[j] = (v && LIK != MCG_LIK_FLAT) ? q[d] : 0.0;
@@ -198,21 +246,30 @@ struct WalkTarget {
     } else if constexpr (LIK == MCG_LIK_FLAT) {
       return 0.0;
     } else {
-      double A[Lay::NA];
+      double S;
+      if constexpr (W == 2) {
+        double e[2];
 #pragma unroll
-      for (int j = 0; j < Lay::NA; ++j) A[j] = 0.0;
+        for (int j = 0; j < 2; ++j)
+          e[j] = LIK == MCG_LIK_DIAG_GAUSS ? fma(y[j], m1[j], -m0[j]) : y[j] - m0[j];
+        S = reduce_canon_w2<P>(e[0], e[1], sub);
+      } else {
+        double A[Lay::NA];
 #pragma unroll
-      for (int i = 0; i < Lay::NCL; ++i)
+        for (int j = 0; j < Lay::NA; ++j) A[j] = 0.0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (!Lay::valid(sub, i, k)) continue;
-          const int j = 4 * i + k;
-          double e;
-          if constexpr (LIK == MCG_LIK_DIAG_GAUSS) e = fma(y[j], m1[j], -m0[j]);
-          else e = y[j] - m0[j];
-          A[i % Lay::NA] = fma(e, e, A[i % Lay::NA]);
-        }
-      const double S = reduce_canon<P>(A);
+        for (int i = 0; i < Lay::NCL; ++i)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            if (!Lay::valid(sub, i, k)) continue;
+            const int j = 4 * i + k;
+            double e;
+            if constexpr (LIK == MCG_LIK_DIAG_GAUSS) e = fma(y[j], m1[j], -m0[j]);
+            else e = y[j] - m0[j];
+            A[i % Lay::NA] = fma(e, e, A[i % Lay::NA]);
+          }
+        S = reduce_canon<P>(A);
+      }
       if constexpr (LIK == MCG_LIK_DIAG_GAUSS) {
         return c0 - 0.5 * S;
       } else {
@@ -255,19 +312,24 @@ struct WalkTarget {
   // lik(y) >= thr, exactly as the comparison of the evaluated likelihood (mcmc_logl, nested.ml:54-59)
   __device__ __forceinline__ bool constraint(const double* y, int sub, const MhArgs& a, double thr) const {
     if constexpr (kReg && LIK == MCG_LIK_GAUSS_SHELL) {
-      double A[Lay::NA];
+      double S;
+      if constexpr (W == 2) {
+        S = reduce_canon_w2<P>(y[0] - m0[0], y[1] - m0[1], sub);
+      } else {
+        double A[Lay::NA];
 #pragma unroll
-      for (int j = 0; j < Lay::NA; ++j) A[j] = 0.0;
+        for (int j = 0; j < Lay::NA; ++j) A[j] = 0.0;
 #pragma unroll
-      for (int i = 0; i < Lay::NCL; ++i)
+        for (int i = 0; i < Lay::NCL; ++i)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (!Lay::valid(sub, i, k)) continue;
-          const int j = 4 * i + k;
-          const double e = y[j] - m0[j];
-          A[i % Lay::NA] = fma(e, e, A[i % Lay::NA]);
-        }
-      const double S = reduce_canon<P>(A);
+          for (int k = 0; k < 4; ++k) {
+            if (!Lay::valid(sub, i, k)) continue;
+            const int j = 4 * i + k;
+            const double e = y[j] - m0[j];
+            A[i % Lay::NA] = fma(e, e, A[i % Lay::NA]);
+          }
+        S = reduce_canon<P>(A);
+      }
       bool in = (S >= s_in_lo) & (S <= s_in_hi);
       const bool out = (S < s_out_lo) | (S > s_out_hi);
       if (!(in | out)) {                             // guard band (rare): the exact evaluation
@@ -307,8 +369,9 @@ struct WalkTarget {
 // depend only on the RNG, so they are loaded while step s computes (one step of prefetch).
 template <int D, int LIK, int P, bool TAB, bool SYM>
 __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
-  using Lay = Layout<D, P>;
+  using Lay = WalkLayout<D, P>;
   constexpr int NL = Lay::NL;
+  constexpr int W = Lay::W;
   NT_STAMP(0, 0);
   __shared__ double2 s_lt[kLogTabN];                 // math tables staged in LDS (gathers)
   const double2* nt = kNrmTab;   // (an LDS copy costs more to stage than its gathers save: 62 vs 52 us)
@@ -385,21 +448,21 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
 #pragma unroll
     for (int i = 0; i < Lay::NCL; ++i)
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        dst[4 * i + q] = Lay::valid(sub, i, q) ? src[Lay::dim(sub, i, q)] : 0.0;
+      for (int q = 0; q < W; ++q)
+        dst[W * i + q] = Lay::valid(sub, i, q) ? src[Lay::dim(sub, i, q)] : 0.0;
   };
   // TAB: the table holds row byte offsets (32-bit: the live set is below 4 GiB); the lane's
   // first dim joins the offset, so a row load is the live set's base (SGPRs) plus one 32-bit
   // VGPR (global_load ... saddr) and one 32-bit add per row
   const char* const xb = (const char*)a.x;
-  const uint32_t lane_b = 32u * (uint32_t)sub;
+  const uint32_t lane_b = 8u * W * (uint32_t)sub;
   auto load_row_off = [&](double* dst, uint32_t v) {
     const char* src = xb + (v + lane_b);
 #pragma unroll
     for (int i = 0; i < Lay::NCL; ++i)
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        dst[4 * i + q] = Lay::valid(sub, i, q) ? *(const double*)(src + 8 * (4 * P * i + q)) : 0.0;
+      for (int q = 0; q < W; ++q)
+        dst[W * i + q] = Lay::valid(sub, i, q) ? *(const double*)(src + 8 * (W * P * i + q)) : 0.0;
   };
   auto refill = [&](double* dst, uint32_t v) {
     if constexpr (TAB) load_row_off(dst, v);
@@ -410,8 +473,8 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
 #pragma unroll
     for (int i = 0; i < Lay::NCL; ++i)
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        dst[4 * i + q] = Lay::valid(sub, i, q) ? src[Lay::dim(sub, i, q)] : 0.0;
+      for (int q = 0; q < W; ++q)
+        dst[W * i + q] = Lay::valid(sub, i, q) ? src[Lay::dim(sub, i, q)] : 0.0;
   };
   // differential_evolution_proposal's pick_samples (mcmc.ml:199-203): i, then j != i
   auto pick = [&](int64_t s, uint32_t& i, uint32_t& j) {
@@ -501,7 +564,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
 #pragma unroll
     for (int i = 0; i < Lay::NCL; ++i)
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < W; ++q)
         if (Lay::valid(sub, i, q)) a.dead_x[m * D + Lay::dim(sub, i, q)] = src[Lay::dim(sub, i, q)];
     if (sub == 0) {
       const double lls = a.ll[ret_slot];
@@ -619,8 +682,8 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
 #pragma unroll
   for (int i = 0; i < Lay::NCL; ++i)
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (Lay::valid(sub, i, q)) a.nx[w * D + Lay::dim(sub, i, q)] = cur[4 * i + q];
+    for (int q = 0; q < W; ++q)
+      if (Lay::valid(sub, i, q)) a.nx[w * D + Lay::dim(sub, i, q)] = cur[W * i + q];
   if (sub == 0) {
     a.nll[w] = nl;
     a.nlp[w] = np;
@@ -659,12 +722,8 @@ __global__ void __launch_bounds__(256) nest_init_kernel(const NestArgs a, double
   keys_slot[s] = (int)s;
 }
 
-template <int D, int LIK>
-hipError_t launch_nest_walk(const NestArgs& a, hipStream_t st) {
-  // lanes per walker: the separable likelihoods split the dims over 4 (or 2) lanes when D is a
-  // multiple of 16 (8), which gives the few-thousand-walker generations 4x (2x) the lanes
-  constexpr bool sep = LIK == MCG_LIK_DIAG_GAUSS || LIK == MCG_LIK_GAUSS_SHELL || LIK == MCG_LIK_FLAT;
-  constexpr int P = (sep && D % 16 == 0) ? 4 : (sep && D % 8 == 0) ? 2 : 1;
+template <int D, int LIK, int P>
+hipError_t launch_nest_walk_p(const NestArgs& a, hipStream_t st) {
   // small workgroups: a generation has only k * P lanes, so one wave per workgroup spreads them
   // over all CUs (their LDS tables, L1 and scalar units) instead of packing four per CU
   const int block = kNestWalkBlock;
@@ -676,6 +735,25 @@ hipError_t launch_nest_walk(const NestArgs& a, hipStream_t st) {
   else if (a.rt_ix) hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, false>), gt, bt, 0, st, a);
   else hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, false, false>), dim3((unsigned)grid), dim3(block), 0, st, a);
   return hipGetLastError();
+}
+
+template <int D, int LIK>
+hipError_t launch_nest_walk(const NestArgs& a, hipStream_t st) {
+  // lanes per walker: the separable likelihoods split the dims over several lanes, which gives
+  // the few-thousand-walker generations that many times the lanes and shortens each walker's
+  // serial step (fewer dims per lane).  One 4-dim block per lane on 8 lanes when D % 32 == 0
+  // (the bench's D = 32 leg: nested run 0.125 -> 0.103 s, A/B on one box), else 4 (D % 16 == 0)
+  // or 2 (D % 8 == 0) lanes; MCG_NEST_LANES: "narrow" (4 at D % 32 == 0), "wide" (two dims per
+  // lane at D = 8 / 16: 4 / 8 lanes), or the lane count
+  constexpr bool sep = LIK == MCG_LIK_DIAG_GAUSS || LIK == MCG_LIK_GAUSS_SHELL || LIK == MCG_LIK_FLAT;
+  constexpr int P = (sep && D % 16 == 0) ? 4 : (sep && D % 8 == 0) ? 2 : 1;
+  if constexpr (sep && D % 32 == 0) {
+    if (a.lanes_hint != -2 && a.lanes_hint != 4) return launch_nest_walk_p<D, LIK, 8>(a, st);
+  }
+  if constexpr (sep && (D == 16 || D == 8)) {          // two dims per lane (WalkLayout W = 2)
+    if (a.lanes_hint == 2 * P || a.lanes_hint == -1) return launch_nest_walk_p<D, LIK, 2 * P>(a, st);
+  }
+  return launch_nest_walk_p<D, LIK, P>(a, st);
 }
 
 template <int D, int LIK>

@@ -198,6 +198,22 @@ def test_nested_multilane_walkers_bit_exact(oracle, T, D, k):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("lanes", ["narrow", "wide"])
+@pytest.mark.parametrize("D,diag", [(8, False), (16, False), (16, True), (32, True), (64, False)])
+def test_nested_walker_lane_splits_bit_exact(oracle, T, monkeypatch, lanes, D, diag):
+    """Every split of a walker's dims over lanes gives the oracle's dead points bit for bit: one
+    4-dim block per lane on 8 lanes (D % 32 == 0, the default there) or on 4, and two dims per
+    lane (D = 8 on 4 lanes, D = 16 on 8), whose lane pairs chain the canonical accumulator."""
+    monkeypatch.setenv("MCG_NEST_LANES", lanes)
+    lik = (T.diag_gauss(np.linspace(-0.3, 0.3, D), np.linspace(0.4, 0.8, D)) if diag
+           else T.gauss_shell(np.zeros(D), 1.0, 0.2))
+    pri = T.box(-2 * np.ones(D), 2 * np.ones(D))
+    g = gpu_nested(lik, pri, 15, nlive=300, nmcmc=15, mode_hopping_frac=0.1, k=24, max_dead=24 * 30)
+    o = oracle_nested(oracle, lik, pri, 15, nlive=300, nmcmc=15, mode_hop=0.1, k=24, max_iter=24 * 30)
+    assert_nested_same(g, o)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("D,sym,diag", [(16, False, False), (16, False, True), (16, True, True)])
 def test_nested_walker_box_forms_bit_exact(oracle, T, D, sym, diag):
     """The walker's two box tests: a box symmetric in every dim is tested as |y| <= h (one
