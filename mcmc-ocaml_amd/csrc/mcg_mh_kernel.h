@@ -299,6 +299,10 @@ struct AccumCfg {
                            // 2: two calls' gathers in flight together (the second hides behind the first)
 #endif
 
+#ifndef MCG_NRM_PIPE
+#define MCG_NRM_PIPE 1     // three-wave kernels gather each normal's rows one normal ahead
+#endif
+
 #ifndef MCG_HM_LDS
 #define MCG_HM_LDS 1       // harmonic-mean partials of the record classes in LDS (not VGPRs)
 #endif
@@ -572,6 +576,35 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
         philox_multi<L::NCL>(wl, gid, tlo, cidx, (TAG_MH << 16) | (thi & 0xFFFFu), rng.k0, rng.k1);
       }
       // the coordinates and terms of call i from its four normals
+      auto dims1 = [&](const int i, const int k, const double zk) {
+        const int cc = sub + P * i;
+        if (!L::valid(sub, i, k)) return;
+        const int d = 4 * cc + k;
+        const double yv = fma(UNI ? a.uni_s : qprop[d], zk, x[4 * i + k]);
+        y[4 * i + k] = yv;
+        double rcm = 0.0, rci = 0.0;
+        if constexpr (kRcLds) {
+          const double2 rc = s_rc[d];
+          rci = rc.x;
+          rcm = rc.y;
+        } else if constexpr (UNI) {
+          rcm = rc_m[4 * i + k];
+          rci = rc_i[4 * i + k];
+        }
+        if constexpr (LIK == MCG_LIK_DIAG_GAUSS) {
+          const double e = UNI ? fma(yv, rci, -rcm) : fma(yv, qlik[D + d], -qlik[d]);
+          A[i % L::NA] = fma(e, e, A[i % L::NA]);
+        } else if constexpr (LIK == MCG_LIK_GAUSS_SHELL) {
+          const double e = yv - (UNI ? rcm : qlik[d]);
+          A[i % L::NA] = fma(e, e, A[i % L::NA]);
+        }
+        if constexpr (UNI == 2) {
+          ok = ok & (__builtin_fabs(yv) <= a.uni_hi);
+        } else {
+          const double lo = UNI ? a.uni_lo : qpri[d], hi = UNI ? a.uni_hi : qpri[D + d];
+          ok = ok & (yv >= lo) & (yv <= hi);
+        }
+      };
       auto dims = [&](const int i, const double* z) {
         const int cc = sub + P * i;
 #pragma unroll
@@ -608,6 +641,25 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
         }
       };
       constexpr int kStride = MCG_NRM_BATCH == 2 ? 2 : 1;
+      if constexpr (MCG_NRM_PIPE && MhShape<D, P, LIK, PROP>::kThree) {
+        // one normal at a time with its table rows gathered one normal ahead: the gathers of
+        // normal m + 1 are in flight while normal m is finished and its dim's terms computed
+        auto word = [&](int m) -> uint32_t {
+          const u32x4 w = wl[m >> 2];
+          const int k = m & 3;
+          return k == 0 ? w.x : k == 1 ? w.y : k == 2 ? w.z : w.w;
+        };
+        constexpr int NM = 4 * L::NCL;
+        constexpr int AH = MCG_NRM_PIPE;               // normals whose gathers are in flight
+        NrmPending q[AH + 1];
+#pragma unroll
+        for (int m = 0; m < AH && m < NM; ++m) q[m] = pnormal_issue(word(m), s_nt);
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+          if (m + AH < NM) q[(m + AH) % (AH + 1)] = pnormal_issue(word(m + AH), s_nt);
+          dims1(m >> 2, m & 3, pnormal_finish(q[m % (AH + 1)]));
+        }
+      } else
 #pragma unroll
       for (int i = 0; i < L::NCL; i += kStride) {
         double z[4];
