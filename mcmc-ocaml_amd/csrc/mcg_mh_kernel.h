@@ -316,12 +316,21 @@ struct AccumCfg {
 // evaluated one at a time (no batched gathers: their 32 in-flight registers would spill);
 // C2 1.87e10 -> 1.96e10 MH steps/s against two waves with batched gathers (A/B on one box).
 // Everything else is left to the compiler's register budget (two waves where it fits).
+#ifndef MCG_PHILOX_SEQ
+#define MCG_PHILOX_SEQ 0   // experiment: the pipelined step's Philox calls computed one after another
+#endif
+#ifndef MCG_MH_THREE
+#define MCG_MH_THREE 1     // the fused Gaussian step with <= 8 dims per lane built for three waves per SIMD
+#endif
 #ifndef MCG_MH_FOUR
 #define MCG_MH_FOUR 0      // experiment: four waves per SIMD, UNI likelihood constants read from LDS
 #endif
 template <int D, int P, int LIK, int PROP>
 struct MhShape {
-  static constexpr bool kThree = separable<LIK, PROP>() && Layout<D, P>::NL <= 8 && MCG_MH_MIN_WAVES <= 3;
+  static constexpr bool kThree = separable<LIK, PROP>() && Layout<D, P>::NL <= 8 && MCG_MH_MIN_WAVES <= 3 && MCG_MH_THREE;
+  // table gathers of the fused step one (or MCG_NRM_PIPE) normals ahead
+  static constexpr bool kPipe = MCG_NRM_PIPE != 0 && separable<LIK, PROP>() && Layout<D, P>::NL <= 8 &&
+                                (kThree || MCG_NRM_PIPE > 1);
   static constexpr bool kFour = kThree && MCG_MH_FOUR;
   static constexpr int kWaves = kFour ? 4 : kThree ? 3 : MCG_MH_MIN_WAVES;
   // four waves per SIMD need two workgroups per CU within the LDS: 512 threads share the tables
@@ -569,7 +578,14 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
       const bool box = a.prior_kind != MCG_PRIOR_FLAT;
       // the lane's Philox calls of this step (c2 = call index sub + P i) advanced together
       u32x4 wl[L::NCL];
-      {
+      // MCG_PHILOX_SEQ (pipelined path): the lane's calls one after the other, the first call's
+      // first gathers issued before the next call's rounds (which then hide their latency)
+      constexpr bool kSeqPhilox = MhShape<D, P, LIK, PROP>::kPipe && MCG_PHILOX_SEQ;
+      auto philox_call = [&](int i) {
+        const uint32_t ci = (uint32_t)(sub + P * i);
+        philox_multi<1>(&wl[i], gid, tlo, &ci, (TAG_MH << 16) | (thi & 0xFFFFu), rng.k0, rng.k1);
+      };
+      if constexpr (!kSeqPhilox) {
         uint32_t cidx[L::NCL];
 #pragma unroll
         for (int i = 0; i < L::NCL; ++i) cidx[i] = (uint32_t)(sub + P * i);
@@ -641,7 +657,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
         }
       };
       constexpr int kStride = MCG_NRM_BATCH == 2 ? 2 : 1;
-      if constexpr (MCG_NRM_PIPE && MhShape<D, P, LIK, PROP>::kThree) {
+      if constexpr (MhShape<D, P, LIK, PROP>::kPipe) {
         // one normal at a time with its table rows gathered one normal ahead: the gathers of
         // normal m + 1 are in flight while normal m is finished and its dim's terms computed
         auto word = [&](int m) -> uint32_t {
@@ -652,8 +668,13 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
         constexpr int NM = 4 * L::NCL;
         constexpr int AH = MCG_NRM_PIPE;               // normals whose gathers are in flight
         NrmPending q[AH + 1];
+        if constexpr (kSeqPhilox) philox_call(0);
 #pragma unroll
         for (int m = 0; m < AH && m < NM; ++m) q[m] = pnormal_issue(word(m), s_nt);
+        if constexpr (kSeqPhilox) {
+#pragma unroll
+          for (int i = 1; i < L::NCL; ++i) philox_call(i);
+        }
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
           if (m + AH < NM) q[(m + AH) % (AH + 1)] = pnormal_issue(word(m + AH), s_nt);
