@@ -64,6 +64,9 @@ __device__ __forceinline__ void transpose_quadrants(double* v) {
 #ifndef MCG_FC_NRM_BATCH
 #define MCG_FC_NRM_BATCH 1   // the four normals of a Philox call gather together (one LDS wait)
 #endif
+#ifndef MCG_FC_PIPE
+#define MCG_FC_PIPE 0        // experiment: each normal's table rows gathered one normal ahead
+#endif
 
 // 512-thread workgroups, one per CU: eight waves = two per SIMD, sharing one copy of the tables
 // (the proposed point's 64 KB LDS park, below, leaves no room for two workgroups per CU)
@@ -208,13 +211,35 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
     dbl4 e[F::NIB];
 #pragma unroll
     for (int ib = 0; ib < F::NIB; ++ib) e[ib] = dbl4{0.0, 0.0, 0.0, 0.0};
+#if MCG_FC_PIPE
+    // the table gathers one normal ahead, across the Philox calls (the next call's words are
+    // drawn before its first normal's gathers go out)
+    u32x4 wcur = rng(gid, tlo, (uint32_t)q, TAG_MH, thi), wnext = wcur;
+    NrmPending pend = pnormal_issue(wcur.x, s_nt);
+#endif
 #pragma unroll
     for (int m = 0; m < F::NM; ++m) {
       // U fragments and mu are loop-invariant LDS reads: without a barrier the compiler hoists
       // all of them out of the step loop into ~110 registers
       asm volatile("" ::: "memory");
-      const u32x4 w = rng(gid, tlo, (uint32_t)(4 * m + q), TAG_MH, thi);
       double v[4];
+#if MCG_FC_PIPE
+      if (m + 1 < F::NM) wnext = rng(gid, tlo, (uint32_t)(4 * (m + 1) + q), TAG_MH, thi);
+      {
+        const uint32_t ww[4] = {wcur.x, wcur.y, wcur.z, wcur.w};
+        const uint32_t wn0 = wnext.x;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          NrmPending nx;
+          const bool more = k < 3 || m + 1 < F::NM;
+          if (more) nx = pnormal_issue(k < 3 ? ww[k + 1] : wn0, s_nt);
+          v[k] = pnormal_finish(pend);
+          if (more) pend = nx;
+        }
+      }
+      wcur = wnext;
+#else
+      const u32x4 w = rng(gid, tlo, (uint32_t)(4 * m + q), TAG_MH, thi);
 #if MCG_FC_NRM_BATCH
       pnormal4_lds(w, s_nt, v);
 #else
@@ -222,6 +247,7 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
       v[1] = pnormal(w.y, s_nt);
       v[2] = pnormal(w.z, s_nt);
       v[3] = pnormal(w.w, s_nt);
+#endif
 #endif
       transpose_quadrants(v);                 // v[k'] = z[16 m + 4 k' + q]
 #pragma unroll
