@@ -45,19 +45,27 @@ __device__ __forceinline__ u32x4 philox(uint32_t c0, uint32_t c1, uint32_t c2, u
 // calls: same chain, step and tag), advanced round by round together: N independent chains of
 // (v_mad_u64_u32 -> v_bitop3) instead of one serial 10-round chain after another, so one wave
 // keeps its SIMD issuing; the shared first-round product of c0 is computed once.
-template <int N>
+// kUniform: c1 and c3 are the same in every lane (the MH step's step counter and tag); their
+// first-round xor with the key then runs on the scalar unit, and each lane does one v_xor with
+// an SGPR operand (v_bitop3 takes one scalar operand, so xor3(v, s, s) costs a v_mov as well)
+template <int N, bool kUniform = false>
 __device__ __forceinline__ void philox_multi(u32x4* out, uint32_t c0, uint32_t c1, const uint32_t* c2,
                                              uint32_t c3, uint32_t k0, uint32_t k1) {
   asm volatile("" : "+s"(k0), "+s"(k1));
   uint32_t a[N], b[N], c[N], d[N];
   {
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    uint32_t c1k = 0, c3k = 0;
+    if constexpr (kUniform) {
+      c1k = (uint32_t)__builtin_amdgcn_readfirstlane((int)(c1 ^ k0));
+      c3k = (uint32_t)__builtin_amdgcn_readfirstlane((int)(c3 ^ k1));
+    }
 #pragma unroll
     for (int n = 0; n < N; ++n) {
       const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2[n];
-      a[n] = xor3((uint32_t)(p1 >> 32), c1, k0);
+      a[n] = kUniform ? ((uint32_t)(p1 >> 32) ^ c1k) : xor3((uint32_t)(p1 >> 32), c1, k0);
       b[n] = (uint32_t)p1;
-      c[n] = xor3((uint32_t)(p0 >> 32), c3, k1);
+      c[n] = kUniform ? ((uint32_t)(p0 >> 32) ^ c3k) : xor3((uint32_t)(p0 >> 32), c3, k1);
       d[n] = (uint32_t)p0;
     }
   }

@@ -589,7 +589,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
         uint32_t cidx[L::NCL];
 #pragma unroll
         for (int i = 0; i < L::NCL; ++i) cidx[i] = (uint32_t)(sub + P * i);
-        philox_multi<L::NCL>(wl, gid, tlo, cidx, (TAG_MH << 16) | (thi & 0xFFFFu), rng.k0, rng.k1);
+        philox_multi<L::NCL, true>(wl, gid, tlo, cidx, (TAG_MH << 16) | (thi & 0xFFFFu), rng.k0, rng.k1);
       }
       // the coordinates and terms of call i from its four normals
       auto dims1 = [&](const int i, const int k, const double zk) {
