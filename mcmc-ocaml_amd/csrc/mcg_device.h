@@ -69,7 +69,9 @@ struct MhArgs {
   int32_t flags;        // RUNF_*
   int32_t is_cauchy;
   int32_t uni;          // isotropic Gaussian proposal and one box for every dim (fused step only)
+  int32_t ubox;         // one box [box_lo, box_hi] for every dim (any proposal; eval_prior)
   double uni_s, uni_lo, uni_hi;
+  double box_lo, box_hi;
   // reversible jump (mcg_rj_kernel.h): model descriptors, tags, recorded tags, B-record counts
   const double* rj;
   uint8_t* tag;                 // [N]

@@ -177,9 +177,11 @@ __device__ __forceinline__ bool mix_has_kd(const double* __restrict__ q, int str
   return kd;
 }
 
-template <int D, int P, int LIK>
-__device__ __forceinline__ double eval_lik(const double* y, int sub, const MhArgs& a,
-                                           const double* __restrict__ q) {
+// Q: a generic pointer, or (the MH kernel's per-step evaluation) a constant-address-space one,
+// whose uniform loads become scalar loads (the scalar cache and lgkmcnt, not vmcnt: a per-step
+// vector load of the constants waited with vmcnt(0) and drained every load issued ahead)
+template <int D, int P, int LIK, typename Q = const double* __restrict__>
+__device__ __forceinline__ double eval_lik(const double* y, int sub, const MhArgs& a, Q q) {
   using L = Layout<D, P>;
   if constexpr (LIK == MCG_LIK_FLAT) {
     return 0.0;
@@ -216,7 +218,7 @@ __device__ __forceinline__ double eval_lik(const double* y, int sub, const MhArg
     double A[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) A[j] = 0.0;
-    const double* __restrict__ U = q + D + 1;
+    const auto U = q + D + 1;
 #pragma unroll
     for (int i = 0; i < D; ++i) {
       double t = 0.0;
@@ -249,21 +251,43 @@ __device__ __forceinline__ double eval_lik(const double* y, int sub, const MhArg
   }
 }
 
-template <int D, int P>
-__device__ __forceinline__ double eval_prior(const double* y, int sub, const MhArgs& a,
-                                             const double* __restrict__ q) {
+template <int D, int P, typename Q = const double* __restrict__>
+__device__ __forceinline__ double eval_prior(const double* y, int sub, const MhArgs& a, Q q) {
   using L = Layout<D, P>;
   if (a.prior_kind == MCG_PRIOR_FLAT) return 0.0;
   int inb = 1;
+  if (a.ubox) {
+    // one box for every dim: the bounds are kernel arguments (SGPRs).  Per-dim loads of the
+    // bounds were compiled into a chain of branches, one global load and a full vmcnt wait each
+    // (the kD kernel of C4 spent most of its step there)
 #pragma unroll
-  for (int i = 0; i < L::NCL; ++i)
+    for (int i = 0; i < L::NCL; ++i)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (!L::valid(sub, i, k)) continue;
-      int d = L::dim(sub, i, k);
-      double v = y[4 * i + k];
-      inb &= (int)(v >= q[d]) & (int)(v <= q[D + d]);   // closed form of the box (see above)
-    }
+      for (int k = 0; k < 4; ++k) {
+        if (!L::valid(sub, i, k)) continue;
+        const double v = y[4 * i + k];
+        inb &= (int)(v >= a.box_lo) & (int)(v <= a.box_hi);
+      }
+  } else {
+    // all bounds loaded before any compare (the same predicate, no per-dim wait)
+    double lo[L::NL], hi[L::NL];
+#pragma unroll
+    for (int i = 0; i < L::NCL; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int d = L::valid(sub, i, k) ? L::dim(sub, i, k) : 0;
+        lo[4 * i + k] = q[d];
+        hi[4 * i + k] = q[D + d];
+      }
+#pragma unroll
+    for (int i = 0; i < L::NCL; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (!L::valid(sub, i, k)) continue;
+        const double v = y[4 * i + k];
+        inb &= (int)(v >= lo[4 * i + k]) & (int)(v <= hi[4 * i + k]);   // closed form of the box (see above)
+      }
+  }
   inb = and_lanes<P>(inb);
   return inb ? q[2 * D] : -__builtin_inf();
 }
@@ -316,6 +340,12 @@ struct AccumCfg {
 // evaluated one at a time (no batched gathers: their 32 in-flight registers would spill);
 // C2 1.87e10 -> 1.96e10 MH steps/s against two waves with batched gathers (A/B on one box).
 // Everything else is left to the compiler's register budget (two waves where it fits).
+#ifndef MCG_SCALAR_CONSTS
+#define MCG_SCALAR_CONSTS 1  // generic step: likelihood / prior constants through scalar loads
+#endif
+#ifndef MCG_KD_PREFETCH
+#define MCG_KD_PREFETCH 1  // kD proposal: leaf two steps ahead, box and log q one step ahead
+#endif
 #ifndef MCG_PHILOX_SEQ
 #define MCG_PHILOX_SEQ 0   // experiment: the pipelined step's Philox calls computed one after another
 #endif
@@ -539,6 +569,30 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
         rc_i[4 * i + k] = LIK == MCG_LIK_DIAG_GAUSS ? a.lik[D + d] : 0.0;
       }
   }
+  // kD independence proposal: a step's draw depends on the RNG only (the picked training point's
+  // leaf, its box, a uniform point in it), so the leaf of step t + 2 and the box and log q of
+  // step t + 1 are loaded while step t computes (a dependent leaf -> box load chain per step
+  // otherwise sits on every step's path).  The same values as loading them in the step.
+  int kd_leaf = 0, kd_leaf_n = 0;
+  double kd_bx[PROP == MCG_PROP_KD_INTERP ? 2 * D : 1];
+  double kd_lqp = 0.0;
+  auto kd_pick_leaf = [&](uint64_t Tp) -> int {
+    const u32x4 w = rng(gid, (uint32_t)Tp, CALL_KD_PICK, TAG_MH, (uint32_t)(Tp >> 32));
+    return a.kd_pt_leaf[randint(w.x, w.y, (uint32_t)a.kd_M)];
+  };
+  auto kd_load_box = [&](int leaf) {
+    const double* __restrict__ bx = a.kd_box + (int64_t)leaf * 2 * D;
+#pragma unroll
+    for (int d = 0; d < (PROP == MCG_PROP_KD_INTERP ? 2 * D : 0); ++d) kd_bx[d] = bx[d];
+    kd_lqp = a.kd_logq[leaf];
+  };
+  if constexpr (PROP == MCG_PROP_KD_INTERP && MCG_KD_PREFETCH) {
+    if (a.nsteps > 0) {
+      kd_leaf = kd_pick_leaf(a.step_base);
+      kd_load_box(kd_leaf);
+      kd_leaf_n = kd_pick_leaf(a.step_base + 1);
+    }
+  }
   for (int64_t t = 0; t < a.nsteps; ++t) {
     const uint64_t T = a.step_base + (uint64_t)t;
     const uint32_t tlo = (uint32_t)T, thi = (uint32_t)(T >> 32);
@@ -749,6 +803,33 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
             y[d + 1] = wrap_uniform(qprop[d + 1], qprop[D + d + 1], qprop[2 * D + d + 1], x[d + 1],
                                     u53(w.z, w.w));
         }
+      } else if constexpr (PROP == MCG_PROP_KD_INTERP && MCG_KD_PREFETCH) {
+        static_assert(P == 1, "KD: one lane per chain");
+        // Interpolate_pdf.draw (interpolate_pdf.ml:114-119) from the leaf and box loaded ahead
+        const int leaf = kd_leaf;
+        bool strict = true;
+#pragma unroll
+        for (int d = 0; d < D; d += 2) {
+          const u32x4 v = rng(gid, tlo, (uint32_t)(d >> 1), TAG_MH, thi);
+          y[d] = kd_bx[d] + (kd_bx[D + d] - kd_bx[d]) * u53(v.x, v.y);
+          strict = strict && (y[d] > kd_bx[d]) && (y[d] < kd_bx[D + d]);
+          if (d + 1 < D) {
+            y[d + 1] = kd_bx[d + 1] + (kd_bx[D + d + 1] - kd_bx[d + 1]) * u53(v.z, v.w);
+            strict = strict && (y[d + 1] > kd_bx[d + 1]) && (y[d + 1] < kd_bx[D + d + 1]);
+          }
+        }
+        // strictly inside its leaf box: that leaf (see below), whose log q came with the box
+        lqy = kd_lqp;
+        if (!strict) lqy = a.kd_logq[kd_find_leaf<D>(a.kd_nodes, a.kd_root, y)];
+        (void)leaf;
+        // the next step's box and log q go out now (its leaf arrived during this step), and
+        // the leaf of the step after it: their latency hides behind this step's likelihood,
+        // accept and records and the next step's uniforms
+        kd_leaf = kd_leaf_n;
+        kd_load_box(kd_leaf);
+        kd_leaf_n = kd_pick_leaf(T + 2);
+        lf = lqy;   // log_jump_prob start proposed = log q(proposed)
+        lb = lq;    // log_jump_prob proposed start = log q(start)
       } else if constexpr (PROP == MCG_PROP_KD_INTERP) {
         static_assert(P == 1, "KD: one lane per chain");
         // Interpolate_pdf.draw (interpolate_pdf.ml:114-119)
@@ -841,8 +922,17 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
         lf = mix_log_jp<D>(qprop, x, y, lqy, s_lt);   // log_jump_prob start proposed
         lb = mix_log_jp<D>(qprop, y, x, lq, s_lt);    // log_jump_prob proposed start
       }
-      lly = eval_lik<D, P, LIK>(y, sub, a, qlik);
-      lpy = eval_prior<D, P>(y, sub, a, qpri);
+      if constexpr (MCG_SCALAR_CONSTS) {
+        typedef const __attribute__((address_space(4))) double kconst;
+        kconst* klik = (kconst*)a.lik;
+        kconst* kpri = (kconst*)a.pri;
+        asm volatile("" : "+s"(klik), "+s"(kpri));
+        lly = eval_lik<D, P, LIK>(y, sub, a, klik);
+        lpy = eval_prior<D, P>(y, sub, a, kpri);
+      } else {
+        lly = eval_lik<D, P, LIK>(y, sub, a, qlik);
+        lpy = eval_prior<D, P>(y, sub, a, qpri);
+      }
     }
     // ---- Hastings ratio and accept test (mcmc.ml:42-56) ----
     const double post_y = lly + lpy;

@@ -538,6 +538,18 @@ MhArgs base_args(mcg_ctx* ctx) {
   const int D = ctx->D;
   const auto& sp = ctx->prop_host;
   const auto& bx = ctx->pri_host;
+  // one box for every dim (bitwise), any proposal: eval_prior compares against kernel arguments
+  // instead of loading 2D bounds per step
+  if (ctx->prior_kind != MCG_PRIOR_FLAT && D >= 1 && (int)bx.size() >= 2 * D && !ctx->rj_active) {
+    bool same = true;
+    for (int d = 1; d < D && same; ++d)
+      same = !std::memcmp(&bx[d], &bx[0], 8) && !std::memcmp(&bx[D + d], &bx[D], 8);
+    if (same) {
+      a.ubox = 1;
+      a.box_lo = bx[0];
+      a.box_hi = bx[D];
+    }
+  }
   if (ctx->prop_kind == MCG_PROP_GAUSS && D >= 1 && (int)sp.size() >= D && (int)bx.size() >= 2 * D) {
     bool same = true;
     for (int d = 1; d < D && same; ++d)
