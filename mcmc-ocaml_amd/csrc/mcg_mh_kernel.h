@@ -413,7 +413,17 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
       x[4 * i + k] = L::valid(sub, i, k) ? a.x[(int64_t)L::dim(sub, i, k) * N + c] : 0.0;
   double ll = a.ll[c], lp = a.lp[c];
   double lq = 0.0;
-  if constexpr (PROP == MCG_PROP_KD_INTERP) lq = a.kd_logq[kd_find_leaf<D>(a.kd_nodes, a.kd_root, x)];
+  if constexpr (PROP == MCG_PROP_KD_INTERP) {
+    if constexpr (P == 1) {
+      lq = a.kd_logq[kd_find_leaf<D>(a.kd_nodes, a.kd_root, x)];
+    } else {
+      // the descent needs every dim: the chain's whole start point, read once per launch
+      double xf[D];
+#pragma unroll
+      for (int d = 0; d < D; ++d) xf[d] = a.x[(int64_t)d * N + c];
+      lq = a.kd_logq[kd_find_leaf<D>(a.kd_nodes, a.kd_root, xf)];
+    }
+  }
   bool mix_kd = false;
   if constexpr (PROP == MCG_PROP_MIXTURE) {
     mix_kd = mix_has_kd(a.prop, MixLayout<D>::kStride);
@@ -573,8 +583,10 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
   // leaf, its box, a uniform point in it), so the leaf of step t + 2 and the box and log q of
   // step t + 1 are loaded while step t computes (a dependent leaf -> box load chain per step
   // otherwise sits on every step's path).  The same values as loading them in the step.
+  // (P > 1: lane `sub` holds the box bounds of its own dims, local slot j at kd_lo[j], kd_hi[j])
+  constexpr int KDN = PROP == MCG_PROP_KD_INTERP ? L::NL : 1;
   int kd_leaf = 0, kd_leaf_n = 0;
-  double kd_bx[PROP == MCG_PROP_KD_INTERP ? 2 * D : 1];
+  double kd_lo[KDN], kd_hi[KDN];
   double kd_lqp = 0.0;
   auto kd_pick_leaf = [&](uint64_t Tp) -> int {
     const u32x4 w = rng(gid, (uint32_t)Tp, CALL_KD_PICK, TAG_MH, (uint32_t)(Tp >> 32));
@@ -583,9 +595,28 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
   auto kd_load_box = [&](int leaf) {
     const double* __restrict__ bx = a.kd_box + (int64_t)leaf * 2 * D;
 #pragma unroll
-    for (int d = 0; d < (PROP == MCG_PROP_KD_INTERP ? 2 * D : 0); ++d) kd_bx[d] = bx[d];
+    for (int i = 0; i < (PROP == MCG_PROP_KD_INTERP ? L::NCL : 0); ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int d = L::valid(sub, i, k) ? L::dim(sub, i, k) : 0;
+        kd_lo[4 * i + k] = bx[d];
+        kd_hi[4 * i + k] = bx[D + d];
+      }
     kd_lqp = a.kd_logq[leaf];
   };
+  // P > 1: the generic step's likelihood / prior constants staged in LDS (lane-dependent dims:
+  // scalar loads do not apply, and vector loads would be waited with vmcnt(0) every step)
+  constexpr bool kKdLds = PROP == MCG_PROP_KD_INTERP && P > 1;
+  constexpr int kKdLik = kKdLds ? 2 * D + 3 : 1, kKdPri = kKdLds ? 2 * D + 1 : 1;
+  __shared__ double s_kl[kKdLik], s_kp[kKdPri];
+  if constexpr (kKdLds) {
+    const int nl = LIK == MCG_LIK_DIAG_GAUSS ? 2 * D + 1 : LIK == MCG_LIK_GAUSS_SHELL ? D + 3 : 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < nl; i += blockDim.x) s_kl[i] = a.lik[i];
+    if (a.prior_kind != MCG_PRIOR_FLAT)
+      for (int i = threadIdx.x; i < 2 * D + 1; i += blockDim.x) s_kp[i] = a.pri[i];
+    __syncthreads();
+  }
   if constexpr (PROP == MCG_PROP_KD_INTERP && MCG_KD_PREFETCH) {
     if (a.nsteps > 0) {
       kd_leaf = kd_pick_leaf(a.step_base);
@@ -804,24 +835,43 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
                                     u53(w.z, w.w));
         }
       } else if constexpr (PROP == MCG_PROP_KD_INTERP && MCG_KD_PREFETCH) {
-        static_assert(P == 1, "KD: one lane per chain");
-        // Interpolate_pdf.draw (interpolate_pdf.ml:114-119) from the leaf and box loaded ahead
-        const int leaf = kd_leaf;
+        static_assert(P == 1 || D % (4 * P) == 0, "KD: P lanes need D % 4P == 0");
+        // Interpolate_pdf.draw (interpolate_pdf.ml:114-119) from the leaf and box loaded ahead;
+        // dims 2c and 2c + 1 from call c (lane `sub`: the calls of its 4-dim blocks)
         bool strict = true;
 #pragma unroll
-        for (int d = 0; d < D; d += 2) {
-          const u32x4 v = rng(gid, tlo, (uint32_t)(d >> 1), TAG_MH, thi);
-          y[d] = kd_bx[d] + (kd_bx[D + d] - kd_bx[d]) * u53(v.x, v.y);
-          strict = strict && (y[d] > kd_bx[d]) && (y[d] < kd_bx[D + d]);
-          if (d + 1 < D) {
-            y[d + 1] = kd_bx[d + 1] + (kd_bx[D + d + 1] - kd_bx[d + 1]) * u53(v.z, v.w);
-            strict = strict && (y[d + 1] > kd_bx[d + 1]) && (y[d + 1] < kd_bx[D + d + 1]);
+        for (int i = 0; i < L::NCL; ++i)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int j = 4 * i + 2 * h;
+            if (!L::valid(sub, i, 2 * h)) continue;
+            const u32x4 v = rng(gid, tlo, (uint32_t)(L::dim(sub, i, 2 * h) >> 1), TAG_MH, thi);
+            y[j] = kd_lo[j] + (kd_hi[j] - kd_lo[j]) * u53(v.x, v.y);
+            strict = strict && (y[j] > kd_lo[j]) && (y[j] < kd_hi[j]);
+            if (L::valid(sub, i, 2 * h + 1)) {
+              y[j + 1] = kd_lo[j + 1] + (kd_hi[j + 1] - kd_lo[j + 1]) * u53(v.z, v.w);
+              strict = strict && (y[j + 1] > kd_lo[j + 1]) && (y[j + 1] < kd_hi[j + 1]);
+            }
           }
-        }
+        if constexpr (P > 1) strict = and_lanes<P>(strict ? 1 : 0) != 0;
         // strictly inside its leaf box: that leaf (see below), whose log q came with the box
         lqy = kd_lqp;
-        if (!strict) lqy = a.kd_logq[kd_find_leaf<D>(a.kd_nodes, a.kd_root, y)];
-        (void)leaf;
+        if (!strict) {
+          if constexpr (P == 1) {
+            lqy = a.kd_logq[kd_find_leaf<D>(a.kd_nodes, a.kd_root, y)];
+          } else {
+            // (rare: a draw rounded onto a face) the descent needs every dim of the proposal
+            double yf[D];
+#pragma unroll
+            for (int o = 0; o < P; ++o)
+#pragma unroll
+              for (int i = 0; i < L::NCL; ++i)
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                  if (L::valid(o, i, k)) yf[L::dim(o, i, k)] = __shfl(y[4 * i + k], (lane & ~(P - 1)) | o, 64);
+            lqy = a.kd_logq[kd_find_leaf<D>(a.kd_nodes, a.kd_root, yf)];
+          }
+        }
         // the next step's box and log q go out now (its leaf arrived during this step), and
         // the leaf of the step after it: their latency hides behind this step's likelihood,
         // accept and records and the next step's uniforms
@@ -922,7 +972,11 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
         lf = mix_log_jp<D>(qprop, x, y, lqy, s_lt);   // log_jump_prob start proposed
         lb = mix_log_jp<D>(qprop, y, x, lq, s_lt);    // log_jump_prob proposed start
       }
-      if constexpr (MCG_SCALAR_CONSTS) {
+      if constexpr (kKdLds) {
+        typedef const __attribute__((address_space(3))) double lconst;
+        lly = eval_lik<D, P, LIK>(y, sub, a, (lconst*)s_kl);
+        lpy = eval_prior<D, P>(y, sub, a, (lconst*)s_kp);
+      } else if constexpr (MCG_SCALAR_CONSTS) {
         typedef const __attribute__((address_space(4))) double kconst;
         kconst* klik = (kconst*)a.lik;
         kconst* kpri = (kconst*)a.pri;

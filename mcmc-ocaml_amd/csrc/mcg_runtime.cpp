@@ -577,13 +577,17 @@ int choose_lanes(mcg_ctx* ctx) {
   // full covariance, Gaussian proposal, D in {16,32,48,64}: the matrix-core kernel (4 lanes/chain)
   const bool fullcov_mfma = ctx->lik_kind == MCG_LIK_FULLCOV_GAUSS && ctx->prop_kind == MCG_PROP_GAUSS &&
                             find_mh_kernel(D, 4, ctx->lik_kind, ctx->prop_kind) != nullptr;
+  // the kD independence proposal with a separable likelihood: its draw splits over lanes too
+  const bool kd_split = ctx->prop_kind == MCG_PROP_KD_INTERP &&
+                        (ctx->lik_kind == MCG_LIK_DIAG_GAUSS || ctx->lik_kind == MCG_LIK_GAUSS_SHELL ||
+                         ctx->lik_kind == MCG_LIK_FLAT);
   if (want > 0) {
     if (want == 1) return 1;
-    if ((separable || fullcov_mfma) && D % (4 * want) == 0 && find_mh_kernel(D, want, ctx->lik_kind, ctx->prop_kind)) return want;
+    if ((separable || fullcov_mfma || kd_split) && D % (4 * want) == 0 && find_mh_kernel(D, want, ctx->lik_kind, ctx->prop_kind)) return want;
     return 1;
   }
   if (fullcov_mfma) return 4;
-  if (!separable) return 1;
+  if (!separable && !kd_split) return 1;
   const int64_t lanes_target = (int64_t)std::max(ctx->num_cus, 1) * 4 * 4 * 64;  // 4 waves/SIMD
   int best = 1;
   for (int P : {2, 4}) {

@@ -161,7 +161,10 @@ def c4(args):
                                 "max_rel_sd_err": float(np.max(np.abs(sd - 1)))},
             "log_z_harmonic_mean": lz, "log_z_analytic": -D * math.log(20.0),
             "roofline": roofline("mcg::mh_kernel<8,P,DIAG_GAUSS,KD_INTERP>", N * S, bps,
-                                 ctx.kernel_timing("mh"))}
+                                 ctx.kernel_timing("mh")),
+            "roofline_note": "SURVEY 8(d) bytes (state + box + two descents); the 4 MB tree and the "
+                             "boxes are cache-resident and strict-interior draws skip the descents, "
+                             "so frac > 1 is possible: the step is instruction-issue bound (DESIGN 5.4)"}
     ctx.close()
     return line
 

@@ -198,6 +198,26 @@ def test_kd_interp_proposal_bit_exact(oracle, T):
     assert_same(g, o)
 
 
+@pytest.mark.parametrize("D,lanes,uniform_box", [(8, 1, True), (8, 2, True), (8, 2, False),
+                                                  (16, 2, False), (16, 4, True)])
+def test_kd_interp_lane_splits_bit_exact(oracle, T, D, lanes, uniform_box):
+    """The kD draw split over 1, 2 or 4 lanes per chain (each lane its dims' box bounds and
+    uniforms, the likelihood / prior constants staged in LDS), with the box prior as kernel
+    arguments or as per-dim bounds: the oracle's chains bit for bit."""
+    rng = np.random.default_rng(11 + D)
+    mu = np.linspace(-0.2, 0.2, D); sg = np.linspace(0.8, 1.2, D)
+    pts = rng.normal(size=(512, D))
+    lo = -5 * np.ones(D) if uniform_box else np.linspace(-5.5, -4.5, D)
+    hi = 5 * np.ones(D) if uniform_box else np.linspace(4.5, 5.5, D)
+    kdp = T.KdInterp(pts, lo, hi)
+    okd = oracle.KdTree(pts, lo, hi)
+    lik, pri = T.diag_gauss(mu, sg), T.box(lo, hi)
+    x0 = rng.normal(size=(D, 160))
+    g = run_gpu(lik, pri, kdp, x0, 9, nbin=3, nskip=2, n_rec=40, lanes=lanes)
+    o = run_oracle(oracle, lik, pri, T.gauss(1.0), x0, 9, 3, 2, 40, kd=okd)
+    assert_same(g, o)
+
+
 def test_kd_tree_export_matches_oracle(oracle, T):
     import ctypes as C
     import mcmc_amd._lib as L
