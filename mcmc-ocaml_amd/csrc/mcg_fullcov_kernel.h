@@ -54,6 +54,36 @@ __device__ __forceinline__ void swap16(double& a, double& b) {
   a = __hiloint2double((int)hi[0], (int)lo[0]);
   b = __hiloint2double((int)hi[1], (int)lo[1]);
 }
+// v + v[lane ^ 32] and v + v[lane ^ 16] with the same two swaps (VALU, no ds_bpermute round
+// trip on the step's serial chain): after swap32(a, b) of two copies of v, a + b holds the pair
+// {v[i], v[i ^ 32]} in every lane (in either order: the sum is the same bits); likewise swap16
+#ifndef MCG_FC_SWAP_SUM
+#define MCG_FC_SWAP_SUM 1
+#endif
+__device__ __forceinline__ void swap32(double& a, double& b);
+__device__ __forceinline__ void swap16(double& a, double& b);
+__device__ __forceinline__ double sum_xor32(double v) {
+  if constexpr (!MCG_FC_SWAP_SUM) return v + __shfl_xor(v, 32, 64);
+  double a = v, b = v;
+  swap32(a, b);
+  return a + b;
+}
+__device__ __forceinline__ double sum_xor16(double v) {
+  if constexpr (!MCG_FC_SWAP_SUM) return v + __shfl_xor(v, 16, 64);
+  double a = v, b = v;
+  swap16(a, b);
+  return a + b;
+}
+__device__ __forceinline__ int and_xor32_16(int v) {
+  if constexpr (!MCG_FC_SWAP_SUM) {
+    v &= __shfl_xor(v, 32, 64);
+    return v & __shfl_xor(v, 16, 64);
+  }
+  auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  v = (int)r[0] & (int)r[1];
+  auto t = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  return (int)t[0] & (int)t[1];
+}
 __device__ __forceinline__ void transpose_quadrants(double* v) {
   swap32(v[0], v[2]);
   swap32(v[1], v[3]);
@@ -275,12 +305,10 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
         else A0 = fma(e[ib][ri], e[ib][ri], A0);
       }
     const double b = A0 + A1;
-    const double cs = b + __shfl_xor(b, 32, 64);
-    const double S = cs + __shfl_xor(cs, 16, 64);
+    const double cs = sum_xor32(b);
+    const double S = sum_xor16(cs);
     const double lly = s_mu[D] - 0.5 * S;
-    int inb = ok ? 1 : 0;
-    inb &= __shfl_xor(inb, 32, 64);
-    inb &= __shfl_xor(inb, 16, 64);
+    const int inb = and_xor32_16(ok ? 1 : 0);
     const double lpy = a.prior_kind == MCG_PRIOR_FLAT ? 0.0 : (inb ? s_mu[D + 1] : -__builtin_inf());
     // ---- Hastings ratio and accept test (mcmc.ml:42-56); staggered accept uniforms ----
     const double ratio = (lly + lpy) - (ll + lp);
