@@ -463,6 +463,15 @@ __device__ __forceinline__ double xor_lane_d(double v) {
   }
 }
 
+// broadcast lane K of each lane pair to the pair (DPP quad_perm [K, K, 2 + K, 2 + K])
+template <int K>
+__device__ __forceinline__ double pair_bcast_f64(double v) {
+  constexpr int ctl = K | (K << 2) | ((2 + K) << 4) | ((2 + K) << 6);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), ctl, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), ctl, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
 // broadcast lane K of each lane quad to the quad (DPP quad_perm, no LDS)
 template <int K>
 __device__ __forceinline__ uint32_t quad_bcast_u32(uint32_t v) {

@@ -1008,6 +1008,8 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
       if constexpr (P == 4 && MCG_DPP_XLANE) {    // quad broadcast of lane q (DPP)
         lu = q == 0 ? quad_bcast_f64<0>(lu_own) : q == 1 ? quad_bcast_f64<1>(lu_own)
            : q == 2 ? quad_bcast_f64<2>(lu_own) : quad_bcast_f64<3>(lu_own);
+      } else if constexpr (P == 2 && MCG_DPP_XLANE) {   // pair broadcast of lane q (DPP)
+        lu = q == 0 ? pair_bcast_f64<0>(lu_own) : pair_bcast_f64<1>(lu_own);
       } else {
         lu = __shfl(lu_own, (lane & ~(P - 1)) | q, 64);
       }
