@@ -349,6 +349,9 @@ struct AccumCfg {
 #ifndef MCG_PHILOX_SEQ
 #define MCG_PHILOX_SEQ 0   // experiment: the pipelined step's Philox calls computed one after another
 #endif
+#ifndef MCG_MH_NARROW_FOUR
+#define MCG_MH_NARROW_FOUR 0
+#endif
 #ifndef MCG_MH_THREE
 #define MCG_MH_THREE 1     // the fused Gaussian step with <= 8 dims per lane built for three waves per SIMD
 #endif
@@ -362,9 +365,11 @@ struct MhShape {
   static constexpr bool kPipe = MCG_NRM_PIPE != 0 && separable<LIK, PROP>() && Layout<D, P>::NL <= 8 &&
                                 (kThree || MCG_NRM_PIPE > 1);
   static constexpr bool kFour = kThree && MCG_MH_FOUR;
-  static constexpr int kWaves = kFour ? 4 : kThree ? 3 : MCG_MH_MIN_WAVES;
+  // experiment: four waves per SIMD for the fused step with <= 4 dims per lane (D 32 on 8 lanes)
+  static constexpr bool kFourNarrow = kThree && MCG_MH_NARROW_FOUR && Layout<D, P>::NL <= 4;
+  static constexpr int kWaves = (kFour || kFourNarrow) ? 4 : kThree ? 3 : MCG_MH_MIN_WAVES;
   // four waves per SIMD need two workgroups per CU within the LDS: 512 threads share the tables
-  static constexpr int kBlock = kFour ? 512 : 256;
+  static constexpr int kBlock = (kFour || kFourNarrow) ? 512 : 256;
   static constexpr bool kBatchNormals = MCG_NRM_BATCH != 0 && !kThree;
 };
 
