@@ -237,6 +237,7 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   if (n < 2 || k >= n || n > 0x7FFFFFFF) return set_error(ctx, MCG_EINVAL, "need 2 <= nlive, 1 <= k < nlive");
   // the generation's estimate tree holds 16 retirements per thread of one 1024-thread workgroup
   if (k > 16384) return set_error(ctx, MCG_EINVAL, "k (points retired per generation) must be <= 16384");
+  if (nmcmc > 0x7FFFFFF0) return set_error(ctx, MCG_EINVAL, "nmcmc must be < 2^31");   // walker step counters
   const int64_t max_dead = opts->max_dead > 0 ? opts->max_dead : 1000 * n;
   nest_walk_fn walk = find_nest_walk(D, ctx->lik_kind);
   nest_init_fn init = find_nest_init(D, ctx->lik_kind);

@@ -577,7 +577,11 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   }
   // whole groups of PD steps with no data-dependent branches around the loads, so the compiler
   // can count the in-flight loads (vmcnt) across iterations; steps past nmcmc only compute
-  for (int64_t s0 = 0; s0 < a.nmcmc; s0 += PD) {
+  // 32-bit step counters: gfx950 has no 64-bit scalar less-than, so int64 step tests became a
+  // v_mov + v_cmp_lt_i64 pair on the walker's issue-bound wave every step (nmcmc < 2^31: the
+  // host caps it)
+  const int nm = (int)a.nmcmc;
+  for (int s0 = 0; s0 < nm; s0 += PD) {
     double dsc_g[PD], lu_g[PD];
     uint32_t ip_g[PD], jp_g[PD];
     if constexpr (TAB) {
@@ -649,7 +653,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
     // the serial constrained steps
 #pragma unroll
     for (int u = 0; u < PD; ++u) {
-      const bool live = s0 + u < a.nmcmc;
+      const bool live = s0 + u < nm;
 #pragma unroll
       for (int d = 0; d < NL; ++d) y[d] = cur[d] + dsc_g[u] * (bj[u][d] - bi[u][d]);
       refill(bi[u], ip_g[u]);                          // refill slot u with step s + PD's rows
