@@ -343,6 +343,9 @@ struct AccumCfg {
 #ifndef MCG_SCALAR_CONSTS
 #define MCG_SCALAR_CONSTS 1  // generic step: likelihood / prior constants through scalar loads
 #endif
+#ifndef MCG_KD_UAHEAD
+#define MCG_KD_UAHEAD 0    // experiment: the kD box-draw uniforms one step ahead (no change on C4)
+#endif
 #ifndef MCG_KD_PREFETCH
 #define MCG_KD_PREFETCH 1  // kD proposal: leaf two steps ahead, box and log q one step ahead
 #endif
@@ -622,8 +625,24 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
       for (int i = threadIdx.x; i < 2 * D + 1; i += blockDim.x) s_kp[i] = a.pri[i];
     __syncthreads();
   }
+  // the uniforms of a step's box draw (dims 2c and 2c + 1 from call c; the lane's own blocks),
+  // drawn one step ahead
+  double kd_u[KDN];
+  auto kd_uniforms = [&](uint64_t Tu) {
+#pragma unroll
+    for (int i = 0; i < (PROP == MCG_PROP_KD_INTERP ? L::NCL : 0); ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int j = 4 * i + 2 * h;
+        if (!L::valid(sub, i, 2 * h)) continue;
+        const u32x4 v = rng(gid, (uint32_t)Tu, (uint32_t)(L::dim(sub, i, 2 * h) >> 1), TAG_MH, (uint32_t)(Tu >> 32));
+        kd_u[j] = u53(v.x, v.y);
+        if (L::valid(sub, i, 2 * h + 1)) kd_u[j + 1] = u53(v.z, v.w);
+      }
+  };
   if constexpr (PROP == MCG_PROP_KD_INTERP && MCG_KD_PREFETCH) {
     if (a.nsteps > 0) {
+      if constexpr (MCG_KD_UAHEAD) kd_uniforms(a.step_base);
       kd_leaf = kd_pick_leaf(a.step_base);
       kd_load_box(kd_leaf);
       kd_leaf_n = kd_pick_leaf(a.step_base + 1);
@@ -843,21 +862,15 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
         static_assert(P == 1 || D % (4 * P) == 0, "KD: P lanes need D % 4P == 0");
         // Interpolate_pdf.draw (interpolate_pdf.ml:114-119) from the leaf and box loaded ahead;
         // dims 2c and 2c + 1 from call c (lane `sub`: the calls of its 4-dim blocks)
+        if constexpr (!MCG_KD_UAHEAD) kd_uniforms(T);
         bool strict = true;
 #pragma unroll
-        for (int i = 0; i < L::NCL; ++i)
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int j = 4 * i + 2 * h;
-            if (!L::valid(sub, i, 2 * h)) continue;
-            const u32x4 v = rng(gid, tlo, (uint32_t)(L::dim(sub, i, 2 * h) >> 1), TAG_MH, thi);
-            y[j] = kd_lo[j] + (kd_hi[j] - kd_lo[j]) * u53(v.x, v.y);
-            strict = strict && (y[j] > kd_lo[j]) && (y[j] < kd_hi[j]);
-            if (L::valid(sub, i, 2 * h + 1)) {
-              y[j + 1] = kd_lo[j + 1] + (kd_hi[j + 1] - kd_lo[j + 1]) * u53(v.z, v.w);
-              strict = strict && (y[j + 1] > kd_lo[j + 1]) && (y[j + 1] < kd_hi[j + 1]);
-            }
-          }
+        for (int j = 0; j < L::NL; ++j) {
+          if (!L::valid(sub, j >> 2, j & 3)) continue;
+          y[j] = kd_lo[j] + (kd_hi[j] - kd_lo[j]) * kd_u[j];
+          strict = strict && (y[j] > kd_lo[j]) && (y[j] < kd_hi[j]);
+        }
+        if constexpr (MCG_KD_UAHEAD) kd_uniforms(T + 1);   // the next step's uniforms, off this step's chain
         if constexpr (P > 1) strict = and_lanes<P>(strict ? 1 : 0) != 0;
         // strictly inside its leaf box: that leaf (see below), whose log q came with the box
         lqy = kd_lqp;
