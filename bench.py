@@ -200,7 +200,7 @@ def main():
             for i in range(args.nested_seeds):
                 with Context(seed=100 + rank * args.nested_seeds + i, device=local) as c:
                     o = _nested.nested_evidence(lik, pri, nlive=args.nested_nlive, nmcmc=args.nested_nmcmc,
-                                                k=args.nested_k, mode_hopping_frac=0.1, ctx=c)
+                                                k=args.nested_k, mode_hopping_frac=0.1, ctx=c, points=False)
                 h = float(np.sum(np.exp(o[3]) * o.ll) - o[0])
                 deltas.append(o[0] - analytic_log_z(mu, sg))
                 sig1.append(math.sqrt(max(h, 0.0) / args.nested_nlive))

@@ -9,13 +9,16 @@ from .context import Context
 
 
 def nested_evidence(log_likelihood, log_prior, epsrel=0.01, nmcmc=1000, nlive=1000,
-                    mode_hopping_frac=0.1, k=1, observer=None, ctx=None, seed=0, max_dead=0):
+                    mode_hopping_frac=0.1, k=1, observer=None, ctx=None, seed=0, max_dead=0,
+                    points=True):
     """Nested.nested_evidence (nested.ml:122-146).
 
     log_prior must be a box prior (draw_prior = uniform in the box).  Returns the
     nested_output tuple (nested.ml:20): (log_ev, log_dev, points (n, D), log_wts (n,)) where the
     points are dead points in retirement order followed by the final live points ascending in
-    log-likelihood; `ll`, `lp` of every point are in the returned .ll / .lp attributes."""
+    log-likelihood; `ll`, `lp` of every point are in the returned .ll / .lp attributes.
+    points=False leaves the points on the device (no D2H copy of n x D doubles; points is None):
+    log Z, log dZ, the weights and ll / lp are computed all the same."""
     ctx = ctx or Context(seed=seed)
     ctx.set_model(log_likelihood, log_prior, None)
     o = L.McgNestedOpts(nlive, nmcmc, k, epsrel, mode_hopping_frac, max_dead)
@@ -33,9 +36,10 @@ def nested_evidence(log_likelihood, log_prior, epsrel=0.01, nmcmc=1000, nlive=10
     cb = L.OBSERVER(_obs) if observer is not None else L.OBSERVER()
     L.check(L.lib().mcg_nested(ctx.ptr, C.byref(o), C.byref(r), cb, None), ctx.ptr)
     n = r.n_total
-    pts = np.zeros((n, D)); ll = np.zeros(n); lp = np.zeros(n); w = np.zeros(n)
-    L.check(L.lib().mcg_nested_get(ctx.ptr, L.dptr(pts), L.dptr(ll), L.dptr(lp), L.dptr(w)),
-            ctx.ptr)
+    pts = np.zeros((n, D)) if points else None
+    ll = np.zeros(n); lp = np.zeros(n); w = np.zeros(n)
+    L.check(L.lib().mcg_nested_get(ctx.ptr, L.dptr(pts) if points else None, L.dptr(ll), L.dptr(lp),
+                                   L.dptr(w)), ctx.ptr)
     if not r.converged:
         warnings.warn("nested_evidence: max_dead (%d dead points) reached before the stop test "
                       "(nested.ml:45-48) fired; log Z comes from an unconverged run" % r.n_dead,

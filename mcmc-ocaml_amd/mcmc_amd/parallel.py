@@ -107,7 +107,8 @@ def nested_evidence_replicas(log_likelihood, log_prior, epsrel=0.01, nmcmc=1000,
     nl, kk = replica_sizes(nlive, k, world)
     with Context(seed=replica_seed(seed, rank), device=device) as ctx:
         out = _nested.nested_evidence(log_likelihood, log_prior, epsrel=epsrel, nmcmc=nmcmc,
-                                      nlive=nl, mode_hopping_frac=mode_hopping_frac, k=kk, ctx=ctx)
+                                      nlive=nl, mode_hopping_frac=mode_hopping_frac, k=kk, ctx=ctx,
+                                      points=points)
     if os.environ.get("MCG_DEBUG_REPLICAS"):
         print("replica rank %d: log Z %.6f n_dead %d n_gen %d" % (rank, out[0], out.n_dead, out.n_gen),
               file=sys.stderr, flush=True)

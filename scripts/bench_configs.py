@@ -102,15 +102,25 @@ def c3(args):
     ctx = Context(seed=args.seed)
     # args.reps timed runs in one context (the same seed: identical runs; the first also pays the
     # buffer allocations), then one run with per-walk HIP events for the roofline
-    walls = []
+    # value: the run with its inputs and outputs in HBM (log Z, log dZ, weights and ll / lp come
+    # back; the n x D dead points stay on the device); the full call that also copies the points
+    # to the host (457 MB over PCIe at C3) is reported beside it
+    walls, walls_pts = [], []
     out = None
     for _ in range(max(1, args.reps)):
         out = None              # the previous run's arrays are freed outside the timed call (~25 ms)
         t0 = time.perf_counter()
         out = nested.nested_evidence(lik, pri, epsrel=0.01, nmcmc=nmcmc, nlive=nlive,
-                                     mode_hopping_frac=0.1, k=k, ctx=ctx)
+                                     mode_hopping_frac=0.1, k=k, ctx=ctx, points=False)
         walls.append(time.perf_counter() - t0)
+    for _ in range(max(1, args.reps)):
+        out = None
+        t0 = time.perf_counter()
+        out = nested.nested_evidence(lik, pri, epsrel=0.01, nmcmc=nmcmc, nlive=nlive,
+                                     mode_hopping_frac=0.1, k=k, ctx=ctx)
+        walls_pts.append(time.perf_counter() - t0)
     dt = float(np.median(walls))
+    dt_pts = float(np.median(walls_pts))
     ctx.set_timing(True)
     nested.nested_evidence(lik, pri, epsrel=0.01, nmcmc=nmcmc, nlive=nlive, mode_hopping_frac=0.1, k=k, ctx=ctx)
     tw = ctx.kernel_timing("nested_walk")
@@ -123,6 +133,8 @@ def c3(args):
     line = {"config": "C3 nested D=16 Gaussian shell, nlive %d, k %d, nmcmc %d" % (nlive, k, nmcmc),
             "unit": "constrained MH steps/s", "dtype": "f64", "value": csteps / dt,
             "wall_s": dt, "wall_s_runs": walls, "n_dead": int(out.n_dead), "n_gen": int(out.n_gen),
+            "with_points_d2h": {"value": csteps / dt_pts, "wall_s": dt_pts, "wall_s_runs": walls_pts,
+                                "note": "the same runs plus the n x D dead points copied to the host"},
             "dead_points_per_s": out.n_dead / dt,
             "log_evidence": {"nested": log_ev, "analytic": truth, "abs_delta": abs(log_ev - truth),
                              "sigma_H": sigma, "within_1sigma": abs(log_ev - truth) <= sigma,

@@ -305,3 +305,19 @@ def test_nested_rejects_bad_generation_sizes(T, nlive, k, what):
             nested.nested_evidence(lik, pri, ctx=ctx, nlive=nlive, nmcmc=2, k=k)
     finally:
         ctx.close()
+
+
+@pytest.mark.gpu
+def test_nested_points_left_on_device_same_result(T):
+    """points=False skips the D2H copy of the dead points: log Z, log dZ, weights, ll and lp are
+    the full call's bit for bit."""
+    D = 8
+    lik = T.gauss_shell(np.zeros(D), 1.0, 0.2)
+    pri = T.box(-2 * np.ones(D), 2 * np.ones(D))
+    a = gpu_nested(lik, pri, 21, nlive=500, nmcmc=20, mode_hopping_frac=0.1, k=25)
+    b = gpu_nested(lik, pri, 21, nlive=500, nmcmc=20, mode_hopping_frac=0.1, k=25, points=False)
+    assert b[2] is None and a[2].shape == (len(a.ll), D)
+    assert a[0] == b[0] and a[1] == b[1]
+    np.testing.assert_array_equal(a[3], b[3])
+    np.testing.assert_array_equal(a.ll, b.ll)
+    np.testing.assert_array_equal(a.lp, b.lp)
