@@ -343,6 +343,9 @@ struct AccumCfg {
 #ifndef MCG_SCALAR_CONSTS
 #define MCG_SCALAR_CONSTS 1  // generic step: likelihood / prior constants through scalar loads
 #endif
+#ifndef MCG_UNI_NO_OPAQUE
+#define MCG_UNI_NO_OPAQUE 1
+#endif
 #ifndef MCG_KD_UAHEAD
 #define MCG_KD_UAHEAD 0    // experiment: the kD box-draw uniforms one step ahead (no change on C4)
 #endif
@@ -660,7 +663,8 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
     gconst* glik = (gconst*)a.lik;
     gconst* gpri = (gconst*)a.pri;
     gconst* gprop = (gconst*)a.prop;
-    asm volatile("" : "+s"(glik), "+s"(gpri), "+s"(gprop));
+    // (the fused step with UNI constants reads none of them: no per-step copies there)
+    if constexpr (!(kSeparable && UNI) || !MCG_UNI_NO_OPAQUE) asm volatile("" : "+s"(glik), "+s"(gpri), "+s"(gprop));
     const double* qlik = (const double*)glik;
     const double* qpri = (const double*)gpri;
     const double* qprop = (const double*)gprop;
@@ -677,7 +681,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
       gdouble* qlik = (gdouble*)a.lik;
       gdouble* qpri = (gdouble*)a.pri;
       gdouble* qprop = (gdouble*)a.prop;
-      asm volatile("" : "+s"(qlik), "+s"(qpri), "+s"(qprop));
+      if constexpr (!UNI || !MCG_UNI_NO_OPAQUE) asm volatile("" : "+s"(qlik), "+s"(qpri), "+s"(qprop));
 #endif
       double A[L::NA];
 #pragma unroll
