@@ -198,9 +198,10 @@ def test_kd_interp_proposal_bit_exact(oracle, T):
     assert_same(g, o)
 
 
-@pytest.mark.parametrize("D,lanes,uniform_box", [(8, 1, True), (8, 2, True), (8, 2, False),
-                                                  (16, 2, False), (16, 4, True)])
-def test_kd_interp_lane_splits_bit_exact(oracle, T, D, lanes, uniform_box):
+@pytest.mark.parametrize("D,lanes,uniform_box,nch", [(8, 1, True, 160), (8, 2, True, 160),
+                                                      (8, 2, False, 100), (16, 2, False, 160),
+                                                      (16, 4, True, 100)])
+def test_kd_interp_lane_splits_bit_exact(oracle, T, D, lanes, uniform_box, nch):
     """The kD draw split over 1, 2 or 4 lanes per chain (each lane its dims' box bounds and
     uniforms, the likelihood / prior constants staged in LDS), with the box prior as kernel
     arguments or as per-dim bounds: the oracle's chains bit for bit."""
@@ -212,7 +213,7 @@ def test_kd_interp_lane_splits_bit_exact(oracle, T, D, lanes, uniform_box):
     kdp = T.KdInterp(pts, lo, hi)
     okd = oracle.KdTree(pts, lo, hi)
     lik, pri = T.diag_gauss(mu, sg), T.box(lo, hi)
-    x0 = rng.normal(size=(D, 160))
+    x0 = rng.normal(size=(D, nch))       # 100 chains: a partial last wave
     g = run_gpu(lik, pri, kdp, x0, 9, nbin=3, nskip=2, n_rec=40, lanes=lanes)
     o = run_oracle(oracle, lik, pri, T.gauss(1.0), x0, 9, 3, 2, 40, kd=okd)
     assert_same(g, o)
