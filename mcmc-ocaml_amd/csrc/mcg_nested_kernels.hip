@@ -264,9 +264,12 @@ __global__ void __launch_bounds__(256) rank_count_kernel(const NestArgs a, int n
     return;
   }
   const uint32_t ncount = gridDim.x - (a.est_in_rank ? 1u : 0u);
-  if (a.fuse_retire) {
-    // the retire kernel's slot writes (the walkers moved the dead rows and emitted the keys):
-    // walker j's point into the slot it replaces, spread over the counting workgroups
+  // the retire kernel's slot writes (the walkers moved the dead rows and emitted the keys):
+  // walker j's point into the slot it replaces, spread over the counting workgroups.  They run
+  // after the counting and the hand-off (nothing in this kernel reads them; the next walk does,
+  // after a kernel boundary), so their loads do not delay the count
+  auto slot_writes = [&]() {
+    if (!a.fuse_retire) return;
     const int64_t kD = a.k * a.row_bytes / 8, D = a.row_bytes / 8;
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < kD; g += (int64_t)ncount * blockDim.x) {
       const int64_t j = g / D;
@@ -278,7 +281,7 @@ __global__ void __launch_bounds__(256) rank_count_kernel(const NestArgs a, int n
         a.lp[sj] = a.nlp[j];
       }
     }
-  }
+  };
   __shared__ double sl[kSub];
   __shared__ double s_ll[kSmallSort];                // last block: keys placed at their ranks
   __shared__ short s_j[kSmallSort];
@@ -311,7 +314,10 @@ __global__ void __launch_bounds__(256) rank_count_kernel(const NestArgs a, int n
   }
   const bool last = last_block_done(a.sync + kSyncUse, ncount);
   NT_STAMP(2, 3);
-  if (!last) return;
+  if (!last) {
+    slot_writes();
+    return;
+  }
   // the last block places every key at its rank in LDS (a random scatter from one CU is bound by
   // its store rate), then writes the sorted keys out coalesced
   constexpr int kPer = kSmallSort / kRun;
@@ -350,6 +356,7 @@ __global__ void __launch_bounds__(256) rank_count_kernel(const NestArgs a, int n
     }
   }
   NT_STAMP(2, 5);
+  slot_writes();
 }
 
 hipError_t launch_sort_new_small(const NestArgs& a, double* oll, long long* otie, int* oslot,
