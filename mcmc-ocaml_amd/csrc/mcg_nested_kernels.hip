@@ -374,8 +374,8 @@ struct KeySample {
   int64_t S;
   int n;
 };
-__device__ __forceinline__ KeySample key_sample(int64_t len, int cap) {
-  int64_t S = 16;
+__device__ __forceinline__ KeySample key_sample(int64_t len, int cap, int64_t smin = 16) {
+  int64_t S = smin;
   while (len / S > cap) S <<= 1;
   return KeySample{S, (int)(len / S)};
 }
@@ -396,7 +396,13 @@ __device__ __forceinline__ int64_t count_less_2l(const double* ll, const long lo
   return lo + count_less(ll, tie, lo, hi, kl, kt);
 }
 
-constexpr int kSampNew = 256, kSampSurv = 2048;
+// the new keys' sample: every 4th key (k <= 4096), so a survivor's search ends with two
+// dependent global probes instead of four
+#ifndef MCG_MERGE_NEW_SAMPLE
+#define MCG_MERGE_NEW_SAMPLE 1024
+#endif
+constexpr int kSampNew = MCG_MERGE_NEW_SAMPLE, kSampSurv = 2048;
+constexpr int64_t kSampNewMin = kSampNew >= 1024 ? 4 : 16;
 
 // survivors keys[k..n) + k sorted new keys -> out[0..n) by rank scatter; the thread placing the
 // largest key also counts the generation (the stop test runs at the start of the next walk).  Each binary search starts in an LDS
@@ -414,7 +420,7 @@ __global__ void __launch_bounds__(256) merge_new_kernel(const NestArgs a, double
   const bool has_surv = e0 < ns_, has_new = e0 + blockDim.x > ns_;   // block-uniform
   const double* sll = a.key_ll + k;
   const long long* stie = a.key_tie + k;
-  const KeySample kn = key_sample(k, kSampNew), kv = key_sample(ns_, kSampSurv);
+  const KeySample kn = key_sample(k, kSampNew, kSampNewMin), kv = key_sample(ns_, kSampSurv);
   KeySample kv_use = kv;
   // own key and the samples: all loads issued before the stop flag is read
   const int64_t ec = e < n ? e : n - 1;
@@ -430,10 +436,16 @@ __global__ void __launch_bounds__(256) merge_new_kernel(const NestArgs a, double
     kt = nt[ec - ns_];
     ks = ns[ec - ns_];
   }
-  if (has_surv && threadIdx.x < kn.n) {
-    const int64_t q = (threadIdx.x + 1) * kn.S - 1;
-    s_nl[threadIdx.x] = nl[q];
-    s_nt[threadIdx.x] = nt[q];
+  if (has_surv) {
+#pragma unroll
+    for (int r = 0; r < (kSampNew + 255) / 256; ++r) {
+      const int i = r * 256 + (int)threadIdx.x;
+      if (i < kn.n) {
+        const int64_t q = (int64_t)(i + 1) * kn.S - 1;
+        s_nl[i] = nl[q];
+        s_nt[i] = nt[q];
+      }
+    }
   }
   if (has_new) {
     // survivors' sample: from the compact sample the previous merge kept beside the keys
