@@ -71,7 +71,11 @@ enum { MCG_PRIOR_FLAT = 0, MCG_PRIOR_BOX = 1, MCG_PRIOR_OPEN_BOX = 2 };
    WRAP_UNIFORM : lo[D], hi[D], dx[D] Mcmc.uniform_wrapping per dim (mcmc.ml:187-196), symmetric
    KD_INTERP    : set with mcg_set_kd_proposal; independence proposal Interpolate_pdf.draw with
                   log_jump_prob _ y = log (jump_prob y)  (interpolate_pdf.ml:114-142)
-   DE           : used by nested sampling (mcmc.ml:198-218)
+   DE           : mode_hopping_frac; set with mcg_set_de_proposal (the sample array).
+                  Mcmc.differential_evolution_proposal (mcmc.ml:198-218): y = x + d (s_j - s_i),
+                  i != j uniform over the samples, d = 1.0 with probability mode_hopping_frac
+                  (never drawn when it is 0) else N(0, 2.38/sqrt(2 ndim)); log_jump_prob = 0.
+                  Also the proposal of nested sampling's walkers (nested.ml:53).
    MIXTURE      : Mcmc.combine_jump_proposals [(p_i, jp_i, ljp_i)] (mcmc.ml:165-185):
                   ncomp, then per component: p, comp_kind, ljp_mode, comp params, where
                     MCG_MIX_GAUSS         s[D]        y = x + s z, z ~ N(0, 1)
@@ -122,6 +126,10 @@ int mcg_set_proposal(mcg_ctx* ctx, int32_t kind, const double* params, size_t n)
    with Kd_tree.tree_of_objects semantics (kd_tree.ml:155-175), flattened into HBM. */
 int mcg_set_kd_proposal(mcg_ctx* ctx, const double* pts /*[M][D] row-major*/, int64_t M,
                         const double* low, const double* high);
+/* Mcmc.differential_evolution_proposal ?mode_hopping_frac to_float from_float samples
+   (mcmc.ml:198-218, mcmc.mli:215-218): samples [M][D] row-major (M >= 2: the reference's
+   pick_samples never ends with one sample), kept in HBM; selects MCG_PROP_DE. */
+int mcg_set_de_proposal(mcg_ctx* ctx, const double* samples, int64_t M, double mode_hopping_frac);
 
 /* flattened tree of the last mcg_set_kd_proposal (pre-order; left child = node + 1):
    node_dim (-1 = leaf), node_split, node_right, node_leaf (-1 = internal), leaf_count,
@@ -258,6 +266,13 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
 int mcg_nested_get(mcg_ctx* ctx, double* pts, double* ll, double* lp, double* log_wts);
 /* Nested.log_total_error_estimate (nested.ml:148-150) */
 double mcg_log_total_error_estimate(double log_ev, double log_dev, int64_t nlive);
+/* Nested.posterior_samples n (nested.ml:167-178) as indices: the running sums of exp log_wts
+   (sequential, glibc exp: :170-173) and, per draw, Random.float 1.0 -> weight_binary_search_index
+   (:152-165) on the device.  Draw i of a call takes u53 of Philox counter (i lo, i hi, call, tag 5):
+   `call` counts this context's posterior_samples calls since mcg_ctx_create / mcg_reseed, so
+   repeated calls draw new samples, as the reference's global Random state does.  idx [n] gets
+   the index into the npts points of each draw. */
+int mcg_posterior_samples(mcg_ctx* ctx, const double* log_wts, int64_t npts, int64_t n, int64_t* idx);
 
 /* ---- nested replicas: merge independent runs into one (multi-GPU C3) ----
    Each of nruns independent runs (one per GPU) gives its points in nested_output order (dead in

@@ -50,6 +50,8 @@ struct MhArgs {
   const double* kd_root;   // [2][D]
   const int32_t* kd_pt_leaf;  // [M] leaf of each training point
   int64_t kd_M;
+  const double* de_pts;    // DE proposal samples [M][D] (differential_evolution_proposal)
+  int64_t de_M;
   int64_t N;
   int64_t bits_row_bytes;
   uint64_t step_base;   // global (RNG) step index of this launch's first step
@@ -92,5 +94,7 @@ mh_launch_fn find_mh_kernel(int D, int P, int lik, int prop);
 typedef hipError_t (*eval_launch_fn)(const MhArgs&, hipStream_t);
 eval_launch_fn find_eval_kernel(int D, int lik);
 hipError_t launch_tile_stats(const TileArgs&, hipStream_t);
+hipError_t launch_posterior_draw(const double* sums, int64_t npts, int64_t n, uint32_t k0, uint32_t k1,
+                                 uint32_t call, int64_t* idx, hipStream_t);
 
 }  // namespace mcg

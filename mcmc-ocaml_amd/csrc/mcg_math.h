@@ -91,7 +91,7 @@ __device__ __forceinline__ void philox_multi(u32x4* out, uint32_t c0, uint32_t c
 
 // counter layout (c0, c1, c2, (tag << 16) | hi16), key = seed
 enum : uint32_t {
-  TAG_MH = 1u, TAG_NEST_WALK = 3u, TAG_NEST_PRIOR = 4u,
+  TAG_MH = 1u, TAG_NEST_WALK = 3u, TAG_NEST_PRIOR = 4u, TAG_POSTERIOR = 5u,
   CALL_ACCEPT = 0xFFFF0000u, CALL_DE_IDX = 0xFFFF0001u, CALL_DE_SCALE = 0xFFFF0002u,
   CALL_KD_PICK = 0xFFFF0003u, CALL_START = 0xFFFF0004u, CALL_MIX = 0xFFFF0005u
 };

@@ -109,15 +109,33 @@ __device__ __forceinline__ int kd_find_leaf(const KdNode* __restrict__ nodes,
   return 0;
 }
 
+// Mcmc.uniform_wrapping (mcmc.ml:187-196): the reference's reflection loop, operation for
+// operation, for up to kWrapExact reflections (|dx| up to ~2048 box widths: every practical
+// step).  Two inputs on which the reference's loop never ends get an exit: a point that lands
+// exactly on xmax (the reflection maps xmax to itself: returned as is), and one so far out that
+// reflections stop shrinking it (|nx| >> width, where rounding makes a 2-cycle).  Past
+// kWrapExact reflections the remaining excess is folded in one step by the loop's
+// real-arithmetic limit, a triangle wave of period 2 (xmax - xmin) (fmod is exact).  Shared
+// with the oracle (oracle.c wrap_uniform) bit for bit.
+constexpr int kWrapExact = 1024;
 __device__ __forceinline__ double wrap_uniform(double xmin, double xmax, double dx, double x,
                                                double u) {
-  double nx = x + (u - 0.5) * dx;                        // mcmc.ml:187-196
-  for (int it = 0; it < 64; ++it) {
-    if (nx < xmin) nx = xmin + (xmin - nx);
-    else if (nx >= xmax) nx = xmax - (nx - xmax);
-    else break;
+  double nx = x + (u - 0.5) * dx;
+  for (int it = 0; it < kWrapExact; ++it) {
+    if (nx < xmin) {
+      nx = xmin + (xmin - nx);
+    } else if (nx >= xmax) {
+      const double r = xmax - (nx - xmax);
+      if (r == nx) return nx;
+      nx = r;
+    } else {
+      return nx;
+    }
   }
-  return nx;
+  const double w = xmax - xmin;
+  double m = fmod(nx - xmin, 2.0 * w);
+  if (m < 0.0) m += 2.0 * w;
+  return m < w ? xmin + m : xmax - (m - w);
 }
 
 // ---- Mcmc.combine_jump_proposals (mcmc.ml:165-185), device layout from mcg_runtime.cpp
@@ -377,6 +395,10 @@ struct MhShape {
   // four waves per SIMD need two workgroups per CU within the LDS: 512 threads share the tables
   static constexpr int kBlock = (kFour || kFourNarrow) ? 512 : 256;
   static constexpr bool kBatchNormals = MCG_NRM_BATCH != 0 && !kThree;
+  // harmonic-mean partials in LDS only where that was measured (C2: P = 4, three waves); a P = 1
+  // instance would hold 2 x 8 x 256 doubles (32 KB) of LDS per workgroup for them, halving the
+  // workgroups per CU of the small-D kD / mixture / generic kernels, so those keep them in VGPRs
+  static constexpr bool kHmLds = MCG_HM_LDS != 0 && (P >= 4 || kThree);
 };
 
 // UNI: 0 = constants through pointers; 1 = isotropic proposal scale and one box [lo, hi] for
@@ -449,14 +471,15 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
   constexpr int NH = P >= 8 ? 1 : 8 / P;
   // the partials live in LDS ([2 NH][256], conflict-free): touched once per P records, they
   // would otherwise hold 4 NH VGPRs through the whole step
-  __shared__ double s_hm[MCG_HM_LDS ? 2 * NH * kBlk : 1];
-  double hcm_r[MCG_HM_LDS ? 1 : NH], hcs_r[MCG_HM_LDS ? 1 : NH];
+  constexpr bool kHmLds = MhShape<D, P, LIK, PROP>::kHmLds;
+  __shared__ double s_hm[kHmLds ? 2 * NH * kBlk : 1];
+  double hcm_r[kHmLds ? 1 : NH], hcs_r[kHmLds ? 1 : NH];
   auto hcm = [&](int l) -> double& {
-    if constexpr (MCG_HM_LDS) return s_hm[(2 * l) * kBlk + threadIdx.x];
+    if constexpr (kHmLds) return s_hm[(2 * l) * kBlk + threadIdx.x];
     else return hcm_r[l];
   };
   auto hcs = [&](int l) -> double& {
-    if constexpr (MCG_HM_LDS) return s_hm[(2 * l + 1) * kBlk + threadIdx.x];
+    if constexpr (kHmLds) return s_hm[(2 * l + 1) * kBlk + threadIdx.x];
     else return hcs_r[l];
   };
   double hm_pv = 0.0;
@@ -495,7 +518,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
   auto hm_flush = [&](int64_t R0) {
     const int li = (int)((R0 & 7) / P);
     if (hm_pok) {
-      if constexpr (MCG_HM_LDS) {
+      if constexpr (kHmLds) {
         hm_update(hcm(li), hcs(li), hm_pv);             // li is wave-uniform (record index)
       } else {
 #pragma unroll
@@ -927,6 +950,26 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
         lqy = a.kd_logq[ly];
         lf = lqy;   // log_jump_prob start proposed = log q(proposed)
         lb = lq;    // log_jump_prob proposed start = log q(start)
+      }
+      else if constexpr (PROP == MCG_PROP_DE) {
+        static_assert(P == 1, "DE: one lane per chain");
+        // Mcmc.differential_evolution_proposal (mcmc.ml:198-218) over the caller's samples:
+        // pick_samples i != j (:199-203; j drawn from the n - 1 others, no retry loop), the scale
+        // 1.0 with probability mode_hopping_frac (no draw consulted when it is 0, :209) else
+        // N(0, 2.38 / sqrt(2 D)) (:212-213), z' = z + d (y_j - x_i) (:214-217).  The samples are
+        // rows of D doubles (two row gathers per step, L2-resident); log_jump_prob = 0.
+        const uint32_t nde = (uint32_t)a.de_M;
+        const u32x4 wi = rng(gid, tlo, CALL_DE_IDX, TAG_MH, thi);
+        const uint32_t ii = randint(wi.x, wi.y, nde);
+        const uint32_t jj = randint(wi.z, wi.w, nde - 1u);
+        const uint32_t jd = jj + (jj >= ii ? 1u : 0u);
+        const u32x4 ws = rng(gid, tlo, CALL_DE_SCALE, TAG_MH, thi);
+        const double mh = qprop[0];
+        const double dsc = (mh != 0.0 && u53(ws.x, ws.y) < mh) ? 1.0 : qprop[1] * pnormal(ws.z, s_nt);
+        const double* __restrict__ si = a.de_pts + (int64_t)ii * D;
+        const double* __restrict__ sj = a.de_pts + (int64_t)jd * D;
+#pragma unroll
+        for (int d = 0; d < D; ++d) y[d] = x[d] + dsc * (sj[d] - si[d]);
       }
       else if constexpr (PROP == MCG_PROP_MIXTURE) {
         static_assert(P == 1, "MIXTURE: one lane per chain");

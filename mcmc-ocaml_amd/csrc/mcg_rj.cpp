@@ -110,6 +110,7 @@ int mcg_set_rjmcmc(mcg_ctx* ctx, const mcg_rj_model* a, const mcg_rj_model* b) {
   if (a->ndim < 1 || b->ndim < 1) return set_error(ctx, MCG_EINVAL, "RJ: ndim >= 1");
   if (!find_rj_kernel(DM)) return set_error(ctx, MCG_EINVAL, "RJ: no compiled kernel for max ndim %d", DM);
   (void)hipSetDevice(ctx->opts.device);
+  // fold_counters zeroes the device tallies too: a validation error below leaves consistent counters
   int qrc;
   if ((qrc = quiesce(ctx)) || (qrc = fold_counters(ctx))) return qrc;
   std::vector<double> dev(32, 0.0);
@@ -184,13 +185,13 @@ int mcg_rj_init(mcg_ctx* ctx, int64_t nchains, const uint8_t* model, const doubl
   if ((rc = hip_check(ctx, ctx->d_nacc.ensure(N * 8), "alloc counters"))) return rc;
   if ((rc = hip_check(ctx, ctx->d_tag.ensure(N), "alloc tags"))) return rc;
   if ((rc = hip_check(ctx, ctx->d_rj_nb.ensure(N * 8), "alloc rj counts"))) return rc;
+  if ((rc = hip_check(ctx, hipMemset(ctx->d_nacc.p, 0, N * 8), "zero counters"))) return rc;
   const int DA = (int)ctx->rj_host[0], DB = (int)ctx->rj_host[16];
   DevBuf dxa, dxb;
   if ((rc = hip_check(ctx, dxa.ensure(N * DA * 8), "alloc xa"))) return rc;
   if ((rc = hip_check(ctx, dxb.ensure(N * DB * 8), "alloc xb"))) return rc;
   if ((rc = hip_check(ctx, hipMemcpy(dxa.p, xa, N * DA * 8, hipMemcpyHostToDevice), "copy xa"))) return rc;
   if ((rc = hip_check(ctx, hipMemcpy(dxb.p, xb, N * DB * 8, hipMemcpyHostToDevice), "copy xb"))) return rc;
-  if ((rc = hip_check(ctx, hipMemset(ctx->d_nacc.p, 0, N * 8), "zero counters"))) return rc;
   if ((rc = hip_check(ctx, hipMemset(ctx->d_rj_nb.p, 0, N * 8), "zero rj counts"))) return rc;
   if (model) {
     for (size_t i = 0; i < N; ++i)

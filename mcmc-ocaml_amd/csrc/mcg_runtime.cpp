@@ -42,7 +42,9 @@ int quiesce(mcg_ctx* ctx) {
 }
 
 // Fold the per-chain device accept counters of the current chains into the context totals
-// (acc_base / rej_base) and zero the step tally; the caller then restarts the device counters.
+// (acc_base / rej_base), zero the step tally AND the device counters, so the context stays
+// consistent whatever the caller does next (an entry point that fails after the fold must not
+// leave the device tallies to be counted twice).  The caller has drained the stream.
 int fold_counters(mcg_ctx* ctx) {
   if (ctx->N < 1 || !ctx->d_nacc.p || ctx->nsteps_total == 0) {
     ctx->nsteps_total = 0;
@@ -51,6 +53,7 @@ int fold_counters(mcg_ctx* ctx) {
   std::vector<uint64_t> h((size_t)ctx->N);
   int rc = hip_check(ctx, hipMemcpy(h.data(), ctx->d_nacc.p, h.size() * 8, hipMemcpyDeviceToHost), "copy counters");
   if (rc) return rc;
+  if ((rc = hip_check(ctx, hipMemset(ctx->d_nacc.p, 0, h.size() * 8), "zero counters"))) return rc;
   uint64_t s = 0;
   for (uint64_t v : h) s += v;
   ctx->acc_base += s;
@@ -432,6 +435,13 @@ int mcg_set_proposal(mcg_ctx* ctx, int32_t kind, const double* params, size_t n)
   } else if (kind == MCG_PROP_MIXTURE) {
     int rc = pack_mixture(ctx, params, n, dev);
     if (rc) return rc;
+  } else if (kind == MCG_PROP_DE) {
+    if (ctx->de_M < 2 || ctx->de_D != D)
+      return set_error(ctx, MCG_ESTATE, "DE: call mcg_set_de_proposal (>= 2 samples of ndim) first");
+    if (!params || n != 1 || !(params[0] >= 0.0 && params[0] <= 1.0))
+      return set_error(ctx, MCG_EINVAL, "DE: params = mode_hopping_frac in [0, 1]");
+    // [mode_hopping_frac, sigma = 2.38 / sqrt(2 ndim)] (mcmc.ml:212, glibc sqrt)
+    dev = {params[0], 2.38 / std::sqrt(2.0 * (double)D)};
   } else {
     return set_error(ctx, MCG_EINVAL, "unsupported proposal kind %d for MH", kind);
   }
@@ -455,6 +465,22 @@ int mcg_set_kd_proposal(mcg_ctx* ctx, const double* pts, int64_t M, const double
   return mcg_set_proposal(ctx, MCG_PROP_KD_INTERP, &z, 1);
 }
 
+int mcg_set_de_proposal(mcg_ctx* ctx, const double* samples, int64_t M, double mode_hopping_frac) {
+  if (!ctx || !samples) return MCG_EINVAL;
+  if (int qrc = quiesce(ctx)) return qrc;
+  const int D = ctx->D;
+  if (D < 1) return set_error(ctx, MCG_ESTATE, "set the likelihood (ndim) first");
+  // pick_samples needs a j != i (mcmc.ml:202 loops forever on one sample)
+  if (M < 2) return set_error(ctx, MCG_EINVAL, "differential_evolution_proposal: need >= 2 samples");
+  if (M > (int64_t)0xFFFFFFFF) return set_error(ctx, MCG_EINVAL, "differential_evolution_proposal: too many samples");
+  int rc;
+  if ((rc = hip_check(ctx, ctx->d_de_pts.ensure((size_t)M * D * 8), "alloc DE samples"))) return rc;
+  if ((rc = hip_check(ctx, hipMemcpy(ctx->d_de_pts.p, samples, (size_t)M * D * 8, hipMemcpyHostToDevice), "copy DE samples"))) return rc;
+  ctx->de_M = M;
+  ctx->de_D = D;
+  return mcg_set_proposal(ctx, MCG_PROP_DE, &mode_hopping_frac, 1);
+}
+
 int mcg_init(mcg_ctx* ctx, int64_t nchains, const double* x_soa, const double* ll,
              const double* lp) {
   if (!ctx || nchains < 1 || !x_soa) return MCG_EINVAL;
@@ -474,8 +500,10 @@ int mcg_init(mcg_ctx* ctx, int64_t nchains, const double* x_soa, const double* l
   if ((rc = hip_check(ctx, ctx->d_ll.ensure(N * 8), "alloc ll"))) return rc;
   if ((rc = hip_check(ctx, ctx->d_lp.ensure(N * 8), "alloc lp"))) return rc;
   if ((rc = hip_check(ctx, ctx->d_nacc.ensure(N * 8), "alloc counters"))) return rc;
-  if ((rc = hip_check(ctx, hipMemcpy(ctx->d_x.p, x_soa, N * D * 8, hipMemcpyHostToDevice), "copy x"))) return rc;
+  // zero the (possibly new) counters before anything else can fail: mcg_get_counters reads
+  // them with the old N if a later copy errors out
   if ((rc = hip_check(ctx, hipMemset(ctx->d_nacc.p, 0, N * 8), "zero counters"))) return rc;
+  if ((rc = hip_check(ctx, hipMemcpy(ctx->d_x.p, x_soa, N * D * 8, hipMemcpyHostToDevice), "copy x"))) return rc;
   ctx->N = nchains;
   // steps_done is NOT reset: the Philox step counter runs on across inits like the reference's
   // global Random state (a re-init must not replay the previous draws); mcg_reseed restarts it
@@ -533,6 +561,8 @@ MhArgs base_args(mcg_ctx* ctx) {
   a.kd_root = (const double*)ctx->kd.d_root.p;
   a.kd_pt_leaf = (const int32_t*)ctx->kd.d_pt_leaf.p;
   a.kd_M = ctx->kd.M;
+  a.de_pts = (const double*)ctx->d_de_pts.p;
+  a.de_M = ctx->de_M;
   if (ctx->rj_active) rj_args(ctx, a);
   // one proposal scale and one box for every dim (bitwise): the fused step takes them as scalars
   const int D = ctx->D;
@@ -869,6 +899,29 @@ double mcg_log_total_error_estimate(double log_ev, double log_dev, int64_t nlive
   return 0.5 * (a + std::log1p(std::exp(b - a)));
 }
 
+int mcg_posterior_samples(mcg_ctx* ctx, const double* log_wts, int64_t npts, int64_t n, int64_t* idx) {
+  if (!ctx || !log_wts || npts < 1 || n < 0 || (n > 0 && !idx)) return MCG_EINVAL;
+  if (n > ((int64_t)1 << 40)) return set_error(ctx, MCG_EINVAL, "posterior_samples: n too large");
+  (void)hipSetDevice(ctx->opts.device);
+  int rc;
+  if ((rc = quiesce(ctx))) return rc;
+  // summed_weights (nested.ml:170-173): sequential, glibc exp, as the reference
+  std::vector<double> sums((size_t)npts);
+  sums[0] = std::exp(log_wts[0]);
+  for (int64_t i = 1; i < npts; ++i) sums[(size_t)i] = std::exp(log_wts[i]) + sums[(size_t)i - 1];
+  DevBuf d_sums, d_idx;
+  if ((rc = hip_check(ctx, d_sums.ensure((size_t)npts * 8), "alloc sums"))) return rc;
+  if ((rc = hip_check(ctx, d_idx.ensure((size_t)std::max<int64_t>(n, 1) * 8), "alloc idx"))) return rc;
+  if ((rc = hip_check(ctx, hipMemcpy(d_sums.p, sums.data(), (size_t)npts * 8, hipMemcpyHostToDevice), "copy sums"))) return rc;
+  const uint32_t call = ctx->post_calls++;
+  if ((rc = hip_check(ctx, launch_posterior_draw((const double*)d_sums.p, npts, n, (uint32_t)ctx->opts.seed,
+                                                 (uint32_t)(ctx->opts.seed >> 32), call, (int64_t*)d_idx.p,
+                                                 ctx->stream), "posterior launch"))) return rc;
+  if ((rc = hip_check(ctx, hipStreamSynchronize(ctx->stream), "posterior sync"))) return rc;
+  if (n > 0 && (rc = hip_check(ctx, hipMemcpy(idx, d_idx.p, (size_t)n * 8, hipMemcpyDeviceToHost), "copy idx"))) return rc;
+  return MCG_OK;
+}
+
 int mcg_set_timing(mcg_ctx* ctx, int32_t enabled) {
   if (!ctx) return MCG_EINVAL;
   timing_harvest(ctx);
@@ -898,6 +951,7 @@ int mcg_reseed(mcg_ctx* ctx, uint64_t seed) {
   if (int rc = quiesce(ctx)) return rc;
   ctx->opts.seed = seed;
   ctx->steps_done = 0;
+  ctx->post_calls = 0;
   return MCG_OK;
 }
 

@@ -62,10 +62,14 @@ struct mcg_ctx {
   std::vector<double> lik_host, pri_host, prop_host;
   mcg::DevBuf d_lik, d_pri, d_prop;
   mcg::KdState kd;
+  mcg::DevBuf d_de_pts;          // differential_evolution_proposal samples [M][D]
+  int64_t de_M = 0;
+  int de_D = 0;
   // chains
   int64_t N = 0;
   mcg::DevBuf d_x, d_ll, d_lp, d_nacc;
   uint64_t steps_done = 0;      // global RNG step counter (all runs)
+  uint32_t post_calls = 0;      // mcg_posterior_samples calls since create / reseed
   int64_t nsteps_total = 0;     // steps of the current chains since init / the last counter reset
   uint64_t acc_base = 0, rej_base = 0;  // tallies of earlier chain sets (folded at mcg_init)
   int64_t last_nsteps = 0;

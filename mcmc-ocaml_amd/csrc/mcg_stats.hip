@@ -97,4 +97,37 @@ hipError_t launch_tile_stats(const TileArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Nested.posterior_samples (nested.ml:167-178): one thread per draw, u = Random.float 1.0 from
+// Philox (i lo, i hi, call, tag 5), then weight_binary_search_index (nested.ml:152-165) over the
+// running sums (L2-resident; log2(npts) dependent loads per draw).
+__global__ void __launch_bounds__(256) posterior_draw_kernel(const double* __restrict__ sums, int64_t npts,
+                                                             int64_t n, uint32_t k0, uint32_t k1,
+                                                             uint32_t call, int64_t* __restrict__ idx) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const u32x4 w = philox((uint32_t)i, (uint32_t)((uint64_t)i >> 32), call, TAG_POSTERIOR << 16, k0, k1);
+  const double x = u53(w.x, w.y);
+  int64_t r;
+  if (x <= sums[0]) {
+    r = 0;
+  } else {
+    int64_t lo = 0, hi = npts - 1;
+    while (hi - lo > 1) {
+      const int64_t mid = (lo + hi) / 2;
+      if (x <= sums[mid]) hi = mid;
+      else lo = mid;
+    }
+    r = hi;
+  }
+  idx[i] = r;
+}
+
+hipError_t launch_posterior_draw(const double* sums, int64_t npts, int64_t n, uint32_t k0, uint32_t k1,
+                                 uint32_t call, int64_t* idx, hipStream_t s) {
+  if (n < 1) return hipSuccess;
+  hipLaunchKernelGGL(posterior_draw_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, sums, npts,
+                     n, k0, k1, call, idx);
+  return hipGetLastError();
+}
+
 }  // namespace mcg

@@ -91,6 +91,8 @@ SIGNATURES = {
                     C.c_void_p], C.c_int),
     "mcg_nested_get": ([C.c_void_p, _dp, _dp, _dp, _dp], C.c_int),
     "mcg_log_total_error_estimate": ([C.c_double, C.c_double, C.c_int64], C.c_double),
+    "mcg_set_de_proposal": ([C.c_void_p, _dp, C.c_int64, C.c_double], C.c_int),
+    "mcg_posterior_samples": ([C.c_void_p, _dp, C.c_int64, C.c_int64, _i64p], C.c_int),
     "mcg_evidence_direct": ([C.c_int32, C.c_int64, _dp, _dp, _dp, C.c_int64, _dp], C.c_int),
     "mcg_evidence_lebesgue": ([C.c_int32, C.c_int64, _dp, _dp, _dp, C.c_int64, C.c_double, _dp], C.c_int),
     "mcg_write_rows": ([C.c_char_p, C.c_int32, C.c_char_p, C.c_int64, C.c_int32, _dp], C.c_int),

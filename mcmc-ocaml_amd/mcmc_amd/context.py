@@ -56,7 +56,14 @@ class Context:
             self._check(L.lib().mcg_set_prior(self._p, pr.kind, L.dptr(pr.params), len(pr.params)))
             self._keep.append(pr)
         if jump is not None:
-            if isinstance(jump, T.KdInterp):
+            if isinstance(jump, T.DifferentialEvolution):
+                M = jump.samples.shape[0]
+                if jump.samples.shape[1] != lk.ndim:
+                    raise L.InvalidArgument(L.MCG_EINVAL, "DE samples have %d dims, model has %d"
+                                            % (jump.samples.shape[1], lk.ndim))
+                self._check(L.lib().mcg_set_de_proposal(self._p, L.dptr(jump.samples), M,
+                                                        jump.mode_hopping_frac))
+            elif isinstance(jump, T.KdInterp):
                 M = jump.pts.shape[0]
                 self._check(L.lib().mcg_set_kd_proposal(self._p, L.dptr(jump.pts), M,
                                                         L.dptr(jump.low), L.dptr(jump.high)))

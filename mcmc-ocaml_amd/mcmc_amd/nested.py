@@ -44,7 +44,7 @@ def nested_evidence(log_likelihood, log_prior, epsrel=0.01, nmcmc=1000, nlive=10
         warnings.warn("nested_evidence: max_dead (%d dead points) reached before the stop test "
                       "(nested.ml:45-48) fired; log Z comes from an unconverged run" % r.n_dead,
                       UnconvergedWarning, stacklevel=2)
-    return NestedOutput(r.log_ev, r.log_dev, pts, w, ll, lp, r.n_dead, r.n_gen, bool(r.converged))
+    return NestedOutput(r.log_ev, r.log_dev, pts, w, ll, lp, r.n_dead, r.n_gen, bool(r.converged), k)
 
 
 class UnconvergedWarning(RuntimeWarning):
@@ -53,10 +53,11 @@ class UnconvergedWarning(RuntimeWarning):
 
 class NestedOutput(tuple):
     """nested_output (nested.ml:20) plus ll / lp per point, counts and `converged` (False when
-    the max_dead cap ended the run before remaining_integral_negligable fired)."""
-    def __new__(cls, log_ev, log_dev, pts, log_wts, ll, lp, n_dead, n_gen, converged=True):
+    the max_dead cap ended the run before remaining_integral_negligable fired) and `k`, the
+    points retired per generation that the run actually used (None when unknown)."""
+    def __new__(cls, log_ev, log_dev, pts, log_wts, ll, lp, n_dead, n_gen, converged=True, k=None):
         t = super().__new__(cls, (log_ev, log_dev, pts, log_wts))
-        t.ll, t.lp, t.n_dead, t.n_gen, t.converged = ll, lp, n_dead, n_gen, converged
+        t.ll, t.lp, t.n_dead, t.n_gen, t.converged, t.k = ll, lp, n_dead, n_gen, converged, k
         return t
 
 
@@ -100,13 +101,23 @@ def log_total_error_estimate(log_ev, log_dev, nlive):
     return L.lib().mcg_log_total_error_estimate(log_ev, log_dev, nlive)
 
 
-def posterior_samples(n, output, rng=None):
-    """Nested.posterior_samples (nested.ml:152-178): multinomial resampling by cumulative weight
-    and the reference's binary search (host-side post-processing of the nested output)."""
-    _, _, pts, log_wts = output
-    rng = rng or np.random.default_rng(0)
-    sums = np.cumsum(np.exp(log_wts))
-    u = rng.random(n)
-    idx = np.searchsorted(sums, u, side="left")
-    idx = np.minimum(idx, len(sums) - 1)
-    return pts[idx]
+def posterior_indices(n, log_wts, ctx=None, seed=0):
+    """The draws of Nested.posterior_samples (nested.ml:167-178) as indices into the points:
+    cumulative weights and the reference's weight_binary_search_index (:152-165) on the device,
+    one Philox draw per sample (include/mcg.h mcg_posterior_samples).  Repeated calls on one
+    context draw new samples (the reference's global Random state advances)."""
+    ctx = ctx or Context(seed=seed)
+    w = np.ascontiguousarray(log_wts, dtype=np.float64)
+    idx = np.zeros(int(n), np.int64)
+    L.check(L.lib().mcg_posterior_samples(ctx.ptr, L.dptr(w), len(w), int(n), L.i64ptr(idx)), ctx.ptr)
+    return idx
+
+
+def posterior_samples(n, output, ctx=None, seed=0):
+    """Nested.posterior_samples n output (nested.ml:167-178): n points resampled by weight from a
+    nested_output (points (npts, D) and log weights)."""
+    _, _, pts, log_wts = output[:4]
+    if pts is None:
+        raise ValueError("posterior_samples needs the points: run nested_evidence with points=True")
+    assert len(pts) == len(log_wts)                 # nested.ml:169
+    return np.asarray(pts)[posterior_indices(n, log_wts, ctx, seed)]

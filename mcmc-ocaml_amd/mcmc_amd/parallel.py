@@ -10,6 +10,7 @@ number of GPUs.
 """
 import os
 import sys
+import warnings
 
 import numpy as np
 
@@ -105,6 +106,10 @@ def nested_evidence_replicas(log_likelihood, log_prior, epsrel=0.01, nmcmc=1000,
     output then has no points)."""
     rank, world = _world(group)
     nl, kk = replica_sizes(nlive, k, world)
+    if kk != k:
+        warnings.warn("nested_evidence_replicas: k = %d retired per generation cannot run on "
+                      "%d live points per replica; using k = %d (recorded as .k)" % (k, nl, kk),
+                      RuntimeWarning, stacklevel=2)
     with Context(seed=replica_seed(seed, rank), device=device) as ctx:
         out = _nested.nested_evidence(log_likelihood, log_prior, epsrel=epsrel, nmcmc=nmcmc,
                                       nlive=nl, mode_hopping_frac=mode_hopping_frac, k=kk, ctx=ctx,
@@ -113,6 +118,7 @@ def nested_evidence_replicas(log_likelihood, log_prior, epsrel=0.01, nmcmc=1000,
         print("replica rank %d: log Z %.6f n_dead %d n_gen %d" % (rank, out[0], out.n_dead, out.n_gen),
               file=sys.stderr, flush=True)
     if world == 1:
+        out.k = kk
         return out
     runs = allgather_runs(out, nl, kk, comm_device, group, points=points)
     merged = _nested.merge_runs(runs)
@@ -122,4 +128,5 @@ def nested_evidence_replicas(log_likelihood, log_prior, epsrel=0.01, nmcmc=1000,
                 rank, i, len(o.ll), a, b, o.ll[0], o.ll[-1], bool(np.all(np.diff(o.ll) >= 0))),
                 file=sys.stderr, flush=True)
         print("rank %d merged log Z %.6f" % (rank, merged[0]), file=sys.stderr, flush=True)
+    merged.k = kk
     return merged

@@ -101,6 +101,22 @@ class KdInterp:
         self.kind = L.PROP_KD_INTERP
 
 
+class DifferentialEvolution:
+    """Mcmc.differential_evolution_proposal ?mode_hopping_frac to_float from_float samples
+    (mcmc.ml:198-218) as an MH jump proposal: samples (M, D) (M >= 2), log_jump_prob = 0."""
+
+    def __init__(self, samples, mode_hopping_frac=0.0):
+        self.samples = np.ascontiguousarray(np.asarray(samples, dtype=np.float64))
+        if self.samples.ndim == 1:
+            self.samples = self.samples[:, None]
+        self.mode_hopping_frac = float(mode_hopping_frac)
+        self.kind = L.PROP_DE
+
+
+def differential_evolution_proposal(samples, mode_hopping_frac=0.0):
+    return DifferentialEvolution(samples, mode_hopping_frac)
+
+
 def shift_uniform(a, b):
     """y = x + random_between a b per dim (the uniform jumps of test/mcmc_test.ml:50,71-74,186-188);
     only as a component of combine_jump_proposals."""

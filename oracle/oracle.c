@@ -47,6 +47,7 @@ void or_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
 #define TAG_MH 1u
 #define TAG_NEST_WALK 3u
 #define TAG_NEST_PRIOR 4u
+#define TAG_POSTERIOR 5u
 #define CALL_ACCEPT 0xFFFF0000u
 #define CALL_DE_IDX 0xFFFF0001u
 #define CALL_DE_SCALE 0xFFFF0002u
@@ -272,6 +273,7 @@ typedef struct {
   const double* wlo; const double* whi; const double* wdx;   /* WRAP_UNIFORM */
   const or_kd* kd;
   int nmix; struct mix_comp* mix; int mix_kd;  /* MIXTURE (combine_jump_proposals) */
+  double de_mh, de_sigma; int64_t de_M; const double* de_pts;   /* DE: samples [M][D] */
 } prep_t;
 
 /* one component of Mcmc.combine_jump_proposals (mcmc.ml:165-185): normalised weight p, log p,
@@ -340,6 +342,14 @@ static int prep_model(const or_model* m, prep_t* p) {
     p->wlo = m->prop_params; p->whi = m->prop_params + D; p->wdx = m->prop_params + 2 * D;
   } else if (p->prop == MCG_PROP_KD_INTERP) {
     p->kd = (const or_kd*)m->kd;
+  } else if (p->prop == MCG_PROP_DE) {
+    /* oracle parameters: mode_hopping_frac, M, samples [M][D]; sigma of mcmc.ml:212 */
+    if (m->n_prop_params < 2) return -1;
+    p->de_mh = m->prop_params[0];
+    p->de_M = (int64_t)m->prop_params[1];
+    p->de_pts = m->prop_params + 2;
+    if (p->de_M < 2 || m->n_prop_params != 2 + p->de_M * D) return -1;
+    p->de_sigma = 2.38 / sqrt(2.0 * (double)D);
   } else if (p->prop == MCG_PROP_MIXTURE) {
     /* parameters: ncomp, then per component p, kind, ljp_mode, params (include/mcg.h) */
     const double* q = m->prop_params;
@@ -481,16 +491,30 @@ double or_logprior(const or_model* m, const double* x) {
   prep_t p; prep_model(m, &p); double v = prior_eval(&p, x); prep_free(&p); return v;
 }
 
-/* Mcmc.uniform_wrapping (mcmc.ml:187-196) with the uniform injected */
-static double wrap_uniform(double xmin, double xmax, double dx, double x, double u) {
+/* Mcmc.uniform_wrapping (mcmc.ml:187-196) with the uniform injected: the reference's loop
+ * (mcmc.ml:189-195) exactly for up to OR_WRAP_EXACT reflections; an exit where that loop never
+ * ends (nx == xmax reflects onto itself; rounding 2-cycles at |nx| >> width); past the bound the
+ * remaining excess folded by the loop's real-arithmetic limit (triangle wave of period 2w). */
+#define OR_WRAP_EXACT 1024
+double or_wrap_uniform(double xmin, double xmax, double dx, double x, double u) {
   double nx = x + (u - 0.5) * dx;
-  for (int it = 0; it < 64; ++it) {
-    if (nx < xmin) nx = xmin + (xmin - nx);
-    else if (nx >= xmax) nx = xmax - (nx - xmax);
-    else break;
+  for (int it = 0; it < OR_WRAP_EXACT; ++it) {
+    if (nx < xmin) {
+      nx = xmin + (xmin - nx);
+    } else if (nx >= xmax) {
+      const double r = xmax - (nx - xmax);
+      if (r == nx) return nx;
+      nx = r;
+    } else {
+      return nx;
+    }
   }
-  return nx;
+  const double w = xmax - xmin;
+  double m = fmod(nx - xmin, 2.0 * w);
+  if (m < 0.0) m += 2.0 * w;
+  return m < w ? xmin + m : xmax - (m - w);
 }
+#define wrap_uniform or_wrap_uniform
 
 /* ======================================================================================
  * kD tree (kd_tree.ml) + Interpolate_pdf (interpolate_pdf.ml) -- declared here, defined below
@@ -590,6 +614,26 @@ static int mh_step(const prep_t* p, uint64_t seed, uint32_t gid, uint64_t T, cha
       lqy = t->llogq[kd_find_leaf_idx(t, y)];
       lf = lqy;         /* log_jump_prob start proposed = log q(proposed) */
       lb = c->lq;       /* log_jump_prob proposed start = log q(start) */
+      break;
+    }
+    case MCG_PROP_DE: {
+      /* Mcmc.differential_evolution_proposal (mcmc.ml:198-218): pick_samples i != j
+         (:199-203; j from the n - 1 others instead of the retry loop), d = 1.0 with
+         probability mode_hopping_frac (:209; the && short-circuits at 0) else
+         draw_gaussian 0.0 sigma (:212-213), z'_d = z_d + d (y_d - x_d) (:214-217) */
+      uint32_t w[4];
+      rng4(seed, gid, lo, CALL_DE_IDX, TAG_MH, hi, w);
+      uint32_t n = (uint32_t)p->de_M;
+      uint32_t i = or_randint(w[0], w[1], n);
+      uint32_t jj = or_randint(w[2], w[3], n - 1);
+      uint32_t j = jj + (jj >= i ? 1u : 0u);
+      rng4(seed, gid, lo, CALL_DE_SCALE, TAG_MH, hi, w);
+      double dsc;
+      if (p->de_mh != 0.0 && or_u53(w[0], w[1]) < p->de_mh) dsc = 1.0;
+      else dsc = p->de_sigma * or_normal(w[2]);
+      const double* xi = p->de_pts + (int64_t)i * D;
+      const double* yj = p->de_pts + (int64_t)j * D;
+      for (int d = 0; d < D; ++d) y[d] = c->x[d] + dsc * (yj[d] - xi[d]);
       break;
     }
     case MCG_PROP_MIXTURE: {
@@ -1295,6 +1339,22 @@ int64_t or_weight_binary_search_index(double x, const double* sums, int64_t n) {
     if (x <= sums[mid]) hi = mid; else lo = mid;
   }
   return hi;
+}
+
+/* Nested.posterior_samples (nested.ml:167-178) as indices, RNG injected: summed weights
+ * sequentially with glibc exp (:170-173), draw i of call `call` = u53 of Philox
+ * (i lo, i hi, call, tag 5), then weight_binary_search_index (:152-165). */
+void or_posterior_indices(uint64_t seed, uint32_t call, const double* log_wts, int64_t npts, int64_t n,
+                          int64_t* idx) {
+  double* sums = (double*)malloc((size_t)npts * sizeof(double));
+  sums[0] = exp(log_wts[0]);
+  for (int64_t i = 1; i < npts; ++i) sums[i] = exp(log_wts[i]) + sums[i - 1];
+  for (int64_t i = 0; i < n; ++i) {
+    uint32_t w[4];
+    rng4(seed, (uint32_t)i, (uint32_t)((uint64_t)i >> 32), call, TAG_POSTERIOR, 0, w);
+    idx[i] = or_weight_binary_search_index(or_u53(w[0], w[1]), sums, npts);
+  }
+  free(sums);
 }
 
 /* ======================================================================================

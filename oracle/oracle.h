@@ -36,6 +36,9 @@ double or_plse(double a, double b);
 /* normals for the MH proposal of chain c at step t: z[0..D) */
 void or_step_normals(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, int D, double* z);
 
+/* Mcmc.uniform_wrapping (mcmc.ml:187-196) with the uniform u injected */
+double or_wrap_uniform(double xmin, double xmax, double dx, double x, double u);
+
 /* ---- Stats restatements (stats.ml) ---- */
 double or_log_sum_logs(double a, double b);                      /* stats.ml:240-248 */
 double or_mean(const double* xs, int64_t n);                     /* stats.ml:17-23 */
@@ -142,6 +145,8 @@ void or_evidence_weights(int64_t n, int64_t nlive, int64_t k, const double* ll,
                          double* log_ev, double* log_dev, double* log_wts);
 double or_log_total_error_estimate(double log_ev, double log_dev, int64_t nlive); /* :148-150 */
 int64_t or_weight_binary_search_index(double x, const double* sums, int64_t n);  /* :152-165 */
+void or_posterior_indices(uint64_t seed, uint32_t call, const double* log_wts, int64_t npts, int64_t n,
+                          int64_t* idx);                                            /* :167-178 */
 
 /* ---- kD tree / Interpolate_pdf (kd_tree.ml:155-175, interpolate_pdf.ml:80-142) ---- */
 typedef struct or_kd or_kd;

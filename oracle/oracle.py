@@ -69,6 +69,8 @@ def lib():
         L.or_normal.argtypes = [C.c_uint32]
         L.or_normal.restype = C.c_double
         L.or_step_normals.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, C.c_int, _dp]
+        L.or_wrap_uniform.argtypes = [C.c_double] * 5
+        L.or_wrap_uniform.restype = C.c_double
         L.or_log_sum_logs.argtypes = [C.c_double, C.c_double]
         L.or_log_sum_logs.restype = C.c_double
         for name in ("or_mean", "or_std"):
@@ -101,6 +103,8 @@ def lib():
         L.or_log_total_error_estimate.restype = C.c_double
         L.or_weight_binary_search_index.argtypes = [C.c_double, _dp, C.c_int64]
         L.or_weight_binary_search_index.restype = C.c_int64
+        L.or_posterior_indices.argtypes = [C.c_uint64, C.c_uint32, _dp, C.c_int64, C.c_int64,
+                                           C.POINTER(C.c_int64)]
         L.or_kd_build.argtypes = [_dp, C.c_int64, C.c_int, _dp, _dp]
         L.or_kd_build.restype = C.c_void_p
         L.or_kd_free.argtypes = [C.c_void_p]

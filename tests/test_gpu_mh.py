@@ -337,3 +337,120 @@ def test_mixture_with_kd_component_bit_exact(oracle, T, D):
     o["tiles"] = oracle.tile_stats(D, x0.shape[1], 40, o)
     g = run_gpu(lik, pri, mix, x0, 21, nbin=3, nskip=1, n_rec=40)
     assert_same(g, o)
+
+
+def test_wrap_uniform_far_steps_bit_exact(oracle, T):
+    """Mcmc.uniform_wrapping (mcmc.ml:187-196) with dx = 200 box widths (~100 reflections per
+    proposal, beyond the old 64-reflection cap) and with dx = 1e5 widths (past the exact-loop
+    bound: the closed-form fold): GPU == oracle bit for bit and every recorded point in the box."""
+    D = 4
+    lo, hi = -np.ones(D), np.ones(D)
+    lik = T.diag_gauss(np.zeros(D), 0.5 * np.ones(D))
+    pri = T.box(lo, hi, -D * math.log(2.0))
+    x0 = np.random.default_rng(21).uniform(-1, 1, size=(D, 320))
+    for widths in (200.0, 1e5):
+        prop = T.uniform_wrapping(lo, hi, widths * (hi - lo))
+        g = run_gpu(lik, pri, prop, x0, 23, nbin=2, nskip=1, n_rec=60)
+        o = run_oracle(oracle, lik, pri, prop, x0, 23, 2, 1, 60)
+        assert_same(g, o)
+        assert np.all(g["rec_x"] >= -1.0) and np.all(g["rec_x"] <= 1.0)
+        assert 0 < g["nacc"] < g["nacc"] + g["nrej"]
+
+
+@pytest.mark.parametrize("mode_hop", [0.0, 0.3])
+@pytest.mark.parametrize("lik_name", ["diag", "fullcov"])
+def test_differential_evolution_proposal_bit_exact(oracle, T, mode_hop, lik_name):
+    """Mcmc.differential_evolution_proposal (mcmc.ml:198-218) as the MH jump over a 500-sample
+    array: GPU == oracle bit for bit (records, bitmap, state, counters, tiles); mode hopping 0
+    (the scale draw never consulted) and 0.3."""
+    rng = np.random.default_rng(31)
+    D = 4
+    mu, sg = rng.uniform(-1, 1, D), rng.uniform(0.5, 1.5, D)
+    if lik_name == "diag":
+        lik = T.diag_gauss(mu, sg)
+    else:
+        lik = T.fullcov_gauss(mu, np.diag(sg ** 2) + 0.1)
+    pri = T.box(-10 * np.ones(D), 10 * np.ones(D), -D * math.log(20.0))
+    samples = rng.normal(mu, sg, size=(500, D))
+    de = T.differential_evolution_proposal(samples, mode_hop)
+    x0 = rng.normal(mu[:, None], sg[:, None], size=(D, 200))
+    g = run_gpu(lik, pri, de, x0, 41, nbin=3, nskip=2, n_rec=50)
+    de_params = np.concatenate([[mode_hop, 500], samples.ravel()])
+    o = run_oracle(oracle, lik, pri, T.Proposal(4, de_params), x0, 41, 3, 2, 50)
+    assert_same(g, o)
+    assert 0 < g["nacc"] < g["nacc"] + g["nrej"]
+
+
+def test_differential_evolution_proposal_reference_width(T):
+    """test/mcmc_test.ml:213-224 on the GPU: 1e6 samples ~ N(10, 1), mode_hopping_frac 1.0,
+    proposals from [0] have mean 0 and sd sqrt 2 within 5e-3 (flat target: every proposal of
+    one MH step of 1e6 chains is accepted, so the state is 1e6 independent proposals)."""
+    from mcmc_amd import Context
+    n = 1_000_000
+    samples = np.random.default_rng(1).normal(10.0, 1.0, size=(n, 1))
+    ctx = Context(seed=3)
+    ctx.set_model(T.flat(1), T.flat_prior(), T.differential_evolution_proposal(samples, 1.0))
+    ctx.init(np.zeros((1, n)), np.zeros(n), np.zeros(n))
+    ctx.run(nbin=1, n_rec=0, record_x=False, record_llp=False)
+    z = ctx.state()[0][0]
+    assert ctx.counters() == (n, 0)
+    assert abs(z.mean()) < 5e-3
+    assert abs(z.std(ddof=1) - math.sqrt(2.0)) < 5e-3
+    ctx.close()
+
+
+def _c5_target(T, D=64, seed=5):
+    rng = np.random.default_rng(seed)
+    Q, _ = np.linalg.qr(rng.normal(size=(D, D)))
+    lam = np.exp(rng.uniform(math.log(0.1), math.log(10.0), D))
+    cov = (Q * lam) @ Q.T
+    cov = 0.5 * (cov + cov.T)
+    mu = rng.uniform(-1, 1, D)
+    s = 2.38 / math.sqrt(D) * math.sqrt(lam.min())
+    return T.fullcov_gauss(mu, cov), mu, cov, s
+
+
+def _assert_shards_equal_full(full, parts):
+    cat = lambda k, ax: np.concatenate([p[k] for p in parts], axis=ax)
+    np.testing.assert_array_equal(full["x"], cat("x", 1))
+    np.testing.assert_array_equal(full["ll"], cat("ll", 0))
+    np.testing.assert_array_equal(full["lp"], cat("lp", 0))
+    np.testing.assert_array_equal(full["rec_x"], cat("rec_x", 2))
+    np.testing.assert_array_equal(full["rec_ll"], cat("rec_ll", 1))
+    # accept bitmap rows: chain c of shard r is chain r*N + c of the full run (N % 64 == 0)
+    np.testing.assert_array_equal(full["bits"], cat("bits", 1))
+    np.testing.assert_array_equal(full["tiles"], cat("tiles", 0))
+    assert full["nacc"] == sum(p["nacc"] for p in parts)
+
+
+def test_sharded_fullcov_matrix_core_equals_single_context(T):
+    """C5's sharding (BASELINE configs[4]) on the matrix-core kernel
+    (mh_fullcov_kernel<64>, 4 lanes per chain): two contexts at chain_offset 0 and 256 reproduce
+    one 512-chain context bit for bit -- state, records, accept bitmap, tiles -- and the tiles
+    combine to identical moments / harmonic-mean evidence."""
+    from mcmc_amd.context import combine_tiles
+    lik, mu, cov, s = _c5_target(T)
+    pri, prop = T.flat_prior(), T.gauss(s)
+    x0 = mu[:, None] + np.linalg.cholesky(cov) @ np.random.default_rng(6).normal(size=(64, 512))
+    full = run_gpu(lik, pri, prop, x0, 19, nbin=7, nskip=1, n_rec=40)
+    a = run_gpu(lik, pri, prop, x0[:, :256], 19, nbin=7, nskip=1, n_rec=40, chain_offset=0)
+    b = run_gpu(lik, pri, prop, x0[:, 256:], 19, nbin=7, nskip=1, n_rec=40, chain_offset=256)
+    _assert_shards_equal_full(full, [a, b])
+    for u, v in zip(combine_tiles(64, full["tiles"]), combine_tiles(64, np.concatenate([a["tiles"], b["tiles"]]))):
+        np.testing.assert_array_equal(u, v)
+
+
+def test_sharded_kd_interp_equals_single_context(T):
+    """C4's kD independence proposal (lanes split per chain) sharded over two contexts at
+    chain_offset 0 and 256 equals one 512-chain context bit for bit (shards are whole 256-chain
+    tiles, as the multi-GPU runs use)."""
+    rng = np.random.default_rng(22)
+    D = 8
+    pts = rng.normal(size=(4096, D))
+    lo, hi = -10 * np.ones(D), 10 * np.ones(D)
+    lik, pri, kdp = T.diag_gauss(np.zeros(D), np.ones(D)), T.box(lo, hi), T.KdInterp(pts, lo, hi)
+    x0 = rng.normal(size=(D, 512))
+    full = run_gpu(lik, pri, kdp, x0, 29, nbin=5, nskip=1, n_rec=30)
+    a = run_gpu(lik, pri, kdp, x0[:, :256], 29, nbin=5, nskip=1, n_rec=30, chain_offset=0)
+    b = run_gpu(lik, pri, kdp, x0[:, 256:], 29, nbin=5, nskip=1, n_rec=30, chain_offset=256)
+    _assert_shards_equal_full(full, [a, b])

@@ -321,3 +321,34 @@ def test_nested_points_left_on_device_same_result(T):
     np.testing.assert_array_equal(a[3], b[3])
     np.testing.assert_array_equal(a.ll, b.ll)
     np.testing.assert_array_equal(a.lp, b.lp)
+
+
+@pytest.mark.gpu
+def test_posterior_samples_bit_exact_and_advancing(oracle, T):
+    """Nested.posterior_samples (nested.ml:152-178) on the device: the drawn indices equal the
+    oracle's weight_binary_search_index over the same Philox draws; a second call on the same
+    context draws new samples (call counter 1), a reseed restarts at call 0; a one-point output
+    always returns that point, and the resampled mean follows the weights."""
+    import ctypes as C
+    from mcmc_amd import Context, nested
+    lik, pri = unit_square_gauss(T)
+    ctx = Context(seed=17)
+    out = nested.nested_evidence(lik, pri, nlive=400, nmcmc=40, k=8, ctx=ctx)
+    w = np.ascontiguousarray(out[3])
+    n = 20000
+    calls = []
+    for call in range(2):
+        got = nested.posterior_indices(n, w, ctx=ctx)
+        ref = np.zeros(n, np.int64)
+        oracle.lib().or_posterior_indices(17, call, oracle.dptr(w), len(w), n,
+                                          ref.ctypes.data_as(C.POINTER(C.c_int64)))
+        np.testing.assert_array_equal(got, ref)
+        calls.append(got)
+    assert not np.array_equal(calls[0], calls[1])
+    ctx.reseed(17)
+    np.testing.assert_array_equal(nested.posterior_indices(n, w, ctx=ctx), calls[0])
+    assert np.all(nested.posterior_indices(50, np.zeros(1), ctx=ctx) == 0)
+    ps = nested.posterior_samples(n, out, ctx=ctx)
+    ww = np.exp(w)
+    assert abs(ps[:, 0].mean() - (ww * out[2][:, 0]).sum()) < 0.01
+    ctx.close()

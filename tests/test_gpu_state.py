@@ -166,3 +166,27 @@ def test_nested_cap_reports_unconverged_and_failed_run_clears_result(T):
     rc = L.lib().mcg_nested_get(ctx.ptr, L.dptr(p), L.dptr(a), L.dptr(a), L.dptr(a))
     assert rc == L.MCG_ESTATE
     ctx.close()
+
+
+def test_failed_set_rjmcmc_leaves_counters_unchanged(oracle, T):
+    """mcg_set_rjmcmc folds the device tallies into the context totals before it validates the
+    models; a model it then rejects (unsupported likelihood kind) must leave get_counters where
+    it was: neither counting the accepts twice nor wrapping the rejects."""
+    from mcmc_amd import Context, mcmc
+    from mcmc_amd._lib import McgError
+    lik, pri, prop, mu, sg = c2_model(T)
+    x0 = np.random.default_rng(12).normal(mu[:, None], sg[:, None], size=(8, 1024))
+    ctx = Context(seed=13)
+    ctx.set_model(lik, pri, prop)
+    ctx.init(x0)
+    ctx.run(nbin=50, n_rec=0, record_x=False, record_llp=False)
+    before = ctx.counters()
+    assert before[0] > 0 and sum(before) == 50 * 1024
+    data = T.cauchy_data(np.zeros((5, 1)))            # RJ rejects data likelihoods after the fold
+    bad = T.RjModel(data, T.flat_prior(), T.rj_gauss(0.1), T.rj_indep_gauss([0, 1], [1, 1]), 0.5)
+    good = T.RjModel(T.flat(2), T.flat_prior(), T.rj_gauss(0.1), T.rj_indep_gauss([0, 1], [1, 1]), 0.5)
+    with pytest.raises(McgError):
+        mcmc.rjmcmc_array(4, bad, good, (np.zeros(2), np.zeros(2)), nchains=8, ctx=ctx)
+    assert ctx.counters() == before
+    assert ctx.counters() == before                    # reading twice changes nothing either
+    ctx.close()

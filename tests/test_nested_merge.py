@@ -58,25 +58,33 @@ def test_merge_of_one_run_is_the_reference_estimate(oracle):
 
 
 def test_merged_replicas_estimate_unit_evidence(oracle):
-    """nested_test.ml:23-39 on a merged run: 4 replicas of 250 live points = one run of 1000.
+    """nested_test.ml:23-39 on merged runs: 4 replicas of 250 live points = one run of 1000.
 
     The reference's check |Z - 1| < 2 err is a ~1.5-sigma test: log_total_error_estimate
     (nested.ml:148-150) puts err ~ Z / sqrt(nlive), while the spread of Z is Z sqrt(H / nlive)
-    with H ~ 1.8 nats here.  Over 24 seed sets of this test (spec v7) (Z - 1)/err has sd 1.36
-    and 4 of 24 sets fail the check, as the reference test itself would; the seeds below are
-    one of the passing sets (the first one, 21-24, gives -2.07 err)."""
-    runs = _runs(oracle, [25, 26, 27, 28], 250, nmcmc=1000)   # the reference default
-    got = _merge(runs, 250, 1)
-    ev = math.exp(got[0])
-    err = math.exp(oracle.lib().or_log_total_error_estimate(got[0], got[1], 1000))
-    assert abs(ev - 1.0) < 2 * err
-    assert err < 0.1
-    w = np.exp(got[3])
-    assert abs(w.sum() - 1.0) < 1e-8
-    assert abs((w * got[2][:, 0]).sum() - 0.5) < 0.1
-    # the merged run is one run of 1000 live points: its information gives the error scale
-    H = float(np.sum(w * got.ll) - got[0])
-    assert H > 0
+    with H ~ 1.8 nats here, so a single seed set fails it now and then, as the reference test
+    itself would.  The check is therefore made on an ensemble of 12 consecutive seed sets
+    (21-24, 25-28, ..., 65-68; no selection): the mean of (Z - 1)/err must be within 3 standard
+    errors of 0 (a systematic evidence bias of ~1.4 err would fail it), the spread must stay near
+    the sqrt(H)-inflated error scale, and most sets must pass the reference's own 2-err check.
+    (Spec v7: mean -0.19, sd 1.58, 10 of 12 sets pass.)"""
+    zs = []
+    for base in range(21, 21 + 4 * 12, 4):
+        got = _merge(_runs(oracle, [base, base + 1, base + 2, base + 3], 250, nmcmc=1000), 250, 1)
+        ev = math.exp(got[0])
+        err = math.exp(oracle.lib().or_log_total_error_estimate(got[0], got[1], 1000))
+        assert err < 0.1
+        w = np.exp(got[3])
+        assert abs(w.sum() - 1.0) < 1e-8
+        assert abs((w * got[2][:, 0]).sum() - 0.5) < 0.1
+        # the merged run is one run of 1000 live points: its information gives the error scale
+        assert float(np.sum(w * got.ll) - got[0]) > 0
+        zs.append((ev - 1.0) / err)
+    zs = np.array(zs)
+    sd = zs.std(ddof=1)
+    assert abs(zs.mean()) < 3 * sd / math.sqrt(len(zs)), zs
+    assert 0.5 < sd < 2.5, zs
+    assert np.sum(np.abs(zs) < 2) >= 8, zs
 
 
 def test_merge_rejects_bad_arguments(gpu_lib):

@@ -444,3 +444,108 @@ def test_device_normal_formulation_matches_oracle(oracle):
     words += [int(w) for E in range(1, 32) for w in rng.integers(1 << (E - 1), 1 << E, size=8)]
     for w in words:
         assert dev(w) == oracle.normal(w), hex(w)
+
+
+def _wrap_literal(xmin, xmax, dx, x, u, cap=1 << 22):
+    """Mcmc.uniform_wrapping (mcmc.ml:187-196) literally: the unbounded reflection loop (capped
+    only to keep a test from hanging where the reference would)."""
+    nx = x + (u - 0.5) * dx
+    for _ in range(cap):
+        if nx < xmin:
+            nx = xmin + (xmin - nx)
+        elif nx >= xmax:
+            nx = xmax - (nx - xmax)
+        else:
+            return nx
+    return None
+
+
+def test_wrap_uniform_equals_the_unbounded_loop(oracle):
+    """The oracle's wrap (shared bit for bit with the kernels) equals the reference's unbounded
+    loop wherever that needs <= 1024 reflections (dx up to 200 widths here: ~100), stays in
+    [xmin, xmax) beyond it, and ends where the reference's loop would not (nx == xmax)."""
+    L = oracle.lib()
+    rng = np.random.default_rng(5)
+    for xmin, xmax in ((-1.0, 1.0), (0.1, 0.2), (-8.0, 8.0), (3.0, 3.5)):
+        w = xmax - xmin
+        for dxw in (0.01, 0.5, 1.0, 3.0, 200.0):
+            for _ in range(400):
+                x, u = rng.uniform(xmin, xmax), rng.random()
+                got = L.or_wrap_uniform(xmin, xmax, dxw * w, x, u)
+                ref = _wrap_literal(xmin, xmax, dxw * w, x, u)
+                assert got == ref, (xmin, xmax, dxw, x, u)
+                assert xmin <= got < xmax
+        # 1e5 widths: past the exact bound, folded by the loop's real-arithmetic limit; the
+        # reference's ~5e4 reflections each round at |nx| ~ 1e5 w, so the two agree to the
+        # loop's own accumulated rounding (observed <= 3e-6 w)
+        for _ in range(25):
+            x, u = rng.uniform(xmin, xmax), rng.random()
+            got = L.or_wrap_uniform(xmin, xmax, 1e5 * w, x, u)
+            ref = _wrap_literal(xmin, xmax, 1e5 * w, x, u)
+            assert xmin <= got <= xmax
+            if ref is not None:
+                assert abs(got - ref) <= 1e-4 * w, (got, ref)
+    # landing exactly on xmax: the reference reflects xmax onto itself forever; the wrap stops
+    assert L.or_wrap_uniform(0.0, 1.0, 2.0, 0.0, 1.0) == 1.0
+    assert math.isnan(L.or_wrap_uniform(0.0, 1.0, 1.0, float("nan"), 0.5))
+
+
+def test_posterior_indices_follow_the_reference_search(oracle):
+    """or_posterior_indices (nested.ml:167-178): the summed weights of :170-173 and the bisection
+    of weight_binary_search_index (:152-165), restated here line by line, on the oracle's own
+    Philox uniforms; every index is the first whose running sum reaches u."""
+    import ctypes as C
+    L = oracle.lib()
+    rng = np.random.default_rng(3)
+    lw = np.log(rng.dirichlet(np.ones(257)))
+    sums = np.zeros(len(lw))
+    sums[0] = math.exp(lw[0])
+    for i in range(1, len(lw)):
+        sums[i] = math.exp(lw[i]) + sums[i - 1]
+
+    def search(x):
+        if x <= sums[0]:
+            return 0
+        lo, hi = 0, len(sums) - 1
+        while hi - lo > 1:
+            mid = (lo + hi) // 2
+            if x <= sums[mid]:
+                hi = mid
+            else:
+                lo = mid
+        return hi
+
+    n = 3000
+    idx = np.zeros(n, np.int64)
+    L.or_posterior_indices(9, 2, oracle.dptr(np.ascontiguousarray(lw)), len(lw), n,
+                           idx.ctypes.data_as(C.POINTER(C.c_int64)))
+    for i in range(n):
+        ctr = (C.c_uint32 * 4)(i, 0, 2, 5 << 16)
+        key = (C.c_uint32 * 2)(9, 0)
+        w = (C.c_uint32 * 4)()
+        L.or_philox(ctr, key, w)
+        assert idx[i] == search(L.or_u53(w[0], w[1]))
+    counts = np.bincount(idx, minlength=len(lw)) / n
+    assert np.abs(counts - np.exp(lw)).max() < 0.02
+
+
+def test_differential_evolution_proposal_width(oracle):
+    """test/mcmc_test.ml:213-224 re-expressed on the oracle's DE proposal (mcmc.ml:198-218):
+    1e6 samples ~ N(10, 1), mode_hopping_frac 1.0, proposals from [0]: mean 0 and sd sqrt 2
+    within 5e-3.  A flat target accepts every proposal, so one MH step of 1e6 chains started at
+    0 returns 1e6 independent proposals."""
+    n = 1_000_000
+    samples = np.random.default_rng(1).normal(10.0, 1.0, size=n)
+    m = oracle.Model(1, 0, [], 0, [], 4, np.concatenate([[1.0, n], samples]))
+    x0 = np.zeros((1, n))
+    r = oracle.mh_run(m, 3, x0, np.zeros(n), np.zeros(n), nbin=1, n_rec=0, record_x=False,
+                      record_llp=False, record_accept=False, accumulate=False, nthreads=8)
+    z = r["x"][0]
+    assert int(r["nacc"].sum()) == n
+    assert abs(z.mean()) < 5e-3
+    assert abs(z.std(ddof=1) - math.sqrt(2.0)) < 5e-3
+    # mode_hopping_frac 0: d ~ N(0, 2.38/sqrt 2) times (s_j - s_i) ~ N(0, 2): sd 2.38
+    m0 = oracle.Model(1, 0, [], 0, [], 4, np.concatenate([[0.0, n], samples]))
+    r0 = oracle.mh_run(m0, 3, x0, np.zeros(n), np.zeros(n), nbin=1, n_rec=0, record_x=False,
+                       record_llp=False, record_accept=False, accumulate=False, nthreads=8)
+    assert abs(r0["x"][0].std(ddof=1) - 2.38) < 0.02
