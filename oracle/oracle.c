@@ -274,6 +274,7 @@ typedef struct {
   const or_kd* kd;
   int nmix; struct mix_comp* mix; int mix_kd;  /* MIXTURE (combine_jump_proposals) */
   double de_mh, de_sigma; int64_t de_M; const double* de_pts;   /* DE: samples [M][D] */
+  const double* raw_lik;                       /* the caller's likelihood parameters */
 } prep_t;
 
 /* one component of Mcmc.combine_jump_proposals (mcmc.ml:165-185): normalised weight p, log p,
@@ -297,6 +298,7 @@ static int prep_model(const or_model* m, prep_t* p) {
   int D = m->ndim;
   p->D = D; p->lik = m->lik_kind; p->prior = m->prior_kind; p->prop = m->prop_kind;
   const double* q = m->lik_params;
+  p->raw_lik = q;
   switch (p->lik) {
     case MCG_LIK_FLAT: break;
     case MCG_LIK_DIAG_GAUSS:
@@ -413,8 +415,43 @@ static inline double canon8(const double* A) {
   return ((A[0] + A[4]) + (A[2] + A[6])) + ((A[1] + A[5]) + (A[3] + A[7]));
 }
 
+/* ---- the reference's literal arithmetic (DESIGN.md §2 "literal mode") ----
+ * The canonical arithmetic above (fma residuals, 8-accumulator sum, host constant C, portable
+ * log of the accept uniform, portable log-sum of the nested running estimate) is what the GPU
+ * computes.  or_set_literal(1) switches the oracle to the reference's own operation order:
+ * Stats.log_multi_gaussian (stats.ml:98-108: division, sequential sum from d = 0, glibc log sigma
+ * in every term, the trailing +. 0.0), glibc log of the accept uniform (mcmc.ml:49), and
+ * Stats.log_sum_logs with glibc exp / log1p (stats.ml:240-248) for the nested running estimate
+ * and stop test, folded one retired point at a time (nested.ml:138-141).  The Gaussian shell
+ * (no reference closure) is Stats.log_gaussian of the sequential-sum radius.  Process-wide;
+ * set it before a run, not during one. */
+static int g_literal = 0;
+void or_set_literal(int on) { g_literal = on != 0; }
+int or_get_literal(void) { return g_literal; }
+
+static double lik_literal(const prep_t* p, const double* x) {
+  const int D = p->D;
+  const double* q = p->raw_lik;
+  if (p->lik == MCG_LIK_DIAG_GAUSS) {
+    double result = 0.0;
+    for (int i = 0; i < D; ++i) {
+      double dx = (x[i] - q[i]) / q[D + i];
+      result = result + ((-0.91893853320467274178 - log(q[D + i])) - 0.5 * dx * dx);
+    }
+    return result + 0.0;
+  }
+  if (p->lik == MCG_LIK_GAUSS_SHELL) {
+    double ss = 0.0;
+    for (int i = 0; i < D; ++i) { double e = x[i] - q[i]; ss = ss + e * e; }
+    double dx = (sqrt(ss) - q[D]) / q[D + 1];
+    return (-0.91893853320467274178 - log(q[D + 1])) - 0.5 * dx * dx;
+  }
+  return NAN;
+}
+
 static double lik_eval(const prep_t* p, const double* x) {
   int D = p->D;
+  if (g_literal && (p->lik == MCG_LIK_DIAG_GAUSS || p->lik == MCG_LIK_GAUSS_SHELL)) return lik_literal(p, x);
   double A[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   switch (p->lik) {
     case MCG_LIK_FLAT: return 0.0;
@@ -572,7 +609,10 @@ static double mix_log_jp(const prep_t* p, const double* x, const double* y, doub
   return acc;
 }
 
-static int mh_step(const prep_t* p, uint64_t seed, uint32_t gid, uint64_t T, chain_t* c) {
+typedef struct { double y[256]; double lly, lpy, ratio, u; int acc; } step_probe;
+
+static int mh_step(const prep_t* p, uint64_t seed, uint32_t gid, uint64_t T, chain_t* c,
+                   step_probe* pr) {
   int D = p->D;
   uint32_t lo = (uint32_t)T, hi = (uint32_t)(T >> 32);
   double y[256];
@@ -692,12 +732,61 @@ static int mh_step(const prep_t* p, uint64_t seed, uint32_t gid, uint64_t T, cha
   double ratio = ((post_y - post_x) + lb) - lf;
   uint32_t w[4];
   rng4(seed, gid, lo, CALL_ACCEPT, TAG_MH, hi, w);
-  double lu = or_log(or_u53(w[0], w[1]));
-  if (lu < ratio) {
+  const double u = or_u53(w[0], w[1]);
+  double lu = g_literal ? log(u) : or_log(u);
+  const int acc = lu < ratio;
+  if (pr) {
+    memcpy(pr->y, y, sizeof(double) * (size_t)D);
+    pr->lly = lly; pr->lpy = lpy; pr->ratio = ratio; pr->u = u; pr->acc = acc;
+  }
+  if (acc) {
     for (int d = 0; d < D; ++d) c->x[d] = y[d];
     c->ll = lly; c->lp = lpy; c->lq = lqy;
     return 1;
   }
+  return 0;
+}
+
+/* Shadow of the reference's literal arithmetic along a canonical chain: N chains run nsteps
+ * canonical MH steps (what the GPU does) from (x [D][N], ll, lp) at global step step0; at every
+ * step the SAME proposal is also judged with the literal arithmetic (literal ll of the current
+ * and proposed points, glibc log of the same uniform).  flips[c] counts the steps whose accept
+ * decision differs; max_rel_ll = max over all proposals of |ll_literal - ll_canonical| / |ll|;
+ * min_margin = the smallest |log u - ratio| seen (how close any decision came to a flip). */
+int or_mh_literal_shadow(const or_model* m, uint64_t seed, int64_t N, uint64_t step0, int64_t nsteps,
+                         const double* x, const double* ll, const double* lp, int64_t* flips,
+                         double* max_rel_ll, double* min_margin) {
+  prep_t p;
+  if (prep_model(m, &p) != 0 || g_literal) return -1;
+  const int D = p.D;
+  if (!(p.lik == MCG_LIK_DIAG_GAUSS || p.lik == MCG_LIK_GAUSS_SHELL) || D > 256) { prep_free(&p); return -1; }
+  step_probe* pr = (step_probe*)malloc(sizeof(step_probe));
+  double mrel = 0.0, mmar = INFINITY;
+  for (int64_t i = 0; i < N; ++i) {
+    chain_t c;
+    for (int d = 0; d < D; ++d) c.x[d] = x[(int64_t)d * N + i];
+    c.ll = ll[i]; c.lp = lp[i]; c.lq = 0.0;
+    int64_t f = 0;
+    for (int64_t t = 0; t < nsteps; ++t) {
+      const double llx_lit = lik_literal(&p, c.x), lpx = c.lp;
+      mh_step(&p, seed, (uint32_t)i, step0 + (uint64_t)t, &c, pr);
+      const double lly_lit = lik_literal(&p, pr->y);
+      if (isfinite(pr->lly) && pr->lly != 0.0) {
+        const double rel = fabs(lly_lit - pr->lly) / fabs(pr->lly);
+        if (rel > mrel) mrel = rel;
+      }
+      const double ratio_lit = (lly_lit + pr->lpy) - (llx_lit + lpx);
+      const int acc_lit = log(pr->u) < ratio_lit;
+      f += acc_lit != pr->acc;
+      const double mar = fabs(or_log(pr->u) - pr->ratio);
+      if (mar < mmar) mmar = mar;
+    }
+    flips[i] = f;
+  }
+  free(pr);
+  prep_free(&p);
+  if (max_rel_ll) *max_rel_ll = mrel;
+  if (min_margin) *min_margin = mmar;
   return 0;
 }
 
@@ -781,7 +870,7 @@ static void* mh_worker(void* arg) {
     if (o->nbin == 0 && o->n_rec > 0) record_sample(j, i, 0, &c);
     uint64_t na = 0;
     for (int64_t t = 0; t < nsteps; ++t) {
-      int a = mh_step(p, j->seed, gid, j->step0 + (uint64_t)t, &c);
+      int a = mh_step(p, j->seed, gid, j->step0 + (uint64_t)t, &c, NULL);
       if (a < 0) { j->status = -1; return NULL; }
       na += (uint64_t)a;
       if (o->record_accept && j->bits && a)
@@ -1204,7 +1293,8 @@ int or_nested(const or_model* m, uint64_t seed, const or_nested_opts* o, double*
         double ml = (lly >= thr) ? prior_eval(&p, y) : -INFINITY;
         double ratio = (((ml + 0.0) - (cur_l + 0.0)) + 0.0) - 0.0;
         rng4(seed, wid, (uint32_t)s, CALL_ACCEPT, TAG_NEST_WALK, 0u, rw);
-        double lu = or_log(or_u53(rw[0], rw[1]));
+        double uw = or_u53(rw[0], rw[1]);
+        double lu = g_literal ? log(uw) : or_log(uw);
         if (lu < ratio) { for (int d = 0; d < D; ++d) cur[d] = y[d]; cur_l = ml; }
       }
       for (int d = 0; d < D; ++d) nx[w * D + d] = cur[d];
@@ -1226,7 +1316,11 @@ int or_nested(const or_model* m, uint64_t seed, const or_nested_opts* o, double*
       tv[j] = lll[sl] + log_dv;
     }
     if (status) break;
-    est = (k == 1) ? or_plse(est, tv[0]) : or_plse(est, tree_lse(tv, k));
+    if (g_literal) {                     /* log_sum_logs per retired point (nested.ml:138-141) */
+      for (int64_t j = 0; j < k; ++j) est = or_log_sum_logs(est, tv[j]);
+    } else {
+      est = (k == 1) ? or_plse(est, tv[0]) : or_plse(est, tree_lse(tv, k));
+    }
     log_vol = log_vol + prefix[k];
     /* replace the retired slots (slot semantics of nested.ml:26-43) */
     for (int64_t j = 0; j < k; ++j) {
@@ -1249,7 +1343,8 @@ int or_nested(const or_model* m, uint64_t seed, const or_nested_opts* o, double*
     mrep += k; ++gen;
     /* remaining_integral_negligable (nested.ml:45-48) on the replaced live set */
     double live_est = log_vol + keys[n - 1].ll;
-    if (live_est - or_plse(est, live_est) <= log(o->epsrel)) break;
+    const double tot = g_literal ? or_log_sum_logs(est, live_est) : or_plse(est, live_est);
+    if (live_est - tot <= log(o->epsrel)) break;
     if (ndead >= max_iter) break;
   }
   int64_t ntot = ndead + n;

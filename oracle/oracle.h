@@ -110,6 +110,14 @@ int or_mh_run(const or_model* m, uint64_t seed, uint32_t chain_offset, int64_t N
               double* rec_x, double* rec_ll, double* rec_lp, uint64_t* accept_bits,
               or_accum* acc, int nthreads);
 
+/* The reference's literal arithmetic instead of the GPU's canonical one (oracle.c):
+   process-wide switch; or_mh_literal_shadow judges every canonical step's proposal both ways. */
+void or_set_literal(int on);
+int or_get_literal(void);
+int or_mh_literal_shadow(const or_model* m, uint64_t seed, int64_t N, uint64_t step0, int64_t nsteps,
+                         const double* x, const double* ll, const double* lp, int64_t* flips,
+                         double* max_rel_ll, double* min_margin);
+
 /* Tile reduction of the accumulators: 256-chain tiles, fixed pairwise tree.
    out per tile: [n, mean[D], m2[D], hm_m, hm_s] (2D+3 doubles). */
 void or_tile_stats(int D, int64_t N, int64_t nrec, const or_accum* acc, double* tiles);

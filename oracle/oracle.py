@@ -69,6 +69,10 @@ def lib():
         L.or_normal.argtypes = [C.c_uint32]
         L.or_normal.restype = C.c_double
         L.or_step_normals.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, C.c_int, _dp]
+        L.or_set_literal.argtypes = [C.c_int]
+        L.or_get_literal.restype = C.c_int
+        L.or_mh_literal_shadow.argtypes = [C.POINTER(OrModel), C.c_uint64, C.c_int64, C.c_uint64, C.c_int64,
+                                           _dp, _dp, _dp, C.POINTER(C.c_int64), _dp, _dp]
         L.or_wrap_uniform.argtypes = [C.c_double] * 5
         L.or_wrap_uniform.restype = C.c_double
         L.or_log_sum_logs.argtypes = [C.c_double, C.c_double]

@@ -3,7 +3,7 @@
 # a crash / timeout (exit >= 2 from pytest, or any signal) stops the script.
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-timeout -k 10 900 python -m pytest tests -q -m gpu -rf > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -v -s -m gpu -rf --timeout 150 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc" | tee -a gpurun_out/status.log
 if [ $rc -ge 2 ]; then exit $rc; fi

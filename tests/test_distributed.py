@@ -4,6 +4,7 @@ oracle stands in for the GPU here), the tile partials are all-gathered with torc
 combined by libmcg's host combine -- the result must be bit-identical to one rank holding every
 chain."""
 import math
+import sys
 import os
 
 import numpy as np
@@ -90,3 +91,18 @@ def test_replica_sizes_keep_k_below_nlive():
         replica_sizes(100, 1, 3)          # not a multiple of the rank count
     with pytest.raises(ValueError):
         replica_sizes(4, 1, 4)            # one live point per replica
+
+
+def test_c5_start_points_do_not_depend_on_sharding():
+    """scripts/bench_c5.py: a chain's start point is a function of its global id, so any split of
+    the global chains over ranks starts the same chains at the same points (the premise of the
+    rank-count invariance the GPU test checks)."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import bench_c5 as b
+    mu, cov, _ = b.c5_target()
+    assert np.all(np.linalg.eigvalsh(cov) > 0)
+    whole = b.start_points(mu, cov, 0, 4 * 8192 + 512)
+    for world in (2, 4, 8):
+        n = whole.shape[1] // world
+        parts = [b.start_points(mu, cov, r * n, n) for r in range(world)]
+        np.testing.assert_array_equal(np.concatenate(parts, axis=1), whole[:, :n * world])
