@@ -101,6 +101,28 @@ def pmc_traffic(D, N, S):
     return t["traffic_bytes"]
 
 
+def pmc_valu(D, N, S, avg_launch_ms):
+    """VALU-issue framing of the dominant kernel (the bound that actually holds for the fused C2
+    step: its HBM traffic is < 1 % of the algorithmic bytes) from the committed PMC pass
+    (profiles/pmc_valu.json, scripts/pmc_valu.py): 4 SIMD cycles per wave64 VALU instruction over
+    1,024 SIMDs, against the 2.4 GHz peak clock for this launch's live duration, and at the clock
+    the chip held during the PMC pass (GRBM_GUI_ACTIVE)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_valu.json")) as fh:
+            v = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    if v.get("config") != {"ndim": D, "chains_per_gpu": N, "sweeps_per_step": S}:
+        return None
+    issue = 4.0 * v["valu_insts_per_launch"] / 1024.0        # SIMD cycles per SIMD
+    return {"bound": "valu", "unit": "VALU issue cycles / SIMD cycles",
+            "insts_per_launch": v["valu_insts_per_launch"],
+            "insts_per_chain_step": v["valu_insts_per_chain_step"],
+            "frac": issue / (2.4e9 * avg_launch_ms * 1e-3), "clock_ghz": 2.4,
+            "frac_at_held_clock": v["valu_busy_frac_at_held_clock"],
+            "source": "profiles/pmc_valu.json (rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -254,7 +276,8 @@ def main():
                      "algorithmic_bytes_per_launch": launch_steps * bytes_per_step,
                      "kernel": "mcg::mh_kernel<32,P,DIAG_GAUSS,GAUSS>",
                      "bytes_per_step": bytes_per_step, "avg_launch_ms": per_launch,
-                     "launches": timing["launches"]},
+                     "launches": timing["launches"],
+                     "valu": pmc_valu(D, N, S, per_launch)},
         "cpu_baseline": cpu,
         "accept_frac": acc / max(acc + rej, 1),
         "log_evidence": log_evidence_line(nest, log_z_hm, lz_true),

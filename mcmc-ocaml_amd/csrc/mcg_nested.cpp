@@ -49,6 +49,11 @@ struct KeyBuf {
 struct NestedBufs {
   DevBuf x, ll, lp, nx, nll, nlp, tv, prefix, qadd, st, dead_x, dead_ll, dead_lp, rank, sync, trace, chk, rt_ix, rt_sc;
   KeyBuf keys[2], newk, newk_tmp;
+  // pipelined merges (a.pipe): the k lowest keys the walk reads, the second sorted-new-keys
+  // buffer, the merge stream and the per-generation hand-off events between the two streams
+  KeyBuf head, newk_tmp2;
+  hipStream_t s2 = nullptr;
+  hipEvent_t ev_sorted[2] = {nullptr, nullptr}, ev_full[2] = {nullptr, nullptr};
   int64_t dead_cap = 0;
   // pinned staging of two in-flight batches' dead (ll, lp) and their completion events
   double* h_stage[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -70,6 +75,14 @@ struct NestedBufs {
     if (h_st) (void)hipHostFree(h_st);
     for (auto e : done)
       if (e) (void)hipEventDestroy(e);
+    for (auto e : ev_sorted)
+      if (e) (void)hipEventDestroy(e);
+    for (auto e : ev_full)
+      if (e) (void)hipEventDestroy(e);
+    if (s2) {
+      (void)hipStreamSynchronize(s2);
+      (void)hipStreamDestroy(s2);
+    }
   }
 };
 
@@ -284,7 +297,7 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   }
   HC(hipMemcpyAsync(B.prefix.p, prefix.data(), (k + 1) * 8, hipMemcpyHostToDevice, s), "copy prefix");
   HC(hipMemcpyAsync(B.qadd.p, qadd.data(), k * 8, hipMemcpyHostToDevice, s), "copy qadd");
-  NestDevState st0{0.0, -HUGE_VAL, 0, 0, 0};
+  NestDevState st0{0.0, -HUGE_VAL, 0, 0, 0, -HUGE_VAL, INT64_MAX};
   HC(hipMemcpyAsync(B.st.p, &st0, sizeof st0, hipMemcpyHostToDevice, s), "copy state");
 
   NestArgs a{};
@@ -316,6 +329,16 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   if (const char* e = std::getenv("MCG_NEST_LANES"))
     a.lanes_hint = !std::strcmp(e, "wide") ? -1 : !std::strcmp(e, "narrow") ? -2 : std::atoi(e);
   a.fuse_retire = a.est_in_rank && std::getenv("MCG_NESTED_RETIRE_KERNEL") == nullptr;
+  // pipelined merges: the full n-key merge of generation g runs on a second
+  // stream beside walk g + 1, which reads only the k lowest keys (a 2k-key head merge)
+  a.pipe = a.fuse_retire && std::getenv("MCG_NESTED_NO_PIPE") == nullptr ? 1 : 0;
+  if (a.pipe) {
+    HC(B.head.ensure(k), "alloc head keys");
+    HC(B.newk_tmp2.ensure(k), "alloc new keys");
+    if (!B.s2) HC(hipStreamCreateWithFlags(&B.s2, hipStreamNonBlocking), "merge stream");
+    for (auto* e : {&B.ev_sorted[0], &B.ev_sorted[1], &B.ev_full[0], &B.ev_full[1]})
+      if (!*e) HC(hipEventCreateWithFlags(e, hipEventDisableTiming), "create event");
+  }
   // the walkers' draws of a generation in a table the previous merge fills (when it fits)
   a.rt_ix = nullptr;
   a.rt_sc = nullptr;
@@ -360,8 +383,13 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   HC(launch_sort_keys(B.keys[0].l(), B.keys[0].t(), B.keys[0].s(), B.keys[1].l(), B.keys[1].t(),
                       B.keys[1].s(), n, &in_tmp, s, nullptr), "sort live keys");
   const int base = in_tmp ? 1 : 0;                   // generation g reads keys[(base + g) % 2]
-  HC(launch_key_sample(B.keys[base].l(), B.keys[base].t(), n, B.keys[base].sl(), B.keys[base].st(), s),
+  HC(launch_key_sample(B.keys[base].l(), B.keys[base].t(), n, B.keys[base].sl(), B.keys[base].st(), s, a.st),
      "sample live keys");
+  if (a.pipe) {                                      // the first walk's head keys: keys[0, k)
+    HC(hipMemcpyAsync(B.head.l(), B.keys[base].l(), k * 8, hipMemcpyDeviceToDevice, s), "head keys");
+    HC(hipMemcpyAsync(B.head.t(), B.keys[base].t(), k * 8, hipMemcpyDeviceToDevice, s), "head keys");
+    HC(hipMemcpyAsync(B.head.s(), B.keys[base].s(), k * 4, hipMemcpyDeviceToDevice, s), "head keys");
+  }
   HC(launch_walk_draws(a, 0, s), "first draws");
 
   // Batches of generations, pipelined: while the GPU runs batch b + 1, the host appends batch b's
@@ -438,6 +466,32 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
 #ifdef MCG_NEST_TRACE
       a.trace = (g == trace_gen) ? (unsigned long long*)B.trace.p : nullptr;
 #endif
+      if (a.pipe) {
+        // generation g: walk (reads the head keys) -> sort the new keys -> [merge stream: full
+        // merge of keys g-1 with them] -> head merge of keys g-1 [k, 2k) with them (waits for the
+        // full merge of generation g-1, which ran beside this walk)
+        NestArgs aw = a;
+        aw.key_ll = B.head.l();
+        aw.key_tie = B.head.t();
+        aw.key_slot = B.head.s();
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (ctx->timing) timing_begin(ctx, &e0, &e1);
+        HC(walk(aw, s), "nested walk");
+        if (ctx->timing) timing_end(ctx, e0, e1, 1);
+        KeyBuf& nk = (g & 1) ? B.newk_tmp2 : B.newk_tmp;
+        HC(launch_sort_new_small(a, nk.l(), nk.t(), nk.s(), s), "sort new keys");
+        if (check) HC(launch_check_sorted(nk.l(), nk.t(), k, g, (long long*)B.chk.p, s), "check");
+        HC(hipEventRecord(B.ev_sorted[g & 1], s), "record sorted");
+        HC(hipStreamWaitEvent(B.s2, B.ev_sorted[g & 1], 0), "merge stream wait");
+        HC(launch_merge_new(a, nxt.l(), nxt.t(), nxt.s(), nk.l(), nk.t(), nk.s(), B.s2), "merge keys");
+        if (check) HC(launch_check_sorted(nxt.l(), nxt.t(), n, g, (long long*)B.chk.p + 1, B.s2), "check");
+        HC(hipEventRecord(B.ev_full[g & 1], B.s2), "record merged");
+        if (g > 0) HC(hipStreamWaitEvent(s, B.ev_full[(g - 1) & 1], 0), "head wait");
+        const int64_t ns = std::min<int64_t>(k, n - k);
+        HC(launch_head_merge(a, cur.l() + k, cur.t() + k, cur.s() + k, ns, nk.l(), nk.t(), nk.s(), B.head.l(),
+                             B.head.t(), B.head.s(), s), "head merge");
+        continue;
+      }
       hipEvent_t e0 = nullptr, e1 = nullptr;
       if (ctx->timing) timing_begin(ctx, &e0, &e1);
       HC(walk(a, s), "nested walk");
@@ -456,6 +510,8 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
       HC(launch_merge_new(a, nxt.l(), nxt.t(), nxt.s(), nk.l(), nk.t(), nk.s(), s), "merge keys");
       if (check) HC(launch_check_sorted(nxt.l(), nxt.t(), n, g, (long long*)B.chk.p + 1, s), "check");
     }
+    // the batch's last full merge (merge stream) before its state is read
+    if (a.pipe && G > 0) HC(hipStreamWaitEvent(s, B.ev_full[(gen + G - 1) & 1], 0), "batch merge wait");
     HC(hipMemcpyAsync(&hst[q], B.st.p, sizeof(NestDevState), hipMemcpyDeviceToHost, s), "read state");
     HC(hipMemcpyAsync(B.h_stage[2 * q], (double*)B.dead_ll.p + gen * k, G * k * 8, hipMemcpyDeviceToHost, s),
        "stage dead ll");

@@ -23,6 +23,8 @@ struct NestDevState {
   int32_t stopped;
   int32_t error;
   long long gen_done;
+  double max_ll;            // the largest live ll (the sorted keys' last): the stop test's L_max
+  long long stop_gen;       // the last generation of a stopped run (pipelined merges; else max)
 };
 
 // The stop / error flags and the generation count are read and written with agent-scope atomics
@@ -77,6 +79,9 @@ struct NestArgs {
                             // put the new points into the freed slots
   int32_t sym_box;          // box prior with lo[d] == -hi[d] for every d: tested as |y| <= hi
   int32_t lanes_hint;       // lanes per walker requested by MCG_NEST_LANES (0: the default)
+  int32_t pipe;             // pipelined key merges: the walk reads the head keys
+                            // (the k lowest), the full merge runs on a second stream beside the
+                            // next walk and skips generations past st->stop_gen only
   uint32_t row_bytes;       // D * 8: the draw table holds DE pairs as row byte offsets
   double* tv;               // ll + log dv of this generation's dead points (padded pow2)
   const double* prefix;     // [k+1] sum_{j'<j} log1p(-1/(n-j'))
@@ -383,10 +388,15 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
     // max live ll; or a failed draw, nested.ml:70-72), made by every workgroup from the same
     // inputs: a flag set inside a kernel could be seen by only some of its workgroups (a late
     // starter would skip its share of the work), so no kernel reads the flag it may set
-    const double live = a.st->log_vol + a.key_ll[a.n - 1];
+    const double live = a.st->log_vol + a.st->max_ll;
     const bool err = __hip_atomic_load(&a.st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
     if (live - plse(a.st->est, live, s_lt) <= a.log_epsrel || err) {
-      if (blockIdx.x == 0 && threadIdx.x == 0) nest_set(&a.st->stopped);
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        // the previous generation was the last: its pipelined full merge (still running on the
+        // merge stream) completes; the ones after it skip
+        __hip_atomic_store(&a.st->stop_gen, (long long)(a.mrep / a.k) - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        nest_set(&a.st->stopped);
+      }
       return;
     }
   }
@@ -785,7 +795,11 @@ hipError_t launch_check_sorted(const double* ll, const long long* tie, int64_t n
 hipError_t launch_retire(const NestArgs& a, int D, hipStream_t st);
 // every kKeySample-th of n sorted keys (indices kKeySample-1, 2 kKeySample-1, ...) into s*
 hipError_t launch_key_sample(const double* ll, const long long* tie, int64_t n, double* sll,
-                             long long* stie, hipStream_t st);
+                             long long* stie, hipStream_t st, NestDevState* state = nullptr);
+// pipelined merges: the k lowest of survivors[0, ns) (ns <= k) and the k sorted new keys into h*
+hipError_t launch_head_merge(const NestArgs& a, const double* sl, const long long* st, const int* ss, int64_t ns,
+                             const double* nl, const long long* nt, const int* nsl, double* hl, long long* ht,
+                             int* hs, hipStream_t s);
 // k <= 4096: new keys sorted into o* by counting ranks (a.rank zeroed by the retire kernel)
 hipError_t launch_sort_new_small(const NestArgs& a, double* oll, long long* otie, int* oslot,
                                  hipStream_t st);

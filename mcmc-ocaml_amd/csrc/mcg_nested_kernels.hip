@@ -355,6 +355,9 @@ __global__ void __launch_bounds__(256) rank_count_kernel(const NestArgs a, int n
       oslot[r] = sl_[e];
     }
   }
+  // pipelined merges: the next walk's L_max is the largest live ll = max(the survivors' largest,
+  // which is the previous L_max, and the largest new key) -- the merged keys' last entry
+  if (a.pipe && t == 0) a.st->max_ll = fmax(a.st->max_ll, s_ll[k - 1]);
   NT_STAMP(2, 5);
   slot_writes();
 }
@@ -483,7 +486,12 @@ __global__ void __launch_bounds__(256) merge_new_kernel(const NestArgs a, double
     kv_use = ku;
   }
   __syncthreads();
-  if (nest_stopped(a.st)) return;
+  // pipelined (a.pipe): this merge runs beside the next generation's walk, which may find the
+  // run finished and set the stop flag; the merge of the last generation must still complete,
+  // so it tests the generation against st->stop_gen instead
+  if (a.pipe ? (a.mrep / a.k > __hip_atomic_load(&a.st->stop_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+             : nest_stopped(a.st))
+    return;
   NT_STAMP(3, 1);
   if (e >= n) return;
   int64_t pos;
@@ -497,23 +505,84 @@ __global__ void __launch_bounds__(256) merge_new_kernel(const NestArgs a, double
     a.out_samp_ll[pos / kKeySample] = kl;
     a.out_samp_tie[pos / kKeySample] = kt;
   }
-  if (pos == n - 1) __hip_atomic_fetch_add(&a.st->gen_done, 1LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (pos == n - 1) {
+    if (!a.pipe) a.st->max_ll = kl;                  // (pipelined: the rank count keeps it)
+    __hip_atomic_fetch_add(&a.st->gen_done, 1LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   NT_STAMP(3, 3);
 }
 
 __global__ void __launch_bounds__(256) key_sample_kernel(const double* ll, const long long* tie,
-                                                         int64_t n, double* sll, long long* stie) {
+                                                         int64_t n, double* sll, long long* stie,
+                                                         NestDevState* st) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && st) st->max_ll = ll[n - 1];          // the initial live set's L_max
   if (c >= n / kKeySample) return;
   sll[c] = ll[(c + 1) * kKeySample - 1];
   stie[c] = tie[(c + 1) * kKeySample - 1];
 }
 
 hipError_t launch_key_sample(const double* ll, const long long* tie, int64_t n, double* sll,
-                             long long* stie, hipStream_t s) {
+                             long long* stie, hipStream_t s, NestDevState* st) {
   const int64_t ns = n / kKeySample;
-  if (ns == 0) return hipSuccess;
-  hipLaunchKernelGGL(key_sample_kernel, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, s, ll, tie, n, sll, stie);
+  hipLaunchKernelGGL(key_sample_kernel, dim3((unsigned)(ns / 256 + 1)), dim3(256), 0, s, ll, tie, n, sll, stie, st);
+  return hipGetLastError();
+}
+
+// Pipelined merges: generation g + 1 needs only the k lowest live keys (its
+// threshold, its retirees and their order), which are the k lowest of survivors[k, 2k) of the
+// previous full key array and the k sorted new keys.  Workgroup b takes 256 keys of one of the two
+// arrays, stages the other whole array (<= 4096 keys, 64 KB) in LDS and places each key at
+// own index + (keys of the other array below it), when that is below k.  Keys are unique, so the
+// two counts never collide.
+__global__ void __launch_bounds__(256) head_merge_kernel(const NestArgs a, const double* sl_, const long long* st_,
+                                                         const int* ss_, int64_t ns, const double* nl,
+                                                         const long long* nt, const int* nsl, double* hl,
+                                                         long long* ht, int* hs) {
+  __shared__ double o_l[kSmallSort];
+  __shared__ long long o_t[kSmallSort];
+  if (nest_stopped(a.st)) return;
+  const int64_t k = a.k;
+  const int nbs = (int)((ns + 255) / 256);
+  const bool from_surv = (int)blockIdx.x < nbs;       // block-uniform
+  const int64_t i = (int64_t)(from_surv ? blockIdx.x : blockIdx.x - nbs) * 256 + threadIdx.x;
+  const int64_t len_own = from_surv ? ns : k, len_oth = from_surv ? k : ns;
+  const double* ol = from_surv ? nl : sl_;
+  const long long* ot = from_surv ? nt : st_;
+  for (int64_t q = threadIdx.x; q < len_oth; q += 256) {
+    o_l[q] = ol[q];
+    o_t[q] = ot[q];
+  }
+  double kl = 0.0;
+  long long kt = 0;
+  int ks = 0;
+  if (i < len_own) {
+    kl = from_surv ? sl_[i] : nl[i];
+    kt = from_surv ? st_[i] : nt[i];
+    ks = from_surv ? ss_[i] : nsl[i];
+  }
+  __syncthreads();
+  if (i >= len_own) return;
+  int lo = 0, hi = (int)len_oth;
+  while (lo < hi) {
+    const int m = (lo + hi) >> 1;
+    if (key_less(o_l[m], o_t[m], kl, kt)) lo = m + 1;
+    else hi = m;
+  }
+  const int64_t pos = i + lo;
+  if (pos < k) {
+    hl[pos] = kl;
+    ht[pos] = kt;
+    hs[pos] = ks;
+  }
+}
+
+hipError_t launch_head_merge(const NestArgs& a, const double* sl, const long long* st, const int* ss, int64_t ns,
+                             const double* nl, const long long* nt, const int* nsl, double* hl, long long* ht,
+                             int* hs, hipStream_t s) {
+  if (a.k > kSmallSort || a.k < 1 || ns > kSmallSort) return hipErrorInvalidValue;
+  const unsigned grid = (unsigned)((ns + 255) / 256 + (a.k + 255) / 256);
+  hipLaunchKernelGGL(head_merge_kernel, dim3(grid), dim3(256), 0, s, a, sl, st, ss, ns, nl, nt, nsl, hl, ht, hs);
   return hipGetLastError();
 }
 

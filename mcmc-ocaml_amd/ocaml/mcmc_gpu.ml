@@ -67,6 +67,12 @@ let c_stats = fn "mcg_stats" (ptr void @-> ptr double @-> ptr double @-> ptr dou
 let c_nested = fn "mcg_nested" (ptr void @-> ptr nested_opts @-> ptr nested_result @-> ptr void @-> ptr void @-> returning int)
 let c_nested_get = fn "mcg_nested_get" (ptr void @-> ptr double @-> ptr double @-> ptr double @-> ptr double @-> returning int)
 let c_log_total_error = fn "mcg_log_total_error_estimate" (double @-> double @-> int64_t @-> returning double)
+let c_set_de = fn "mcg_set_de_proposal" (ptr void @-> ptr double @-> int64_t @-> double @-> returning int)
+let c_get_state = fn "mcg_get_state" (ptr void @-> ptr double @-> ptr double @-> ptr double @-> returning int)
+let c_posterior = fn "mcg_posterior_samples" (ptr void @-> ptr double @-> int64_t @-> int64_t @-> ptr int64_t @-> returning int)
+(* mcg_observer_fn: void (void* user, const double* pts, const double* ll, const double* lp, int64_t n) *)
+let observer_t = ptr void @-> ptr double @-> ptr double @-> ptr double @-> int64_t @-> returning void
+let c_nested_obs = fn "mcg_nested" (ptr void @-> ptr nested_opts @-> ptr nested_result @-> funptr observer_t @-> ptr void @-> returning int)
 
 (* status codes -> the reference's exceptions (kd_tree.ml:70,97; nested.ml:71) *)
 let check ctx rc =
@@ -102,6 +108,9 @@ type proposal =
   | Uniform_wrapping of float array * float array * float array
   | Interp of float array array * float array * float array
   | Mixture of (float * mix_component * bool) list * (float array array * float array * float array) option
+  | De of float array array * float
+
+let differential_evolution_proposal ?(mode_hopping_frac = 0.0) samples = De (samples, mode_hopping_frac)
 
 let dims = Hashtbl.create 8
 
@@ -163,6 +172,28 @@ let set_model ctx lik pri prop =
       | Mix_interp -> [| p; 4.0; 1.0 |] in
     let params = Array.concat ([| float (List.length comps) |] :: List.map comp comps) in
     check ctx (c_set_proposal ctx 5l (carr params) (Unsigned.Size_t.of_int (Array.length params)))
+  | Some (De (samples, mh)) ->
+    (* Mcmc.differential_evolution_proposal (mcmc.ml:198-218): samples kept in HBM *)
+    check ctx (c_set_de ctx (carr (flatten samples)) (Int64.of_int (Array.length samples)) mh)
+
+type state = mat * vec * vec
+
+(* Mcmc.make_mcmc_sampler (mcmc.ml:37-56) over a batch of chains: one MH step per call *)
+let make_mcmc_sampler ctx lik pri prop =
+  set_model ctx lik pri (Some prop);
+  fun ((x : mat), (ll : vec), (lp : vec)) ->
+    let d = Bigarray.Array2.dim1 x and nch = Bigarray.Array2.dim2 x in
+    check ctx (c_init ctx (Int64.of_int nch) (bigarray_start array2 x) (bigarray_start array1 ll)
+                 (bigarray_start array1 lp));
+    let o = make run_opts in
+    setf o r_nbin 1L; setf o r_nskip 1L; setf o r_nrec 0L;
+    setf o r_rx 0l; setf o r_rllp 0l; setf o r_racc 0l; setf o r_accum 0l; setf o r_append 0l;
+    check ctx (c_run ctx (addr o));
+    let open Bigarray in
+    let x' = Array2.create float64 c_layout d nch in
+    let ll' = Array1.create float64 c_layout nch and lp' = Array1.create float64 c_layout nch in
+    check ctx (c_get_state ctx (bigarray_start array2 x') (bigarray_start array1 ll') (bigarray_start array1 lp'));
+    (x', ll', lp')
 
 let reset_counters ctx = check ctx (c_reset_counters ctx)
 
@@ -197,14 +228,22 @@ let stats ctx =
   check ctx (c_stats ctx (CArray.start m) (CArray.start s) z);
   (Array.of_list (CArray.to_list m), Array.of_list (CArray.to_list s), !@z)
 
-let nested_evidence ?(epsrel = 0.01) ?(nmcmc = 1000) ?(nlive = 1000) ?(mode_hopping_frac = 0.1)
+let nested_run ?observer ?(epsrel = 0.01) ?(nmcmc = 1000) ?(nlive = 1000) ?(mode_hopping_frac = 0.1)
     ?(k = 1) ctx =
   let d = Hashtbl.find dims ctx in
   let o = make nested_opts in
   setf o n_nlive (Int64.of_int nlive); setf o n_nmcmc (Int64.of_int nmcmc); setf o n_k (Int64.of_int k);
   setf o n_epsrel epsrel; setf o n_mode_hop mode_hopping_frac; setf o n_max_dead 0L;
   let r = make nested_result in
-  check ctx (c_nested ctx (addr o) (addr r) null null);
+  (match observer with
+   | None -> check ctx (c_nested ctx (addr o) (addr r) null null)
+   | Some f ->
+     (* the per-point ?observer of nested.ml:136, fed from libmcg's per-generation batches *)
+     let cb _ pts ll lp n =
+       for i = 0 to Int64.to_int n - 1 do
+         f (Array.init d (fun j -> !@(pts +@ (i * d + j))), !@(ll +@ i), !@(lp +@ i))
+       done in
+     check ctx (c_nested_obs ctx (addr o) (addr r) cb null));
   if getf r nr_converged = 0l then
     prerr_endline "Mcmc_gpu.nested_evidence: max_dead cap reached before the stop test (unconverged)";
   let n = Int64.to_int (getf r nr_n_total) in
@@ -212,10 +251,23 @@ let nested_evidence ?(epsrel = 0.01) ?(nmcmc = 1000) ?(nlive = 1000) ?(mode_hopp
   and lp = CArray.make double n and w = CArray.make double n in
   check ctx (c_nested_get ctx (CArray.start pts) (CArray.start ll) (CArray.start lp) (CArray.start w));
   let pts = Array.init n (fun i -> Array.init d (fun j -> CArray.get pts (i * d + j))) in
-  (getf r nr_log_ev, getf r nr_log_dev, pts, Array.of_list (CArray.to_list w))
+  ((getf r nr_log_ev, getf r nr_log_dev, pts, Array.of_list (CArray.to_list w)),
+   Array.of_list (CArray.to_list ll), Array.of_list (CArray.to_list lp))
+
+let nested_evidence ?observer ?epsrel ?nmcmc ?nlive ?mode_hopping_frac ?k ctx =
+  let (out, _, _) = nested_run ?observer ?epsrel ?nmcmc ?nlive ?mode_hopping_frac ?k ctx in
+  out
 
 let log_total_error_estimate log_ev log_dev nlive =
   c_log_total_error log_ev log_dev (Int64.of_int nlive)
+
+(* Nested.posterior_samples (nested.ml:152-178): the draws on the device, the points picked here *)
+let posterior_samples ctx n (_, _, (pts : float array array), (log_wts : float array)) =
+  let npts = Array.length log_wts in
+  assert (Array.length pts = npts);
+  let idx = CArray.make int64_t (max n 1) in
+  check ctx (c_posterior ctx (carr log_wts) (Int64.of_int npts) (Int64.of_int n) (CArray.start idx));
+  Array.init n (fun i -> pts.(Int64.to_int (CArray.get idx i)))
 
 (* ---- reversible jump (Mcmc.rjmcmc_array, mcmc.ml:118-132) ---- *)
 type rj_jump =

@@ -48,8 +48,22 @@ type proposal =
   (** combine_jump_proposals [(p, jump, density?)]: [density] = the component's log_jump_prob is
       its log density (else the constant 0 of a symmetric jump); the optional kD tree serves
       Mix_interp *)
+  | De of float array array * float
+  (** differential_evolution_proposal: the samples (M >= 2 rows of D), mode_hopping_frac *)
 
 val set_model : ctx -> likelihood -> prior -> proposal option -> unit
+
+(** Mcmc.differential_evolution_proposal ?mode_hopping_frac to_float from_float samples
+    (mcmc.mli:215-218) over the samples' coordinates (log_jump_prob 0). *)
+val differential_evolution_proposal : ?mode_hopping_frac:float -> float array array -> proposal
+
+type state = mat * vec * vec
+(** a batch of mcmc_sample records (mcmc.mli:33-42): values D x N, log-likelihoods, log-priors *)
+
+(** Mcmc.make_mcmc_sampler (mcmc.mli:58-60) over a batch: sets the model on [ctx] and returns the
+    step function; each call advances every chain of the state by one MH step (a rejected chain
+    keeps its state, mcmc.ml:55) and continues the context's Philox stream. *)
+val make_mcmc_sampler : ctx -> likelihood -> prior -> proposal -> (state -> state)
 
 (** Mcmc.reset_counters / get_counters (mcmc.mli:29-30) for this context. *)
 val reset_counters : ctx -> unit
@@ -73,8 +87,22 @@ val stats : ctx -> float array * float array * float
     [k] live points retired per generation (1 = the reference algorithm).  Returns the
     nested_output tuple: log Z, log dZ, points (n x D), log weights. *)
 val nested_evidence :
+  ?observer:(float array * float * float -> unit) ->
   ?epsrel:float -> ?nmcmc:int -> ?nlive:int -> ?mode_hopping_frac:float -> ?k:int -> ctx ->
   float * float * float array array * float array
+(** [observer] (nested.mli:50) sees every retired point (value, log_likelihood, log_prior), in
+    retirement order, after each generation of [k] retirements. *)
+
+(** [nested_evidence] plus the log_likelihood and log_prior of every returned point (the
+    like_prior halves of the reference's sample records). *)
+val nested_run :
+  ?observer:(float array * float * float -> unit) ->
+  ?epsrel:float -> ?nmcmc:int -> ?nlive:int -> ?mode_hopping_frac:float -> ?k:int -> ctx ->
+  (float * float * float array array * float array) * float array * float array
+
+(** Nested.posterior_samples n output (nested.mli:77): n points drawn by weight on the device from
+    the context's Philox stream (include/mcg.h mcg_posterior_samples). *)
+val posterior_samples : ctx -> int -> float * float * float array array * float array -> float array array
 
 (** Nested.log_total_error_estimate (nested.mli:69). *)
 val log_total_error_estimate : float -> float -> int -> float

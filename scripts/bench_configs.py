@@ -169,6 +169,9 @@ def c4(args):
     line = {"config": "C4 kD interp proposal D=8, M=%d, %d chains, %d sweeps" % (M, N, K * S),
             "unit": "MH steps/s", "dtype": "f64", "value": N * S * K / dt,
             "accept_frac": acc / (acc + rej),
+            # the independence proposal from a 32,768-point tree accepts ~0.1 % of its draws: the
+            # rate of accepted moves is the figure to compare across proposals
+            "accepted_steps_per_s": N * S * K / dt * acc / (acc + rej),
             "posterior_check": {"max_abs_mean_err": float(np.max(np.abs(mean))),
                                 "max_rel_sd_err": float(np.max(np.abs(sd - 1)))},
             "log_z_harmonic_mean": lz, "log_z_analytic": -D * math.log(20.0),

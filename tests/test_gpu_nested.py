@@ -230,18 +230,34 @@ def test_nested_walker_box_forms_bit_exact(oracle, T, D, sym, diag):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", ["MCG_NESTED_NO_TABLE", "MCG_NESTED_RETIRE_KERNEL", "both"])
+@pytest.mark.parametrize("env", ["MCG_NESTED_NO_TABLE", "MCG_NESTED_RETIRE_KERNEL", "both", "MCG_NESTED_NO_PIPE"])
 @pytest.mark.parametrize("D", [3, 16])
 def test_nested_alternate_paths_bit_exact(oracle, T, monkeypatch, env, D):
     """The paths the default run does not take: walkers drawing their own random numbers (no
-    draw table: what a generation too big for the table uses) and the separate retire kernel
-    (k > 4096 uses it) -- the same dead points as the oracle, bit for bit."""
+    draw table: what a generation too big for the table uses), the separate retire kernel
+    (k > 4096 uses it) and the serial full merge instead of the pipelined head + full merges --
+    the same dead points as the oracle, bit for bit."""
     for var in (["MCG_NESTED_NO_TABLE", "MCG_NESTED_RETIRE_KERNEL"] if env == "both" else [env]):
         monkeypatch.setenv(var, "1")
     lik = T.gauss_shell(np.zeros(D), 1.0, 0.2)
     pri = T.box(-2 * np.ones(D), 2 * np.ones(D))
     g = gpu_nested(lik, pri, 14, nlive=300, nmcmc=15, mode_hopping_frac=0.1, k=30, max_dead=30 * 30)
     o = oracle_nested(oracle, lik, pri, 14, nlive=300, nmcmc=15, mode_hop=0.1, k=30, max_iter=30 * 30)
+    assert_nested_same(g, o)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nlive,k", [(300, 200), (257, 256), (5000, 4096)])
+def test_nested_pipelined_head_merge_edges_bit_exact(oracle, T, nlive, k):
+    """Pipelined merges where the head merge sees fewer survivors than new keys
+    (k > nlive / 2), a single survivor (k = nlive - 1), and the largest counted-rank k, run to
+    convergence: dead points, stop generation, log Z and weights equal the oracle's."""
+    D = 4
+    lik = T.gauss_shell(np.zeros(D), 1.0, 0.2)
+    pri = T.box(-2 * np.ones(D), 2 * np.ones(D))
+    g = gpu_nested(lik, pri, 23, nlive=nlive, nmcmc=6, mode_hopping_frac=0.1, k=k)
+    o = oracle_nested(oracle, lik, pri, 23, nlive=nlive, nmcmc=6, mode_hop=0.1, k=k)
+    assert g.converged
     assert_nested_same(g, o)
 
 
