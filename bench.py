@@ -81,7 +81,7 @@ def cpu_baseline(args, mu, sg, s):
     s1 = max(20, int(3.0 * (n1 * 20 / d1) / n1))
     d1 = run(n1, s1, 1)
     return dict(value=nch * nsteps / dt, unit="MH steps/s", cores=threads, kind="port",
-                sample="%d chains x %d steps of the C2 target (oracle/oracle.c, -O2, %d threads)"
+                sample="%d chains x %d steps of the C2 target (oracle/oracle.c, -O3 -march=x86-64-v3, %d threads)"
                        % (nch, nsteps, threads),
                 single_core_value=n1 * s1 / d1,
                 single_core_sample="%d chains x %d steps, 1 thread" % (n1, s1))

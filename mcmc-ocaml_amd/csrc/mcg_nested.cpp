@@ -329,9 +329,11 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   if (const char* e = std::getenv("MCG_NEST_LANES"))
     a.lanes_hint = !std::strcmp(e, "wide") ? -1 : !std::strcmp(e, "narrow") ? -2 : std::atoi(e);
   a.fuse_retire = a.est_in_rank && std::getenv("MCG_NESTED_RETIRE_KERNEL") == nullptr;
-  // pipelined merges: the full n-key merge of generation g runs on a second
-  // stream beside walk g + 1, which reads only the k lowest keys (a 2k-key head merge)
-  a.pipe = a.fuse_retire && std::getenv("MCG_NESTED_NO_PIPE") == nullptr ? 1 : 0;
+  // pipelined merges (MCG_NESTED_PIPE=1): the full n-key merge of generation g
+  // runs on a second stream beside rank count g + 1 and the next walk reads only the k lowest
+  // keys (a 2k-key head merge).  Measured slower than the serial merge (the cross-stream event
+  // waits cost more per generation than the merge they hide), so it is not the default.
+  a.pipe = a.fuse_retire && std::getenv("MCG_NESTED_PIPE") != nullptr ? 1 : 0;
   if (a.pipe) {
     HC(B.head.ensure(k), "alloc head keys");
     HC(B.newk_tmp2.ensure(k), "alloc new keys");
@@ -428,6 +430,27 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
     HC(hipMemsetAsync(B.trace.p, 0, 4 * 1024 * 8 * 8, s), "clear trace");
   }
 #endif
+  // pipelined merges: full merge of generation gm on the merge stream after event `after`:
+  // keys gm-1 (all n) with the sorted new keys of gm into keys gm; event ev_full[gm & 1]
+  auto full_merge = [&](int64_t gm, hipEvent_t after) -> hipError_t {
+    hipError_t e;
+    KeyBuf& c = B.keys[(base + gm) % 2];
+    KeyBuf& x = B.keys[(base + gm + 1) % 2];
+    KeyBuf& nk = (gm & 1) ? B.newk_tmp2 : B.newk_tmp;
+    NestArgs am = a;
+    am.key_ll = c.l();
+    am.key_tie = c.t();
+    am.key_slot = c.s();
+    am.key_samp_ll = c.sl();
+    am.key_samp_tie = c.st();
+    am.out_samp_ll = x.sl();
+    am.out_samp_tie = x.st();
+    am.mrep = gm * k;
+    if ((e = hipStreamWaitEvent(B.s2, after, 0)) != hipSuccess) return e;
+    if ((e = launch_merge_new(am, x.l(), x.t(), x.s(), nk.l(), nk.t(), nk.s(), B.s2)) != hipSuccess) return e;
+    if (check && (e = launch_check_sorted(x.l(), x.t(), n, gm, (long long*)B.chk.p + 1, B.s2)) != hipSuccess) return e;
+    return hipEventRecord(B.ev_full[gm & 1], B.s2);
+  };
   // enqueue generations [gen, gen + G) and the copies of their state / dead ll, lp into slot q
   auto launch_batch = [&](int64_t G, int q) -> int {
     const int64_t need = (gen + G) * k;
@@ -467,9 +490,11 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
       a.trace = (g == trace_gen) ? (unsigned long long*)B.trace.p : nullptr;
 #endif
       if (a.pipe) {
-        // generation g: walk (reads the head keys) -> sort the new keys -> [merge stream: full
-        // merge of keys g-1 with them] -> head merge of keys g-1 [k, 2k) with them (waits for the
-        // full merge of generation g-1, which ran beside this walk)
+        // generation g: walk g (reads the head keys) -> rank count g (sorts the new keys) ->
+        // head merge g (keys g-1 [k, 2k) with them).  The full merge of generation g - 1 runs on
+        // the merge stream beside rank count g (both are latency-bound; beside the walk it slowed
+        // the walkers), after walk g, and head merge g waits for it.  The batch's last full merge
+        // is enqueued at the batch's end (launch_batch below).
         NestArgs aw = a;
         aw.key_ll = B.head.l();
         aw.key_tie = B.head.t();
@@ -478,14 +503,13 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
         if (ctx->timing) timing_begin(ctx, &e0, &e1);
         HC(walk(aw, s), "nested walk");
         if (ctx->timing) timing_end(ctx, e0, e1, 1);
+        if (g > gen) {                                 // full merge g - 1 (its walk's batch)
+          HC(hipEventRecord(B.ev_sorted[g & 1], s), "record walk");
+          HC(full_merge(g - 1, B.ev_sorted[g & 1]), "full merge");
+        }
         KeyBuf& nk = (g & 1) ? B.newk_tmp2 : B.newk_tmp;
         HC(launch_sort_new_small(a, nk.l(), nk.t(), nk.s(), s), "sort new keys");
         if (check) HC(launch_check_sorted(nk.l(), nk.t(), k, g, (long long*)B.chk.p, s), "check");
-        HC(hipEventRecord(B.ev_sorted[g & 1], s), "record sorted");
-        HC(hipStreamWaitEvent(B.s2, B.ev_sorted[g & 1], 0), "merge stream wait");
-        HC(launch_merge_new(a, nxt.l(), nxt.t(), nxt.s(), nk.l(), nk.t(), nk.s(), B.s2), "merge keys");
-        if (check) HC(launch_check_sorted(nxt.l(), nxt.t(), n, g, (long long*)B.chk.p + 1, B.s2), "check");
-        HC(hipEventRecord(B.ev_full[g & 1], B.s2), "record merged");
         if (g > 0) HC(hipStreamWaitEvent(s, B.ev_full[(g - 1) & 1], 0), "head wait");
         const int64_t ns = std::min<int64_t>(k, n - k);
         HC(launch_head_merge(a, cur.l() + k, cur.t() + k, cur.s() + k, ns, nk.l(), nk.t(), nk.s(), B.head.l(),
@@ -510,8 +534,13 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
       HC(launch_merge_new(a, nxt.l(), nxt.t(), nxt.s(), nk.l(), nk.t(), nk.s(), s), "merge keys");
       if (check) HC(launch_check_sorted(nxt.l(), nxt.t(), n, g, (long long*)B.chk.p + 1, s), "check");
     }
-    // the batch's last full merge (merge stream) before its state is read
-    if (a.pipe && G > 0) HC(hipStreamWaitEvent(s, B.ev_full[(gen + G - 1) & 1], 0), "batch merge wait");
+    // the batch's last full merge (merge stream), then the state is read after it
+    if (a.pipe && G > 0) {
+      const int64_t gl = gen + G - 1;
+      HC(hipEventRecord(B.ev_sorted[(gl + 1) & 1], s), "record sorted");
+      HC(full_merge(gl, B.ev_sorted[(gl + 1) & 1]), "full merge");
+      HC(hipStreamWaitEvent(s, B.ev_full[gl & 1], 0), "batch merge wait");
+    }
     HC(hipMemcpyAsync(&hst[q], B.st.p, sizeof(NestDevState), hipMemcpyDeviceToHost, s), "read state");
     HC(hipMemcpyAsync(B.h_stage[2 * q], (double*)B.dead_ll.p + gen * k, G * k * 8, hipMemcpyDeviceToHost, s),
        "stage dead ll");

@@ -549,9 +549,27 @@ __global__ void __launch_bounds__(256) head_merge_kernel(const NestArgs a, const
   const int64_t len_own = from_surv ? ns : k, len_oth = from_surv ? k : ns;
   const double* ol = from_surv ? nl : sl_;
   const long long* ot = from_surv ? nt : st_;
-  for (int64_t q = threadIdx.x; q < len_oth; q += 256) {
-    o_l[q] = ol[q];
-    o_t[q] = ot[q];
+  {
+    // every staging load in flight together (a loop of unknown trip count issued them one
+    // memory round trip at a time), then the LDS stores
+    constexpr int kPer = kSmallSort / 256;
+    double vl[kPer];
+    long long vt[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      const int64_t q = (int64_t)r * 256 + threadIdx.x;
+      const int64_t qc = q < len_oth ? q : len_oth - 1;
+      vl[r] = ol[qc];
+      vt[r] = ot[qc];
+    }
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      const int64_t q = (int64_t)r * 256 + threadIdx.x;
+      if (q < len_oth) {
+        o_l[q] = vl[r];
+        o_t[q] = vt[r];
+      }
+    }
   }
   double kl = 0.0;
   long long kt = 0;

@@ -98,7 +98,7 @@ def test_c5_full_size_per_gpu_moments(T):
         mean, sd, lz = ctx.stats()
         acc, rej = ctx.counters()
     sdt = np.sqrt(np.diag(cov))
-    assert 0.1 < acc / (acc + rej) < 0.5
+    assert 0.3 < acc / (acc + rej) < 0.8              # scale from the smallest eigenvalue: ~0.58
     assert np.max(np.abs(mean - mu) / sdt) < 0.02
     assert np.max(np.abs(sd / sdt - 1)) < 0.02
     assert np.isfinite(lz)

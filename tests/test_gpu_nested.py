@@ -230,12 +230,12 @@ def test_nested_walker_box_forms_bit_exact(oracle, T, D, sym, diag):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", ["MCG_NESTED_NO_TABLE", "MCG_NESTED_RETIRE_KERNEL", "both", "MCG_NESTED_NO_PIPE"])
+@pytest.mark.parametrize("env", ["MCG_NESTED_NO_TABLE", "MCG_NESTED_RETIRE_KERNEL", "both", "MCG_NESTED_PIPE"])
 @pytest.mark.parametrize("D", [3, 16])
 def test_nested_alternate_paths_bit_exact(oracle, T, monkeypatch, env, D):
     """The paths the default run does not take: walkers drawing their own random numbers (no
     draw table: what a generation too big for the table uses), the separate retire kernel
-    (k > 4096 uses it) and the serial full merge instead of the pipelined head + full merges --
+    (k > 4096 uses it) and the pipelined head + full merges instead of the serial merge --
     the same dead points as the oracle, bit for bit."""
     for var in (["MCG_NESTED_NO_TABLE", "MCG_NESTED_RETIRE_KERNEL"] if env == "both" else [env]):
         monkeypatch.setenv(var, "1")
@@ -248,10 +248,12 @@ def test_nested_alternate_paths_bit_exact(oracle, T, monkeypatch, env, D):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("nlive,k", [(300, 200), (257, 256), (5000, 4096)])
-def test_nested_pipelined_head_merge_edges_bit_exact(oracle, T, nlive, k):
-    """Pipelined merges where the head merge sees fewer survivors than new keys
-    (k > nlive / 2), a single survivor (k = nlive - 1), and the largest counted-rank k, run to
-    convergence: dead points, stop generation, log Z and weights equal the oracle's."""
+def test_nested_pipelined_head_merge_edges_bit_exact(oracle, T, monkeypatch, nlive, k):
+    """Pipelined merges (MCG_NESTED_PIPE) where the head merge sees fewer
+    survivors than new keys (k > nlive / 2), a single survivor (k = nlive - 1), and the largest
+    counted-rank k, run to convergence: dead points, stop generation, log Z and weights equal the
+    oracle's."""
+    monkeypatch.setenv("MCG_NESTED_PIPE", "1")
     D = 4
     lik = T.gauss_shell(np.zeros(D), 1.0, 0.2)
     pri = T.box(-2 * np.ones(D), 2 * np.ones(D))
