@@ -145,11 +145,14 @@ def main():
         acc, rej = (int(v) for v in cc.cpu().numpy())
     timing = ctx.kernel_timing("mh")
     per_launch = timing["total_ms"] / max(timing["launches"], 1)
-    launch_steps = float(N) * S
+    # a bench step of S sweeps may run as several launches (the runtime caps a launch at
+    # min(4096, 2^26 / N) sweeps): the framing uses the kernel time of all the timed launches
+    kernel_ms_per_step = timing["total_ms"] / max(args.steps, 1)
+    step_chain_steps = float(N) * S
     bytes_per_step = 8.0 * (D + 2)
     flops_per_step = 2.0 * D * (D + 1) / 2        # triangular quadratic form: D(D+1)/2 FMA
-    ach_gbs = launch_steps * bytes_per_step / (per_launch * 1e-3) / 1e9
-    ach_tfs = launch_steps * flops_per_step / (per_launch * 1e-3) / 1e12
+    ach_gbs = step_chain_steps * bytes_per_step / (kernel_ms_per_step * 1e-3) / 1e9
+    ach_tfs = step_chain_steps * flops_per_step / (kernel_ms_per_step * 1e-3) / 1e12
     total_chains = N * world
     if rank == 0:
         sdt = np.sqrt(np.diag(cov))
@@ -175,7 +178,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": ach_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach_gbs / HBM_PEAK_GBS, "bytes_per_step": bytes_per_step,
                          "kernel": "mcg::mh_fullcov_kernel<64>", "avg_launch_ms": per_launch,
-                         "launches": timing["launches"],
+                         "launches": timing["launches"], "kernel_ms_per_step": kernel_ms_per_step,
                          "fp64_matrix": {"achieved": ach_tfs, "peak": FP64_MATRIX_PEAK_TFS,
                                          "unit": "TFLOP/s", "frac": ach_tfs / FP64_MATRIX_PEAK_TFS,
                                          "flops_per_step": flops_per_step}},

@@ -36,6 +36,24 @@ def roofline(kernel, steps_per_launch, bytes_per_step, timing):
             "avg_launch_ms": per_launch, "launches": timing["launches"]}
 
 
+def valu_framing(name, D, N, S, avg_launch_ms):
+    """VALU-issue framing from a committed PMC pass of this config (profiles/pmc_valu_<name>.json,
+    scripts/pmc_valu.py): 4 SIMD cycles per wave64 VALU instruction over 1,024 SIMDs, against the
+    2.4 GHz peak for this run's launch time, and at the clock held in the PMC pass."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_valu_%s.json" % name)) as fh:
+            v = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    if v.get("config") != {"ndim": D, "chains_per_gpu": N, "sweeps_per_step": S}:
+        return None
+    issue = 4.0 * v["valu_insts_per_launch"] / 1024.0
+    return {"bound": "valu", "insts_per_launch": v["valu_insts_per_launch"],
+            "frac": issue / (2.4e9 * avg_launch_ms * 1e-3), "clock_ghz": 2.4,
+            "frac_at_held_clock": v["valu_busy_frac_at_held_clock"],
+            "source": "profiles/pmc_valu_%s.json" % name}
+
+
 def shell_log_z(D, r, w, half):
     """Analytic log Z of one Gaussian shell in [-half, half]^D (radial quadrature; the shell
     lies well inside the box)."""
@@ -179,7 +197,9 @@ def c4(args):
                                  ctx.kernel_timing("mh")),
             "roofline_note": "SURVEY 8(d) bytes (state + box + two descents); the 4 MB tree and the "
                              "boxes are cache-resident and strict-interior draws skip the descents, "
-                             "so frac > 1 is possible: the step is instruction-issue bound (DESIGN 5.4)"}
+                             "so frac > 1 is possible: the step is instruction-issue bound (DESIGN 5.4); "
+                             "roofline_valu is the bound that holds"}
+    line["roofline_valu"] = valu_framing("c4", D, N, S, line["roofline"]["avg_launch_ms"])
     ctx.close()
     return line
 
@@ -216,6 +236,7 @@ def c5(args):
             "roofline": roofline("mcg::mh_kernel<64,P,FULLCOV,GAUSS>", N * S, 8.0 * (D + 2),
                                  ctx.kernel_timing("mh")),
             "flops_per_step": D * (D + 1)}
+    line["roofline_valu"] = valu_framing("c5", D, N, S, line["roofline"]["avg_launch_ms"])
     ctx.close()
     return line
 
