@@ -124,12 +124,17 @@ void parallel_for(int64_t lo, int64_t hi, int threads, F f) {
 
 class EvFold {
  public:
-  EvFold(int64_t nlive, int64_t k) : n_(nlive), k_(k), prefix_((size_t)k + 1, 0.0) {
+  EvFold(int64_t nlive, int64_t k) : n_(nlive), k_(k), prefix_((size_t)k + 1, 0.0), lfrac_((size_t)k) {
     for (int64_t j = 0; j < k; ++j) prefix_[j + 1] = prefix_[j] + std::log1p(-1.0 / (double)(nlive - j));
+    // log(1 / (n - j)) of every retirement slot j, and the k = 1 terms of nested.ml:96, computed
+    // once (the per-point log was most of the fold's time; the same values bit for bit)
+    for (int64_t j = 0; j < k; ++j) lfrac_[(size_t)j] = std::log(1.0 / (double)(nlive - j));
+    l1_ = std::log(1.0 / (double)nlive);
+    l1p_ = std::log1p(-1.0 / (double)nlive);
     threads_ = (int)std::max<unsigned>(1, std::min<unsigned>(14, std::thread::hardware_concurrency()));
     // while the GPU runs (on the fold worker, beside the launching thread)
     const char* e = std::getenv("MCG_NESTED_FOLD_THREADS");
-    stream_threads_ = std::max(1, std::min(threads_, e ? std::atoi(e) : 6));
+    stream_threads_ = std::max(1, std::min(threads_, e ? std::atoi(e) : 12));
   }
 
   // ll[0, avail) are dead points (avail <= ilive): fold the blocks and weights that need no
@@ -186,9 +191,9 @@ class EvFold {
     double ldv_live;
     int64_t ntot = INT64_MAX;
     double ldv_dead(int64_t i) const {
-      if (f->k_ == 1) return std::log(1.0 / (double)f->n_) + (double)i * std::log1p(-1.0 / (double)f->n_);
+      if (f->k_ == 1) return f->l1_ + (double)i * f->l1p_;
       const int64_t j = i % f->k_, g = i / f->k_;
-      return std::log(1.0 / (double)(f->n_ - j)) + ((double)g * f->prefix_[(size_t)f->k_] + f->prefix_[(size_t)j]);
+      return f->lfrac_[(size_t)j] + ((double)g * f->prefix_[(size_t)f->k_] + f->prefix_[(size_t)j]);
     }
     // iteration i's (dl, dh): first loop i < ilive, second loop i >= ilive (nested.ml:90-113)
     double dl(int64_t i) const { return i < ilive ? ldv_dead(i) + ll[i] : ldv_live + ll[i - 1]; }
@@ -222,7 +227,8 @@ class EvFold {
   }
 
   int64_t n_, k_;
-  std::vector<double> prefix_;
+  std::vector<double> prefix_, lfrac_;
+  double l1_ = 0.0, l1p_ = 0.0;
   int threads_ = 1, stream_threads_ = 1;
   std::vector<double> blow_, bhigh_;
   int64_t wdone_ = 0;
@@ -334,6 +340,9 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   // keys (a 2k-key head merge).  Measured slower than the serial merge (the cross-stream event
   // waits cost more per generation than the merge they hide), so it is not the default.
   a.pipe = a.fuse_retire && std::getenv("MCG_NESTED_PIPE") != nullptr ? 1 : 0;
+  // k <= 4096 (retire in the walk): sort + merge in one launch; MCG_NESTED_MERGE2=1 keeps the
+  // counted-rank sort and the merge as two launches
+  const bool fused_merge = a.fuse_retire && !a.pipe && std::getenv("MCG_NESTED_MERGE2") == nullptr;
   if (a.pipe) {
     HC(B.head.ensure(k), "alloc head keys");
     HC(B.newk_tmp2.ensure(k), "alloc new keys");
@@ -520,6 +529,12 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
       if (ctx->timing) timing_begin(ctx, &e0, &e1);
       HC(walk(a, s), "nested walk");
       if (ctx->timing) timing_end(ctx, e0, e1, 1);
+      if (fused_merge) {
+        // the new keys sorted and merged into the survivors in one launch (merge_fused_kernel)
+        HC(launch_merge_fused(a, nxt.l(), nxt.t(), nxt.s(), s), "merge keys");
+        if (check) HC(launch_check_sorted(nxt.l(), nxt.t(), n, g, (long long*)B.chk.p + 1, s), "check");
+        continue;
+      }
       if (!a.fuse_retire) HC(launch_retire(a, D, s), "nested retire");
       bool nk_tmp = false;
       if (k <= 4096) {

@@ -796,6 +796,9 @@ hipError_t launch_retire(const NestArgs& a, int D, hipStream_t st);
 // every kKeySample-th of n sorted keys (indices kKeySample-1, 2 kKeySample-1, ...) into s*
 hipError_t launch_key_sample(const double* ll, const long long* tie, int64_t n, double* sll,
                              long long* stie, hipStream_t st, NestDevState* state = nullptr);
+// k <= 4096: the generation's unsorted new keys merged into the survivors in one launch (plus the
+// estimate and the slot writes): keys -> o*
+hipError_t launch_merge_fused(const NestArgs& a, double* oll, long long* otie, int* oslot, hipStream_t s);
 // pipelined merges: the k lowest of survivors[0, ns) (ns <= k) and the k sorted new keys into h*
 hipError_t launch_head_merge(const NestArgs& a, const double* sl, const long long* st, const int* ss, int64_t ns,
                              const double* nl, const long long* nt, const int* nsl, double* hl, long long* ht,

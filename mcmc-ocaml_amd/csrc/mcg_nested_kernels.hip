@@ -512,6 +512,188 @@ __global__ void __launch_bounds__(256) merge_new_kernel(const NestArgs a, double
   NT_STAMP(3, 3);
 }
 
+// One-kernel sort + merge of a generation's k <= 4096 unsorted new keys into the n - k survivors
+// (DESIGN.md §5.3, round 3).  Survivor block b (256 consecutive survivors s[256b, 256b + 256))
+// owns the key range [s[256b], s[256b + 256]) (block 0 from -inf, the last block to +inf), so
+// every new key belongs to exactly one block.  Each block stages the k new ll in LDS (a new key's
+// tie, -(mrep + j + 1), is known from its index j) and finds
+//   c_lo = #new keys below its range          (every new key below s[256b]),
+//   its subset: the new keys inside its range, ranked among themselves by counting;
+// then survivor i goes to  i + c_lo + #subset below it,  and subset key x to
+//   256b + #block survivors below x + c_lo + rank of x in the subset.
+// No sorted new-key array, no hand-off between workgroups: the old rank count -> merge pair
+// (two launches, 11.5 + 11.1 us at C3) becomes one launch.  An extra workgroup folds the running
+// estimate; every merge workgroup then takes a share of the new points' slot writes.
+constexpr int kSubCap = kSmallSort;
+
+__global__ void __launch_bounds__(256) merge_fused_kernel(const NestArgs a, double* oll, long long* otie,
+                                                          int* oslot) {
+  if (nest_stopped(a.st)) return;                         // grid-uniform: set by an earlier launch
+  const int64_t n = a.n, k = a.k, ns = n - k;
+  const int nblk = (int)((ns + 255) / 256);
+  const int t = threadIdx.x;
+  if ((int)blockIdx.x == nblk) {                          // the running estimate (retire wrote tv)
+    estimate_body<256>(a);
+    return;
+  }
+  __shared__ double s_nl[kSmallSort];                     // new ll by walker index j
+  __shared__ double s_sv_l[256];                          // this block's survivors
+  __shared__ long long s_sv_t[256];
+  __shared__ short s_sub[kSubCap];                        // subset (new-key indices), then sorted
+  __shared__ short s_srt[kSubCap];
+  __shared__ int s_scan[256];
+  __shared__ int s_below[4];
+  const int b = blockIdx.x;
+  const int64_t i0 = (int64_t)b * 256;
+  const int nsb = (int)min((int64_t)256, ns - i0);
+  const double* sll = a.key_ll + k;
+  const long long* stie = a.key_tie + k;
+  const int* sslot = a.key_slot + k;
+  const long long tie0 = -(long long)a.mrep - 1;          // tie of new key j: tie0 - j
+  // loads: own survivor, the range's upper bound, the k new ll -- all in flight together
+  double kl = 0.0;
+  long long kt = 0;
+  int ks = 0;
+  if (t < nsb) {
+    kl = sll[i0 + t];
+    kt = stie[i0 + t];
+    ks = sslot[i0 + t];
+  }
+  const bool has_hi = i0 + 256 < ns;
+  const double hi_l = has_hi ? sll[i0 + 256] : 0.0;
+  const long long hi_t = has_hi ? stie[i0 + 256] : 0;
+  constexpr int kPer = kSmallSort / 256;
+  double nv[kPer];
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) {
+    const int64_t j = (int64_t)r * 256 + t;
+    nv[r] = a.newk_ll[j < k ? j : k - 1];
+  }
+  if (t < nsb) {
+    s_sv_l[t] = kl;
+    s_sv_t[t] = kt;
+  }
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) {
+    const int64_t j = (int64_t)r * 256 + t;
+    if (j < k) s_nl[j] = nv[r];
+  }
+  __syncthreads();
+  const double lo_l = s_sv_l[0];
+  const long long lo_t = s_sv_t[0];
+  // classify this thread's new keys j = r * 256 + t: below the range, or inside it
+  int below = 0;
+  uint32_t inmask = 0;
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) {
+    const int64_t j = (int64_t)r * 256 + t;
+    if (j >= k) continue;
+    const double x = nv[r];
+    const long long xt = tie0 - j;
+    const bool ge_lo = b == 0 || !key_less(x, xt, lo_l, lo_t);
+    const bool lt_hi = !has_hi || key_less(x, xt, hi_l, hi_t);
+    below += ge_lo ? 0 : 1;
+    if (ge_lo && lt_hi) inmask |= 1u << r;
+  }
+  // c_lo (block sum of `below`) and the subset offsets (exclusive scan of the in-range counts)
+  int cnt = __popc(inmask);
+  int bw = below;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) bw += __shfl_xor(bw, o, 64);
+  if ((t & 63) == 0) s_below[t >> 6] = bw;
+  s_scan[t] = cnt;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {                     // inclusive scan (Hillis-Steele)
+    const int v = t >= o ? s_scan[t - o] : 0;
+    __syncthreads();
+    s_scan[t] += v;
+    __syncthreads();
+  }
+  const int64_t c_lo = (int64_t)s_below[0] + s_below[1] + s_below[2] + s_below[3];
+  const int m = s_scan[255];
+  {
+    int o = s_scan[t] - cnt;
+#pragma unroll
+    for (int r = 0; r < kPer; ++r)
+      if (inmask & (1u << r)) s_sub[o++] = (short)(r * 256 + t);
+  }
+  __syncthreads();
+  // rank the subset among itself (counting), place it sorted, write the subset keys out
+  for (int e = t; e < m; e += 256) {
+    const int j = s_sub[e];
+    const double x = s_nl[j];
+    const long long xt = tie0 - j;
+    int lr = 0;
+    for (int q = 0; q < m; ++q) {
+      const int jq = s_sub[q];
+      lr += key_less(s_nl[jq], tie0 - jq, x, xt) ? 1 : 0;
+    }
+    s_srt[lr] = (short)j;
+    int lo = 0, hi = nsb;                                 // block survivors below x
+    while (lo < hi) {
+      const int md = (lo + hi) >> 1;
+      if (key_less(s_sv_l[md], s_sv_t[md], x, xt)) lo = md + 1;
+      else hi = md;
+    }
+    const int64_t pos = i0 + lo + c_lo + lr;
+    oll[pos] = x;
+    otie[pos] = xt;
+    oslot[pos] = a.newk_slot[j];
+    if (pos % kKeySample == kKeySample - 1) {
+      a.out_samp_ll[pos / kKeySample] = x;
+      a.out_samp_tie[pos / kKeySample] = xt;
+    }
+    if (pos == n - 1) {
+      if (!a.pipe) a.st->max_ll = x;
+      __hip_atomic_fetch_add(&a.st->gen_done, 1LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  if (t < nsb) {                                          // survivors: i + c_lo + #subset below
+    int lo = 0, hi = m;
+    while (lo < hi) {
+      const int md = (lo + hi) >> 1;
+      const int jm = s_srt[md];
+      if (key_less(s_nl[jm], tie0 - jm, kl, kt)) lo = md + 1;
+      else hi = md;
+    }
+    const int64_t pos = i0 + t + c_lo + lo;
+    oll[pos] = kl;
+    otie[pos] = kt;
+    oslot[pos] = ks;
+    if (pos % kKeySample == kKeySample - 1) {
+      a.out_samp_ll[pos / kKeySample] = kl;
+      a.out_samp_tie[pos / kKeySample] = kt;
+    }
+    if (pos == n - 1) {
+      if (!a.pipe) a.st->max_ll = kl;
+      __hip_atomic_fetch_add(&a.st->gen_done, 1LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  // the walkers' new points into the slots they replace (the next walk reads them after this
+  // kernel): element g of the k x D block, spread over the merge workgroups
+  if (a.fuse_retire) {
+    const int64_t kD = a.k * a.row_bytes / 8, D = a.row_bytes / 8;
+    for (int64_t g = (int64_t)b * 256 + t; g < kD; g += (int64_t)nblk * 256) {
+      const int64_t j = g / D;
+      const int64_t d = g - j * D;
+      const int sj = a.newk_slot[j];
+      a.x[(int64_t)sj * D + d] = a.nx[g];
+      if (d == 0) {
+        a.ll[sj] = a.nll[j];
+        a.lp[sj] = a.nlp[j];
+      }
+    }
+  }
+}
+
+hipError_t launch_merge_fused(const NestArgs& a, double* oll, long long* otie, int* oslot, hipStream_t s) {
+  if (a.k > kSmallSort || a.k < 1 || !a.est_in_rank) return hipErrorInvalidValue;
+  const unsigned nblk = (unsigned)((a.n - a.k + 255) / 256);
+  hipLaunchKernelGGL(merge_fused_kernel, dim3(nblk + 1), dim3(256), 0, s, a, oll, otie, oslot);
+  return hipGetLastError();
+}
+
 __global__ void __launch_bounds__(256) key_sample_kernel(const double* ll, const long long* tie,
                                                          int64_t n, double* sll, long long* stie,
                                                          NestDevState* st) {
