@@ -108,6 +108,9 @@ struct NestArgs {
 #ifndef MCG_NEST_PREFETCH
 #define MCG_NEST_PREFETCH 4
 #endif
+#ifndef MCG_NEST_SPEC
+#define MCG_NEST_SPEC 1      // walker steps in speculated pairs (nest_walk_kernel)
+#endif
 constexpr int kNestPrefetch = MCG_NEST_PREFETCH;    // DE steps whose partner rows are in flight
 // pad rows per draw-table half: the walker loads entries up to 3 prefetch groups past its step
 constexpr int kWalkTabPad = 3 * kNestPrefetch;
@@ -661,6 +664,48 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
       }
     }
     // the serial constrained steps
+#if MCG_NEST_SPEC
+    // two steps at a time, the second one speculated both ways: step u's proposal y0 and the two
+    // candidates of step u + 1 -- from y0 if step u accepts (ya), from the current point if it
+    // rejects (yr), the same arithmetic as computing it after the decision -- are judged
+    // together, three independent dependency chains on the walker's one wave instead of one,
+    // then the two accept decisions resolve in order.  The same states bit for bit.
+    static_assert(PD % 2 == 0, "speculated walker steps come in pairs");
+#pragma unroll
+    for (int u = 0; u < PD; u += 2) {
+      const bool live0 = s0 + u < nm, live1 = s0 + u + 1 < nm;
+      double y0[NL], ya[NL], yr[NL];
+#pragma unroll
+      for (int d = 0; d < NL; ++d) {
+        const double e1 = dsc_g[u + 1] * (bj[u + 1][d] - bi[u + 1][d]);
+        y0[d] = cur[d] + dsc_g[u] * (bj[u][d] - bi[u][d]);
+        ya[d] = y0[d] + e1;
+        yr[d] = cur[d] + e1;
+      }
+      refill(bi[u], ip_g[u]);                          // refill slots u, u + 1 with the rows of
+      refill(bj[u], jp_g[u]);                          // steps s + PD, s + PD + 1
+      refill(bi[u + 1], ip_g[u + 1]);
+      refill(bj[u + 1], jp_g[u + 1]);
+      const bool ok0 = tgt.constraint(y0, sub, a.m, thr);
+      const bool oka = tgt.constraint(ya, sub, a.m, thr);
+      const bool okr = tgt.constraint(yr, sub, a.m, thr);
+      const double lp0 = tgt.prior(y0, sub, a.m);
+      const double lpa = tgt.prior(ya, sub, a.m);
+      const double lpr = tgt.prior(yr, sub, a.m);
+      const double ninf = -__builtin_inf();
+      const double ml0 = ok0 ? lp0 : ninf, mla = oka ? lpa : ninf, mlr = okr ? lpr : ninf;
+      const bool acc0 = live0 && lu_g[u] < ml0 - cur_l;
+      const double cl1 = acc0 ? ml0 : cur_l;           // step u + 1 from the state u leaves
+      const double ml1 = acc0 ? mla : mlr;
+      const bool acc1 = live1 && lu_g[u + 1] < ml1 - cl1;
+#pragma unroll
+      for (int d = 0; d < NL; ++d) {
+        const double c1 = acc0 ? y0[d] : cur[d];
+        cur[d] = acc1 ? (acc0 ? ya[d] : yr[d]) : c1;
+      }
+      cur_l = acc1 ? ml1 : cl1;
+    }
+#else
 #pragma unroll
     for (int u = 0; u < PD; ++u) {
       const bool live = s0 + u < nm;
@@ -680,6 +725,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
         cur_l = ml;
       }
     }
+#endif
     if constexpr (TAB) {
 #pragma unroll
       for (int u = 0; u < PD; ++u) {

@@ -541,8 +541,7 @@ __global__ void __launch_bounds__(256) merge_fused_kernel(const NestArgs a, doub
   __shared__ long long s_sv_t[256];
   __shared__ short s_sub[kSubCap];                        // subset (new-key indices), then sorted
   __shared__ short s_srt[kSubCap];
-  __shared__ int s_scan[256];
-  __shared__ int s_below[4];
+  __shared__ int s_scan[2];
   const int b = blockIdx.x;
   const int64_t i0 = (int64_t)b * 256;
   const int nsb = (int)min((int64_t)256, ns - i0);
@@ -569,6 +568,22 @@ __global__ void __launch_bounds__(256) merge_fused_kernel(const NestArgs a, doub
     const int64_t j = (int64_t)r * 256 + t;
     nv[r] = a.newk_ll[j < k ? j : k - 1];
   }
+  // the walkers' new points into the slots they replace (the next walk reads them after this
+  // kernel; nothing here reads them): element g of the k x D block, spread over the merge
+  // workgroups, issued while the staging loads are in flight
+  if (a.fuse_retire) {
+    const int64_t kD = a.k * a.row_bytes / 8, D = a.row_bytes / 8;
+    for (int64_t g = (int64_t)b * 256 + t; g < kD; g += (int64_t)nblk * 256) {
+      const int64_t j = g / D;
+      const int64_t d = g - j * D;
+      const int sj = a.newk_slot[j];
+      a.x[(int64_t)sj * D + d] = a.nx[g];
+      if (d == 0) {
+        a.ll[sj] = a.nll[j];
+        a.lp[sj] = a.nlp[j];
+      }
+    }
+  }
   if (t < nsb) {
     s_sv_l[t] = kl;
     s_sv_t[t] = kt;
@@ -581,9 +596,15 @@ __global__ void __launch_bounds__(256) merge_fused_kernel(const NestArgs a, doub
   __syncthreads();
   const double lo_l = s_sv_l[0];
   const long long lo_t = s_sv_t[0];
-  // classify this thread's new keys j = r * 256 + t: below the range, or inside it
+  // classify this thread's new keys j = r * 256 + t: below the range, or inside it; the subset
+  // is gathered in any order (LDS atomics: it is ranked by counting below) and c_lo is summed
+  // the same way (integers: exact in any order)
+  if (t == 0) {
+    s_scan[0] = 0;                                        // subset size
+    s_scan[1] = 0;                                        // c_lo
+  }
+  __syncthreads();
   int below = 0;
-  uint32_t inmask = 0;
 #pragma unroll
   for (int r = 0; r < kPer; ++r) {
     const int64_t j = (int64_t)r * 256 + t;
@@ -593,31 +614,14 @@ __global__ void __launch_bounds__(256) merge_fused_kernel(const NestArgs a, doub
     const bool ge_lo = b == 0 || !key_less(x, xt, lo_l, lo_t);
     const bool lt_hi = !has_hi || key_less(x, xt, hi_l, hi_t);
     below += ge_lo ? 0 : 1;
-    if (ge_lo && lt_hi) inmask |= 1u << r;
+    if (ge_lo && lt_hi) s_sub[atomicAdd(&s_scan[0], 1)] = (short)j;
   }
-  // c_lo (block sum of `below`) and the subset offsets (exclusive scan of the in-range counts)
-  int cnt = __popc(inmask);
-  int bw = below;
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) bw += __shfl_xor(bw, o, 64);
-  if ((t & 63) == 0) s_below[t >> 6] = bw;
-  s_scan[t] = cnt;
+  for (int o = 32; o >= 1; o >>= 1) below += __shfl_xor(below, o, 64);
+  if ((t & 63) == 0 && below) atomicAdd(&s_scan[1], below);
   __syncthreads();
-  for (int o = 1; o < 256; o <<= 1) {                     // inclusive scan (Hillis-Steele)
-    const int v = t >= o ? s_scan[t - o] : 0;
-    __syncthreads();
-    s_scan[t] += v;
-    __syncthreads();
-  }
-  const int64_t c_lo = (int64_t)s_below[0] + s_below[1] + s_below[2] + s_below[3];
-  const int m = s_scan[255];
-  {
-    int o = s_scan[t] - cnt;
-#pragma unroll
-    for (int r = 0; r < kPer; ++r)
-      if (inmask & (1u << r)) s_sub[o++] = (short)(r * 256 + t);
-  }
-  __syncthreads();
+  const int m = s_scan[0];
+  const int64_t c_lo = s_scan[1];
   // rank the subset among itself (counting), place it sorted, write the subset keys out
   for (int e = t; e < m; e += 256) {
     const int j = s_sub[e];
@@ -668,21 +672,6 @@ __global__ void __launch_bounds__(256) merge_fused_kernel(const NestArgs a, doub
     if (pos == n - 1) {
       if (!a.pipe) a.st->max_ll = kl;
       __hip_atomic_fetch_add(&a.st->gen_done, 1LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  // the walkers' new points into the slots they replace (the next walk reads them after this
-  // kernel): element g of the k x D block, spread over the merge workgroups
-  if (a.fuse_retire) {
-    const int64_t kD = a.k * a.row_bytes / 8, D = a.row_bytes / 8;
-    for (int64_t g = (int64_t)b * 256 + t; g < kD; g += (int64_t)nblk * 256) {
-      const int64_t j = g / D;
-      const int64_t d = g - j * D;
-      const int sj = a.newk_slot[j];
-      a.x[(int64_t)sj * D + d] = a.nx[g];
-      if (d == 0) {
-        a.ll[sj] = a.nll[j];
-        a.lp[sj] = a.nlp[j];
-      }
     }
   }
 }
