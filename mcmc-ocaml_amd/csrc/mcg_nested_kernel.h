@@ -109,7 +109,7 @@ struct NestArgs {
 #define MCG_NEST_PREFETCH 4
 #endif
 #ifndef MCG_NEST_SPEC
-#define MCG_NEST_SPEC 1      // walker steps in speculated pairs (nest_walk_kernel)
+#define MCG_NEST_SPEC 0      // experiment: walker steps in speculated pairs (slower: 28.3 -> 35.0 us at C3)
 #endif
 constexpr int kNestPrefetch = MCG_NEST_PREFETCH;    // DE steps whose partner rows are in flight
 // pad rows per draw-table half: the walker loads entries up to 3 prefetch groups past its step
