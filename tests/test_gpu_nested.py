@@ -9,6 +9,12 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
+# Parity tests that compare a fixed number of generations end at max_dead on purpose (the
+# oracle is cut at the same point); their UnconvergedWarning is expected.  The converged paths
+# are tested with the stop test firing (test_nested_converged_batched_default_path_bit_exact,
+# test_nested_pipelined_head_merge_edges_bit_exact, test_nested_batched_bit_exact).
+pytestmark = pytest.mark.filterwarnings("ignore:nested_evidence. max_dead")
+
 
 @pytest.fixture(scope="module")
 def T():
@@ -261,6 +267,20 @@ def test_nested_pipelined_head_merge_edges_bit_exact(oracle, T, monkeypatch, nli
     pri = T.box(-2 * np.ones(D), 2 * np.ones(D))
     g = gpu_nested(lik, pri, 23, nlive=nlive, nmcmc=6, mode_hopping_frac=0.1, k=k)
     o = oracle_nested(oracle, lik, pri, 23, nlive=nlive, nmcmc=6, mode_hop=0.1, k=k)
+    assert g.converged
+    assert_nested_same(g, o)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nlive,k,D", [(3000, 256, 4), (8192, 1024, 16), (20000, 4096, 8)])
+def test_nested_converged_batched_default_path_bit_exact(oracle, T, nlive, k, D):
+    """The default k > 1 path (walk -> one-launch sort + merge) run to its own stop test at
+    larger nlive, with survivor blocks holding many new keys each: every dead point, the stop
+    generation, log Z, log dZ and the weights equal the oracle's."""
+    lik = T.gauss_shell(np.zeros(D), 1.0, 0.2)
+    pri = T.box(-2 * np.ones(D), 2 * np.ones(D))
+    g = gpu_nested(lik, pri, 31, nlive=nlive, nmcmc=4, mode_hopping_frac=0.1, k=k)
+    o = oracle_nested(oracle, lik, pri, 31, nlive=nlive, nmcmc=4, mode_hop=0.1, k=k)
     assert g.converged
     assert_nested_same(g, o)
 
