@@ -578,36 +578,51 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   } fw_guard{fw};
   int64_t G = std::min<int64_t>(batch, max_dead / k);
   if (G <= 0) return set_error(ctx, MCG_EINVAL, "max_dead below one generation");
+  // Two batches in flight: while the GPU runs the batch in one slot, the other slot's batch is
+  // already enqueued behind it, so the GPU does not idle while the host wakes up, reads a
+  // finished batch's state and enqueues the next one.  A batch enqueued past the stop runs as
+  // no-ops (every kernel tests the stop flag).
+  int64_t gstart[2] = {0, 0};
+  bool inflight[2] = {false, false};
+  gstart[q] = gen;
   if ((rc = launch_batch(G, q))) return rc;
-  int64_t gen_q = 0;                                  // first generation of the batch in slot q
+  inflight[q] = true;
+  if (max_dead / k - gen > 0) {
+    batch = std::min<int64_t>(batch * 2, kMaxBatch);
+    gstart[q ^ 1] = gen;
+    if ((rc = launch_batch(std::min(batch, max_dead / k - gen), q ^ 1))) return rc;
+    inflight[q ^ 1] = true;
+  }
   NestDevState st{};
   std::vector<double> hx;
   for (;;) {
     const auto tw0 = now();
     HC(hipEventSynchronize(B.done[q]), "nested sync");
     t_wait += ms(tw0, now());
+    inflight[q] = false;
     st = hst[q];
-    if (st.error)
+    if (st.error) {
+      if (inflight[q ^ 1]) (void)hipEventSynchronize(B.done[q ^ 1]);
       return set_error(ctx, MCG_EFAIL, "Error in draw_new_live_point: new log(L) below the threshold");
-    const int64_t remaining = max_dead / k - gen;
-    const bool last = st.stopped || remaining <= 0;
-    const int64_t gen_b = gen_q;
-    if (!last) {                                      // keep the GPU busy: enqueue the next batch
-      batch = std::min<int64_t>(batch * 2, kMaxBatch);
-      gen_q = gen;
-      const auto tl = now();
-      if ((rc = launch_batch(std::min(batch, remaining), q ^ 1))) return rc;
-      t_launch += ms(tl, now());
     }
     // the fold worker must be done with R.ll / R.wts before they grow
     const auto tf = now();
     if (fw.joinable()) fw.join();
     t_fold += ms(tf, now());
-    // this batch's dead points: generations [gen_b, st.gen_done) of the ones it launched
-    const int64_t d0 = gen_b * k, d1 = st.gen_done * k;
+    // this batch's dead points: generations [gstart[q], st.gen_done) of the ones it launched
+    const int64_t d0 = gstart[q] * k, d1 = st.gen_done * k;
     if (d1 > d0) {
       R.ll.insert(R.ll.end(), B.h_stage[2 * q], B.h_stage[2 * q] + (d1 - d0));
       R.lp.insert(R.lp.end(), B.h_stage[2 * q + 1], B.h_stage[2 * q + 1] + (d1 - d0));
+    }
+    const int64_t remaining = max_dead / k - gen;
+    if (!st.stopped && remaining > 0) {               // the slot is free again: refill it
+      batch = std::min<int64_t>(batch * 2, kMaxBatch);
+      gstart[q] = gen;
+      const auto tl = now();
+      if ((rc = launch_batch(std::min(batch, remaining), q))) return rc;
+      t_launch += ms(tl, now());
+      inflight[q] = true;
     }
     const int64_t ndead = d1;
     if (observer && ndead > reported) {
@@ -617,7 +632,12 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
       observer(user, hx.data(), R.ll.data() + reported, R.lp.data() + reported, m);
       reported = ndead;
     }
-    if (last) break;
+    if (st.stopped) {
+      // a batch enqueued past the stop retires nothing; let it drain before the final copies
+      if (inflight[q ^ 1]) HC(hipEventSynchronize(B.done[q ^ 1]), "nested sync");
+      break;
+    }
+    if (!inflight[q] && !inflight[q ^ 1]) break;      // max_dead reached
     // fold what is final on the worker while this thread keeps the GPU fed
     R.wts.resize(R.ll.size());
     fw = std::thread([&fold, llp = R.ll.data(), av = (int64_t)R.ll.size(), wp = R.wts.data()] {
