@@ -88,6 +88,10 @@ struct NestedBufs {
 
 double lse_host(double a, double b) {            // Stats.log_sum_logs (stats.ml:240-248)
   if (a == -HUGE_VAL && b == -HUGE_VAL) return -HUGE_VAL;
+  // one side -inf: exp(-inf) = 0 and log1p(0) = 0, so the sum is the other side + 0.0 (the
+  // same bits, without the two libm calls)
+  if (a == -HUGE_VAL) return b + 0.0;
+  if (b == -HUGE_VAL) return a + 0.0;
   if (b > a) std::swap(a, b);
   return a + std::log1p(std::exp(b - a));
 }
@@ -104,6 +108,7 @@ double lse_host(double a, double b) {            // Stats.log_sum_logs (stats.ml
 // block and weight whose inputs are dead points already on the host; finish() does the rest
 // (the live points, ldv_live) once the run has stopped.
 constexpr int64_t kEvBlock = 65536;
+constexpr int64_t kWeightChunk = 16384;                 // weights per fold task
 constexpr double kLogHalf = -0.69314718055994530942;
 
 template <class F>
@@ -119,6 +124,26 @@ void parallel_for(int64_t lo, int64_t hi, int threads, F f) {
     tw.emplace_back([&, t] {
       for (int64_t i = lo + t * (hi - lo) / T; i < lo + (t + 1) * (hi - lo) / T; ++i) f(i);
     });
+  for (auto& x : tw) x.join();
+}
+
+// tasks [0, n) on `threads` threads, handed out one at a time (the block folds are long, the
+// weight chunks short: a static split would leave threads idle behind a block)
+template <class F>
+void parallel_tasks(int64_t n, int threads, F f) {
+  if (n <= 0) return;
+  const int64_t T = std::max<int64_t>(1, std::min<int64_t>(threads, n));
+  if (T == 1) {
+    for (int64_t i = 0; i < n; ++i) f(i);
+    return;
+  }
+  std::atomic<int64_t> next{0};
+  auto run = [&] {
+    for (int64_t i; (i = next.fetch_add(1, std::memory_order_relaxed)) < n;) f(i);
+  };
+  std::vector<std::thread> tw;
+  for (int64_t t = 1; t < T; ++t) tw.emplace_back(run);
+  run();
   for (auto& x : tw) x.join();
 }
 
@@ -141,12 +166,12 @@ class EvFold {
   // later point; wts must hold avail entries
   void advance(const double* ll, int64_t avail, double* wts) {
     View v{this, ll, INT64_MAX, 0.0};
-    // block b is complete when its last iteration's ll[i + 1] is known: (b + 1) B < avail
+    // block b is complete when its last iteration's ll[i + 1] is known: (b + 1) B < avail;
+    // weight m (dead, with m + 1 dead too) needs ll[m] only: m < avail - 1.  The block folds
+    // (sequential inside a block) and the weight chunks run as one task list.
     const int64_t nb = avail > 0 ? (avail - 1) / kEvBlock : 0;
-    fold_blocks(v, nb, stream_threads_);
-    // weight m (dead, with m + 1 dead too) needs ll[m] only: m < avail - 1
     const int64_t wend = std::max<int64_t>(wdone_, avail - 1);
-    parallel_for(wdone_, wend, stream_threads_, [&](int64_t m) { wts[m] = v.weight(m); });
+    fold_and_weigh(v, nb, wend, wts, stream_threads_);
     wdone_ = wend;
   }
 
@@ -168,8 +193,7 @@ class EvFold {
     } else {
       v.ldv_live = std::log(1.0 / (double)n_);
     }
-    fold_blocks(v, (ntot + kEvBlock - 1) / kEvBlock, threads_);
-    parallel_for(wdone_, ntot, threads_, [&](int64_t m) { wts[m] = v.weight(m); });
+    fold_and_weigh(v, (ntot + kEvBlock - 1) / kEvBlock, ntot, wts, threads_);
     double low = -HUGE_VAL, high = -HUGE_VAL;
     for (size_t b = 0; b < blow_.size(); ++b) {
       low = lse_host(low, blow_[b]);
@@ -209,20 +233,32 @@ class EvFold {
     }
   };
 
-  void fold_blocks(const View& v, int64_t nb, int threads) {
+  // blocks [blow_.size(), nb) folded and weights [wdone_, wend) computed, as one task list
+  void fold_and_weigh(const View& v, int64_t nb, int64_t wend, double* wts, int threads) {
     const int64_t b0 = (int64_t)blow_.size();
-    if (nb <= b0) return;
-    blow_.resize((size_t)nb, -HUGE_VAL);
-    bhigh_.resize((size_t)nb, -HUGE_VAL);
+    const int64_t nbt = std::max<int64_t>(0, nb - b0);
+    if (nbt) {
+      blow_.resize((size_t)nb, -HUGE_VAL);
+      bhigh_.resize((size_t)nb, -HUGE_VAL);
+    }
     const int64_t end = std::min<int64_t>(v.ntot, nb * kEvBlock);
-    parallel_for(b0, nb, threads, [&](int64_t b) {
-      double lo = -HUGE_VAL, hi = -HUGE_VAL;
-      for (int64_t i = b * kEvBlock; i < std::min(end, (b + 1) * kEvBlock); ++i) {
-        lo = lse_host(lo, v.dl(i));
-        hi = lse_host(hi, v.dh(i));
+    const int64_t w0 = wdone_, nw = std::max<int64_t>(0, wend - w0);
+    const int64_t nwt = (nw + kWeightChunk - 1) / kWeightChunk;
+    parallel_tasks(nbt + nwt, threads, [&](int64_t task) {
+      if (task < nbt) {
+        const int64_t b = b0 + task;
+        double lo = -HUGE_VAL, hi = -HUGE_VAL;
+        for (int64_t i = b * kEvBlock; i < std::min(end, (b + 1) * kEvBlock); ++i) {
+          lo = lse_host(lo, v.dl(i));
+          hi = lse_host(hi, v.dh(i));
+        }
+        blow_[(size_t)b] = lo;
+        bhigh_[(size_t)b] = hi;
+      } else {
+        const int64_t m0 = w0 + (task - nbt) * kWeightChunk;
+        const int64_t m1 = std::min(wend, m0 + kWeightChunk);
+        for (int64_t m = m0; m < m1; ++m) wts[m] = v.weight(m);
       }
-      blow_[(size_t)b] = lo;
-      bhigh_[(size_t)b] = hi;
     });
   }
 
@@ -411,7 +447,9 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   R.lp.clear();
   R.wts.clear();
   EvFold fold(n, k);
-  constexpr int64_t kMaxBatch = 64;
+  // generations per batch: doubling from 4 up to kMaxBatch (MCG_NESTED_MAX_BATCH)
+  const char* mb_env = std::getenv("MCG_NESTED_MAX_BATCH");
+  const int64_t kMaxBatch = std::max<int64_t>(4, mb_env ? std::atoll(mb_env) : 64);
   if (B.h_cap < kMaxBatch * k) {
     for (auto& h : B.h_stage) {
       if (h) (void)hipHostFree(h);
@@ -460,11 +498,22 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
     if (check && (e = launch_check_sorted(x.l(), x.t(), n, gm, (long long*)B.chk.p + 1, B.s2)) != hipSuccess) return e;
     return hipEventRecord(B.ev_full[gm & 1], B.s2);
   };
+  // dead buffers replaced while batches were in flight: freed after the stream drains
+  struct RetiredBufs {
+    hipStream_t s;
+    std::vector<void*> bufs;
+    ~RetiredBufs() {
+      if (bufs.empty()) return;
+      (void)hipStreamSynchronize(s);
+      for (void* p : bufs) (void)hipFree(p);
+    }
+  } retired_dead{s, {}};
   // enqueue generations [gen, gen + G) and the copies of their state / dead ll, lp into slot q
   auto launch_batch = [&](int64_t G, int q) -> int {
     const int64_t need = (gen + G) * k;
     if (need > B.dead_cap) {
-      const int64_t cap = std::max<int64_t>(need, std::max<int64_t>(2 * B.dead_cap, 16 * n));
+      // room for the live rows too (gathered behind the dead ones at the end)
+      const int64_t cap = std::max<int64_t>(need + n, std::max<int64_t>(2 * B.dead_cap, 16 * n));
       DevBuf nxb, nlb, npb;
       HC(nxb.ensure(cap * D * 8), "alloc dead");
       HC(nlb.ensure(cap * 8), "alloc dead");
@@ -475,10 +524,17 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
         HC(hipMemcpyAsync(nlb.p, B.dead_ll.p, used * 8, hipMemcpyDeviceToDevice, s), "grow dead");
         HC(hipMemcpyAsync(npb.p, B.dead_lp.p, used * 8, hipMemcpyDeviceToDevice, s), "grow dead");
       }
-      HC(hipStreamSynchronize(s), "grow dead");
+      // no host sync: the copies are stream-ordered behind every kernel that writes the old
+      // buffers and ahead of every kernel that writes the new ones; the old buffers are freed
+      // once the run has drained (retired_dead)
       std::swap(B.dead_x.p, nxb.p); std::swap(B.dead_x.bytes, nxb.bytes);
       std::swap(B.dead_ll.p, nlb.p); std::swap(B.dead_ll.bytes, nlb.bytes);
       std::swap(B.dead_lp.p, npb.p); std::swap(B.dead_lp.bytes, npb.bytes);
+      for (DevBuf* o : {&nxb, &nlb, &npb}) {
+        retired_dead.bufs.push_back(o->p);
+        o->p = nullptr;
+        o->bytes = 0;
+      }
       B.dead_cap = cap;
     }
     a.dead_x = (double*)B.dead_x.p;

@@ -13,7 +13,7 @@ namespace mcg {
 
 
 __device__ __forceinline__ bool key_less(double la, long long ta, double lb, long long tb) {
-  return la < lb || (la == lb && ta < tb);
+  return (la < lb) | ((la == lb) & (ta < tb));       // branchless: both halves are cheap
 }
 
 // number of entries of the sorted run [lo, hi) strictly below key
@@ -525,9 +525,13 @@ __global__ void __launch_bounds__(256) merge_new_kernel(const NestArgs a, double
 // (two launches, 11.5 + 11.1 us at C3) becomes one launch.  An extra workgroup folds the running
 // estimate; every merge workgroup then takes a share of the new points' slot writes.
 constexpr int kSubCap = kSmallSort;
+#ifndef MCG_MERGE_UNROLL
+#define MCG_MERGE_UNROLL 16
+#endif
 
 __global__ void __launch_bounds__(256) merge_fused_kernel(const NestArgs a, double* oll, long long* otie,
                                                           int* oslot) {
+  NT_STAMP(3, 0);
   if (nest_stopped(a.st)) return;                         // grid-uniform: set by an earlier launch
   const int64_t n = a.n, k = a.k, ns = n - k;
   const int nblk = (int)((ns + 255) / 256);
@@ -541,7 +545,7 @@ __global__ void __launch_bounds__(256) merge_fused_kernel(const NestArgs a, doub
   __shared__ long long s_sv_t[256];
   __shared__ short s_sub[kSubCap];                        // subset (new-key indices), then sorted
   __shared__ short s_srt[kSubCap];
-  __shared__ int s_scan[2];
+  __shared__ int s_scan[8];
   const int b = blockIdx.x;
   const int64_t i0 = (int64_t)b * 256;
   const int nsb = (int)min((int64_t)256, ns - i0);
@@ -549,7 +553,25 @@ __global__ void __launch_bounds__(256) merge_fused_kernel(const NestArgs a, doub
   const long long* stie = a.key_tie + k;
   const int* sslot = a.key_slot + k;
   const long long tie0 = -(long long)a.mrep - 1;          // tie of new key j: tie0 - j
-  // loads: own survivor, the range's upper bound, the k new ll -- all in flight together
+  // loads: own survivor, the range's upper bound, the k new ll, and the first element of the
+  // walkers' new points this thread copies into the slots they replace -- all in flight together
+  // (the next walk reads the copied points after this kernel; nothing here reads them).  Element
+  // g of the k x D block goes to thread g mod (nblk * 256) of the merge workgroups.
+  const int64_t D = a.row_bytes / 8, kD = a.fuse_retire ? a.k * D : 0;
+  const int64_t g0 = (int64_t)b * 256 + t, gstride = (int64_t)nblk * 256;
+  int sj0 = 0;
+  double cx0 = 0.0, cl0 = 0.0, cp0 = 0.0;
+  int64_t d0 = -1;
+  if (g0 < kD) {
+    const int64_t j = g0 / D;
+    d0 = g0 - j * D;
+    sj0 = a.newk_slot[j];
+    cx0 = a.nx[g0];
+    if (d0 == 0) {
+      cl0 = a.nll[j];
+      cp0 = a.nlp[j];
+    }
+  }
   double kl = 0.0;
   long long kt = 0;
   int ks = 0;
@@ -568,20 +590,21 @@ __global__ void __launch_bounds__(256) merge_fused_kernel(const NestArgs a, doub
     const int64_t j = (int64_t)r * 256 + t;
     nv[r] = a.newk_ll[j < k ? j : k - 1];
   }
-  // the walkers' new points into the slots they replace (the next walk reads them after this
-  // kernel; nothing here reads them): element g of the k x D block, spread over the merge
-  // workgroups, issued while the staging loads are in flight
-  if (a.fuse_retire) {
-    const int64_t kD = a.k * a.row_bytes / 8, D = a.row_bytes / 8;
-    for (int64_t g = (int64_t)b * 256 + t; g < kD; g += (int64_t)nblk * 256) {
-      const int64_t j = g / D;
-      const int64_t d = g - j * D;
-      const int sj = a.newk_slot[j];
-      a.x[(int64_t)sj * D + d] = a.nx[g];
-      if (d == 0) {
-        a.ll[sj] = a.nll[j];
-        a.lp[sj] = a.nlp[j];
-      }
+  if (g0 < kD) {
+    a.x[(int64_t)sj0 * D + d0] = cx0;
+    if (d0 == 0) {
+      a.ll[sj0] = cl0;
+      a.lp[sj0] = cp0;
+    }
+  }
+  for (int64_t g = g0 + gstride; g < kD; g += gstride) {   // k * D beyond one element a thread
+    const int64_t j = g / D;
+    const int64_t d = g - j * D;
+    const int sj = a.newk_slot[j];
+    a.x[(int64_t)sj * D + d] = a.nx[g];
+    if (d == 0) {
+      a.ll[sj] = a.nll[j];
+      a.lp[sj] = a.nlp[j];
     }
   }
   if (t < nsb) {
@@ -594,41 +617,58 @@ __global__ void __launch_bounds__(256) merge_fused_kernel(const NestArgs a, doub
     if (j < k) s_nl[j] = nv[r];
   }
   __syncthreads();
+  NT_STAMP(3, 1);
   const double lo_l = s_sv_l[0];
   const long long lo_t = s_sv_t[0];
-  // classify this thread's new keys j = r * 256 + t: below the range, or inside it; the subset
-  // is gathered in any order (LDS atomics: it is ranked by counting below) and c_lo is summed
-  // the same way (integers: exact in any order)
-  if (t == 0) {
-    s_scan[0] = 0;                                        // subset size
-    s_scan[1] = 0;                                        // c_lo
-  }
-  __syncthreads();
-  int below = 0;
-#pragma unroll
+  // classify this thread's new keys j = r * 256 + t: below the range, or inside it.  Subset
+  // offsets come from wave ballots (the r-th key of every lane: its rank among the wave's set
+  // bits), the wave totals go through LDS; c_lo is summed the same way (integers: exact in any
+  // order).  The subset order does not matter: it is ranked by counting below.
+  uint32_t inmask = 0;
+  int wsub = 0, wbelow = 0;                               // wave-uniform
+#pragma unroll MCG_MERGE_UNROLL
   for (int r = 0; r < kPer; ++r) {
     const int64_t j = (int64_t)r * 256 + t;
-    if (j >= k) continue;
+    const bool ok = j < k;
     const double x = nv[r];
     const long long xt = tie0 - j;
-    const bool ge_lo = b == 0 || !key_less(x, xt, lo_l, lo_t);
-    const bool lt_hi = !has_hi || key_less(x, xt, hi_l, hi_t);
-    below += ge_lo ? 0 : 1;
-    if (ge_lo && lt_hi) s_sub[atomicAdd(&s_scan[0], 1)] = (short)j;
+    const bool ge_lo = (b == 0) | !key_less(x, xt, lo_l, lo_t);
+    const bool lt_hi = !has_hi | key_less(x, xt, hi_l, hi_t);
+    const bool in = ok & ge_lo & lt_hi;
+    inmask |= (in ? 1u : 0u) << r;
+    wsub += __popcll(__ballot(in));
+    wbelow += __popcll(__ballot(ok & !ge_lo));
   }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) below += __shfl_xor(below, o, 64);
-  if ((t & 63) == 0 && below) atomicAdd(&s_scan[1], below);
+  const int lane = t & 63, wv = t >> 6;
+  if (lane == 0) {
+    s_scan[wv] = wsub;                                    // wave totals
+    s_scan[4 + wv] = wbelow;
+  }
   __syncthreads();
-  const int m = s_scan[0];
-  const int64_t c_lo = s_scan[1];
+  int o = 0;
+#pragma unroll
+  for (int w2 = 0; w2 < 4; ++w2) o += w2 < wv ? s_scan[w2] : 0;
+  const int m = s_scan[0] + s_scan[1] + s_scan[2] + s_scan[3];
+  const int64_t c_lo = (int64_t)s_scan[4] + s_scan[5] + s_scan[6] + s_scan[7];
+#pragma unroll MCG_MERGE_UNROLL
+  for (int r = 0; r < kPer; ++r) {
+    const bool in = (inmask >> r) & 1u;
+    const unsigned long long bm = __ballot(in);
+    const int below_lane = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+    if (in) s_sub[o + below_lane] = (short)(r * 256 + t);
+    o += __popcll(bm);
+  }
+  __syncthreads();
+  NT_STAMP(3, 2);
   // rank the subset among itself (counting), place it sorted, write the subset keys out
   for (int e = t; e < m; e += 256) {
     const int j = s_sub[e];
     const double x = s_nl[j];
     const long long xt = tie0 - j;
     int lr = 0;
-    for (int q = 0; q < m; ++q) {
+#pragma unroll 8
+    for (int q = 0; q < m; ++q) {                         // broadcast LDS reads, 8 in flight
       const int jq = s_sub[q];
       lr += key_less(s_nl[jq], tie0 - jq, x, xt) ? 1 : 0;
     }
@@ -653,6 +693,7 @@ __global__ void __launch_bounds__(256) merge_fused_kernel(const NestArgs a, doub
     }
   }
   __syncthreads();
+  NT_STAMP(3, 3);
   if (t < nsb) {                                          // survivors: i + c_lo + #subset below
     int lo = 0, hi = m;
     while (lo < hi) {
@@ -674,6 +715,7 @@ __global__ void __launch_bounds__(256) merge_fused_kernel(const NestArgs a, doub
       __hip_atomic_fetch_add(&a.st->gen_done, 1LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  NT_STAMP(3, 4);
 }
 
 hipError_t launch_merge_fused(const NestArgs& a, double* oll, long long* otie, int* oslot, hipStream_t s) {
