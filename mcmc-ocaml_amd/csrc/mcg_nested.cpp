@@ -244,18 +244,21 @@ class EvFold {
     const int64_t end = std::min<int64_t>(v.ntot, nb * kEvBlock);
     const int64_t w0 = wdone_, nw = std::max<int64_t>(0, wend - w0);
     const int64_t nwt = (nw + kWeightChunk - 1) / kWeightChunk;
-    parallel_tasks(nbt + nwt, threads, [&](int64_t task) {
-      if (task < nbt) {
-        const int64_t b = b0 + task;
-        double lo = -HUGE_VAL, hi = -HUGE_VAL;
-        for (int64_t i = b * kEvBlock; i < std::min(end, (b + 1) * kEvBlock); ++i) {
-          lo = lse_host(lo, v.dl(i));
-          hi = lse_host(hi, v.dh(i));
+    // a block's two running sums (low, high) are independent folds: two tasks
+    parallel_tasks(2 * nbt + nwt, threads, [&](int64_t task) {
+      if (task < 2 * nbt) {
+        const int64_t b = b0 + task / 2;
+        const int64_t i1 = std::min(end, (b + 1) * kEvBlock);
+        double acc = -HUGE_VAL;
+        if (task & 1) {
+          for (int64_t i = b * kEvBlock; i < i1; ++i) acc = lse_host(acc, v.dh(i));
+          bhigh_[(size_t)b] = acc;
+        } else {
+          for (int64_t i = b * kEvBlock; i < i1; ++i) acc = lse_host(acc, v.dl(i));
+          blow_[(size_t)b] = acc;
         }
-        blow_[(size_t)b] = lo;
-        bhigh_[(size_t)b] = hi;
       } else {
-        const int64_t m0 = w0 + (task - nbt) * kWeightChunk;
+        const int64_t m0 = w0 + (task - 2 * nbt) * kWeightChunk;
         const int64_t m1 = std::min(wend, m0 + kWeightChunk);
         for (int64_t m = m0; m < m1; ++m) wts[m] = v.weight(m);
       }

@@ -108,6 +108,9 @@ struct NestArgs {
 #ifndef MCG_NEST_PREFETCH
 #define MCG_NEST_PREFETCH 4
 #endif
+#ifndef MCG_NEST_PFOLD
+#define MCG_NEST_PFOLD 1     // the walker's box prior folded into its constraint reduction
+#endif
 #ifndef MCG_NEST_SPEC
 #define MCG_NEST_SPEC 0      // experiment: walker steps in speculated pairs (slower: 28.3 -> 35.0 us at C3)
 #endif
@@ -351,6 +354,49 @@ struct WalkTarget {
     }
   }
 
+  // The step's constraint and box prior as ONE cross-lane reduction (MCG_NEST_PFOLD): a lane
+  // outside the box adds NaN to one of its canonical accumulators, inside it adds 0.0.  Every
+  // accumulator is a sum of squares started from +0.0, so x + 0.0 = x and S keeps its bits; a
+  // NaN makes S NaN, which the band test below counts as outside (!(S >= lo) is true for NaN),
+  // so the step rejects for any threshold -- as prior() = -inf would.  Inside the box the
+  // decision is constraint() && prior() > -inf exactly.  W = 4 register targets (the shell).
+  static constexpr bool kFold = kReg && LIK == MCG_LIK_GAUSS_SHELL && W == 4 && MCG_NEST_PFOLD;
+  __device__ __forceinline__ double lp_box() const { return (SYM || box) ? lp_in : 0.0; }
+  __device__ __forceinline__ bool constraint_box(const double* y, int sub, double thr) const {
+    double pen = 0.0;
+    if (SYM || box) {
+      int inb = 1;
+#pragma unroll
+      for (int j = 0; j < NL; ++j) {
+        if constexpr (SYM) inb &= (int)(__builtin_fabs(y[j]) <= hi[j]);
+        else inb &= (int)(y[j] >= lo[j]) & (int)(y[j] <= hi[j]);
+      }
+      pen = inb ? 0.0 : __builtin_nan("");
+    }
+    double A[Lay::NA];
+#pragma unroll
+    for (int j = 0; j < Lay::NA; ++j) A[j] = 0.0;
+#pragma unroll
+    for (int i = 0; i < Lay::NCL; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (!Lay::valid(sub, i, k)) continue;
+        const int j = 4 * i + k;
+        const double e = y[j] - m0[j];
+        A[i % Lay::NA] = fma(e, e, A[i % Lay::NA]);
+      }
+    A[Lay::NA - 1] = A[Lay::NA - 1] + pen;
+    const double S = reduce_canon<P>(A);
+    bool in = (S >= s_in_lo) & (S <= s_in_hi);
+    const bool out = !(S >= s_out_lo) | !(S <= s_out_hi);   // NaN: out
+    if (!(in | out)) {                               // guard band (rare): the exact evaluation
+      const double r = psqrt(S);
+      const double qq = (r - c0) * c1;
+      in = (c2 - 0.5 * qq * qq) >= thr;
+    }
+    return in;
+  }
+
   __device__ __forceinline__ double prior(const double* y, int sub, const MhArgs& a) const {
     if constexpr (!kReg) {
       return eval_prior<D, P>(y, sub, a, a.pri);
@@ -383,17 +429,77 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   NT_STAMP(0, 0);
   __shared__ double2 s_lt[kLogTabN];                 // math tables staged in LDS (gathers)
   const double2* nt = kNrmTab;   // (an LDS copy costs more to stage than its gathers save: 62 vs 52 us)
+  // The walker wave's first loads go out before the table staging and the stop test, so their
+  // latencies overlap instead of queueing one behind the other: the stop-test state, the
+  // target constants, the threshold, the retired slot, the first start candidate's ll / lp / row (accepted ~(n - k) / n
+  // of the time; the search below only runs when it fails), and with the draw table the first
+  // group's draws and the partner-row indices of the ring.  All are plain reads of buffers the
+  // previous kernels finished.
+  const bool stopped0 = nest_stopped(a.st);
+  const double st_lv = a.st->log_vol, st_mx = a.st->max_ll, st_est = a.st->est;
+  const bool st_err = __hip_atomic_load(&a.st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  const bool walker = !TAB || threadIdx.x < 64;       // wave-uniform
+  const int64_t tid = (int64_t)blockIdx.x * (TAB ? 64 : blockDim.x) + threadIdx.x;
+  const int sub = (int)(tid & (P - 1));
+  const int64_t w = tid / P;
+  const bool active = w < a.k;
+  // inactive lanes of a partial wave run walker 0's arithmetic (shuffle partners) but store nothing
+  const int64_t wc = active ? w : 0;
+  const Rng rng{a.k0, a.k1};
+  const uint32_t wid = (uint32_t)(a.mrep + wc);
+  const uint32_t n = (uint32_t)a.n;
+  constexpr int PD = kNestPrefetch;
+  const int64_t tbase = TAB ? walk_tab_base(a, a.mrep) : 0;
+  // per-lane entry pointers; step st (clamped to the last step) is at [st * k].  32-bit offsets
+  // (the table is skipped beyond 512 MB, so k nmcmc < 2^25): as 64-bit products with the clamp
+  // compare in VALU the eight entry addresses of a group cost ~80 SALU/VALU per group, issued by
+  // the walker's single wave on its SIMD
+  const double2* const tsc_lane = a.rt_sc + tbase + wc;
+  const unsigned long long* const tix_lane = a.rt_ix + tbase + wc;
+  const uint32_t tk = (uint32_t)a.k;
+  auto tab_off = [&](int64_t st) -> uint32_t { return (uint32_t)st * tk; };   // pad rows: no clamp
+  double thr = 0.0, ll_first = -__builtin_inf(), lp_first = 0.0;
+  int ret_slot = 0;
+  uint32_t s_first = 0;
+  double row_first[NL];
+  unsigned long long tix_cur[PD], tix_ring[PD];
+  double2 tsc_cur[PD];
+  WalkTarget<D, P, LIK, SYM> tgt;                    // the log-target's constants (registers)
+  if (walker) {
+    tgt.load(a.m, sub);
+    thr = a.key_ll[a.k - 1];
+    ret_slot = a.key_slot[wc];                         // the live slot walker w's point replaces
+    const u32x4 r = rng(wid, 0u, CALL_START, TAG_NEST_WALK, 0u);
+    s_first = randint(r.x, r.y, n);
+    ll_first = a.ll[s_first];
+    lp_first = a.lp[s_first];
+    const double* __restrict__ src = a.x + (int64_t)s_first * D;
+#pragma unroll
+    for (int i = 0; i < Lay::NCL; ++i)
+#pragma unroll
+      for (int q = 0; q < W; ++q)
+        row_first[W * i + q] = Lay::valid(sub, i, q) ? src[Lay::dim(sub, i, q)] : 0.0;
+    if constexpr (TAB) {
+#pragma unroll
+      for (int u = 0; u < PD; ++u) {
+        tix_ring[u] = tix_lane[tab_off(u)];
+        tsc_cur[u] = tsc_lane[tab_off(u)];
+        tix_cur[u] = tix_lane[tab_off(PD + u)];
+      }
+    }
+  }
   for (int i = threadIdx.x; i < kLogTabN; i += blockDim.x) s_lt[i] = kLogTab[i];
   __syncthreads();
-  if (nest_stopped(a.st)) return;
+  NT_STAMP(0, 1);
+  if (stopped0) return;
   if (a.mrep > 0) {
     // the previous generation's stop test (remaining_integral_negligable, nested.ml:45-48, on the
     // max live ll; or a failed draw, nested.ml:70-72), made by every workgroup from the same
     // inputs: a flag set inside a kernel could be seen by only some of its workgroups (a late
     // starter would skip its share of the work), so no kernel reads the flag it may set
-    const double live = a.st->log_vol + a.st->max_ll;
-    const bool err = __hip_atomic_load(&a.st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-    if (live - plse(a.st->est, live, s_lt) <= a.log_epsrel || err) {
+    const double live = st_lv + st_mx;
+    const bool err = st_err;
+    if (live - plse(st_est, live, s_lt) <= a.log_epsrel || err) {
       if (blockIdx.x == 0 && threadIdx.x == 0) {
         // the previous generation was the last: its pipelined full merge (still running on the
         // merge stream) completes; the ones after it skip
@@ -433,29 +539,22 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
       return;
     }
   }
-  const int64_t tid = (int64_t)blockIdx.x * (TAB ? 64 : blockDim.x) + threadIdx.x;
-  const int sub = (int)(tid & (P - 1));
-  const int64_t w = tid / P;
-  const bool active = w < a.k;
-  // inactive lanes of a partial wave run walker 0's arithmetic (shuffle partners) but store nothing
-  const int64_t wc = active ? w : 0;
-  const Rng rng{a.k0, a.k1};
-  const uint32_t wid = (uint32_t)(a.mrep + wc);
-  const double thr = a.key_ll[a.k - 1];
-  const int ret_slot = a.key_slot[wc];               // the live slot walker w's point replaces
-  const uint32_t n = (uint32_t)a.n;
   // start: a uniformly random live point satisfying the constraint (nested.ml:63); with k = 1
-  // every live point does, so this is Random.int nlive
-  int64_t start = -1;
-  for (uint32_t att = 0; att < 4096; ++att) {
-    const u32x4 r = rng(wid, att, CALL_START, TAG_NEST_WALK, 0u);
-    const uint32_t s = randint(r.x, r.y, n);
-    if (a.ll[s] >= thr) {
-      start = s;
-      break;
+  // every live point does, so this is Random.int nlive.  Attempt 0 was loaded above.
+  const bool first_ok = ll_first >= thr;
+  int64_t start = first_ok ? (int64_t)s_first : -1;
+  if (!first_ok) {
+    for (uint32_t att = 1; att < 4096; ++att) {
+      const u32x4 r = rng(wid, att, CALL_START, TAG_NEST_WALK, 0u);
+      const uint32_t s = randint(r.x, r.y, n);
+      if (a.ll[s] >= thr) {
+        start = s;
+        break;
+      }
     }
   }
   if (start < 0) start = a.key_slot[a.k - 1];
+  NT_STAMP(0, 2);
   double cur[NL], y[NL];
   auto load_row_at = [&](double* dst, const double* __restrict__ src) {
 #pragma unroll
@@ -496,12 +595,16 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
     const uint32_t jj = randint(ri.z, ri.w, n - 1);
     j = jj + (jj >= i ? 1u : 0u);
   };
-  WalkTarget<D, P, LIK, SYM> tgt;
-  tgt.load(a.m, sub);
   tgt.setup_constraint(thr);
-  load_row(cur, start);
-  double cur_l = (a.ll[start] >= thr) ? a.lp[start] : -__builtin_inf();   // mcmc_logl, :54-59
-  constexpr int PD = kNestPrefetch;
+  double cur_l;                                      // mcmc_logl, :54-59
+  if (first_ok) {
+#pragma unroll
+    for (int d = 0; d < NL; ++d) cur[d] = row_first[d];
+    cur_l = lp_first;
+  } else {
+    load_row(cur, start);
+    cur_l = (a.ll[start] >= thr) ? a.lp[start] : -__builtin_inf();
+  }
   // The random numbers of a group of PD steps are independent of the walker state.  With P = 4
   // lane q of the quad draws those of steps s0 + 4h + q (DE scale, accept uniform, and the DE
   // indices of step s0 + 4h + q + PD, whose rows refill that slot), one group AHEAD: the normal's
@@ -534,31 +637,15 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   // TAB: the generation's draws come from the table the previous merge filled (rt_ix, rt_sc),
   // loaded one group ahead like the rows: (scale, log u) of steps s0 + u and the refill indices
   // of steps s0 + PD + u
-  const int64_t tbase = TAB ? walk_tab_base(a, a.mrep) : 0;
-  // per-lane entry pointers; step st (clamped to the last step) is at [st * k].  32-bit offsets
-  // (the table is skipped beyond 512 MB, so k nmcmc < 2^25): as 64-bit products with the clamp
-  // compare in VALU the eight entry addresses of a group cost ~80 SALU/VALU per group, issued by
-  // the walker's single wave on its SIMD
-  const double2* const tsc_lane = a.rt_sc + tbase + wc;
-  const unsigned long long* const tix_lane = a.rt_ix + tbase + wc;
-  const uint32_t tk = (uint32_t)a.k;
-  auto tab_off = [&](int64_t st) -> uint32_t { return (uint32_t)st * tk; };   // pad rows: no clamp
-  unsigned long long tix_cur[PD], tix_next[PD];
-  double2 tsc_cur[PD], tsc_next[PD];
-  if constexpr (TAB) {
-#pragma unroll
-    for (int u = 0; u < PD; ++u) {
-      tsc_cur[u] = tsc_lane[tab_off(u)];
-      tix_cur[u] = tix_lane[tab_off(PD + u)];
-    }
-  }
+  unsigned long long tix_next[PD];
+  double2 tsc_next[PD];
   // partner rows of steps s .. s + PD - 1 in flight: ring slot u holds step s0 + u
   double bi[PD][NL], bj[PD][NL];
 #pragma unroll
   for (int u = 0; u < PD; ++u) {
     uint32_t i0, j0;
     if constexpr (TAB) {
-      const unsigned long long ix = tix_lane[tab_off(u)];
+      const unsigned long long ix = tix_ring[u];
       i0 = (uint32_t)ix;
       j0 = (uint32_t)(ix >> 32);
     } else {
@@ -594,6 +681,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   // v_mov + v_cmp_lt_i64 pair on the walker's issue-bound wave every step (nmcmc < 2^31: the
   // host caps it)
   const int nm = (int)a.nmcmc;
+  NT_STAMP(0, 3);
   for (int s0 = 0; s0 < nm; s0 += PD) {
     double dsc_g[PD], lu_g[PD];
     uint32_t ip_g[PD], jp_g[PD];
@@ -713,16 +801,29 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
       for (int d = 0; d < NL; ++d) y[d] = cur[d] + dsc_g[u] * (bj[u][d] - bi[u][d]);
       refill(bi[u], ip_g[u]);                          // refill slot u with step s + PD's rows
       refill(bj[u], jp_g[u]);
-      const bool ok = tgt.constraint(y, sub, a.m, thr);
-      const double lpy = tgt.prior(y, sub, a.m);
-      const double ml = ok ? lpy : -__builtin_inf();
       // mcmc.ml:47-48 computes (((ml + 0) - (cur_l + 0)) + 0) - 0 (flat proposal density); the
       // +0 / -0 terms change at most the sign of a zero, so `lu < ratio` is the same test
-      const double ratio = ml - cur_l;
-      if (live && lu_g[u] < ratio) {
+      if constexpr (WalkTarget<D, P, LIK, SYM>::kFold) {
+        // ml is lp_box when the proposal passes and -inf when it fails, and -inf - cur_l fails
+        // `lu < ratio` for every cur_l (-inf or NaN), so the step accepts iff it passes and
+        // lu < lp_box - cur_l: that half is ready before the reduction, off the serial chain
+        const double lpb = tgt.lp_box();
+        const bool pre = live && lu_g[u] < lpb - cur_l;
+        if (tgt.constraint_box(y, sub, thr) && pre) {
 #pragma unroll
-        for (int d = 0; d < NL; ++d) cur[d] = y[d];
-        cur_l = ml;
+          for (int d = 0; d < NL; ++d) cur[d] = y[d];
+          cur_l = lpb;
+        }
+      } else {
+        const bool ok = tgt.constraint(y, sub, a.m, thr);
+        const double lpy = tgt.prior(y, sub, a.m);
+        const double ml = ok ? lpy : -__builtin_inf();
+        const double ratio = ml - cur_l;
+        if (live && lu_g[u] < ratio) {
+#pragma unroll
+          for (int d = 0; d < NL; ++d) cur[d] = y[d];
+          cur_l = ml;
+        }
       }
     }
 #endif
@@ -736,6 +837,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
       gcur = gnext;
     }
   }
+  NT_STAMP(0, 4);
   const double nl = tgt.lik(cur, sub, a.m);
   const double np = tgt.prior(cur, sub, a.m);
   if (!active) return;
