@@ -6,6 +6,7 @@
 // which reproduces the reference's tie order (stable initial sort, nested.ml:132; a new point is
 // inserted before equal likelihoods, the strict > of nested.ml:36).
 #include <algorithm>
+#include <cstdlib>
 
 #include "mcg_nested_kernel.h"
 
@@ -525,30 +526,36 @@ __global__ void __launch_bounds__(256) merge_new_kernel(const NestArgs a, double
 // (two launches, 11.5 + 11.1 us at C3) becomes one launch.  An extra workgroup folds the running
 // estimate; every merge workgroup then takes a share of the new points' slot writes.
 constexpr int kSubCap = kSmallSort;
+#ifndef MCG_MERGE_BS
+#define MCG_MERGE_BS 256
+#endif
+constexpr int kMergeBS = MCG_MERGE_BS;
 #ifndef MCG_MERGE_UNROLL
 #define MCG_MERGE_UNROLL 16
 #endif
 
-__global__ void __launch_bounds__(256) merge_fused_kernel(const NestArgs a, double* oll, long long* otie,
-                                                          int* oslot) {
+template <int BS>   // workgroup size = survivors per workgroup
+__global__ void __launch_bounds__(BS) merge_fused_kernel(const NestArgs a, double* oll, long long* otie,
+                                                         int* oslot) {
   NT_STAMP(3, 0);
   if (nest_stopped(a.st)) return;                         // grid-uniform: set by an earlier launch
   const int64_t n = a.n, k = a.k, ns = n - k;
-  const int nblk = (int)((ns + 255) / 256);
+  const int nblk = (int)((ns + BS - 1) / BS);
   const int t = threadIdx.x;
   if ((int)blockIdx.x == nblk) {                          // the running estimate (retire wrote tv)
-    estimate_body<256>(a);
+    estimate_body<BS>(a);
     return;
   }
   __shared__ double s_nl[kSmallSort];                     // new ll by walker index j
-  __shared__ double s_sv_l[256];                          // this block's survivors
-  __shared__ long long s_sv_t[256];
+  __shared__ double s_sv_l[BS];                           // this block's survivors
+  __shared__ long long s_sv_t[BS];
   __shared__ short s_sub[kSubCap];                        // subset (new-key indices), then sorted
   __shared__ short s_srt[kSubCap];
-  __shared__ int s_scan[8];
+  constexpr int NW = BS / 64;                             // waves
+  __shared__ int s_scan[2 * NW];
   const int b = blockIdx.x;
-  const int64_t i0 = (int64_t)b * 256;
-  const int nsb = (int)min((int64_t)256, ns - i0);
+  const int64_t i0 = (int64_t)b * BS;
+  const int nsb = (int)min((int64_t)BS, ns - i0);
   const double* sll = a.key_ll + k;
   const long long* stie = a.key_tie + k;
   const int* sslot = a.key_slot + k;
@@ -556,9 +563,9 @@ __global__ void __launch_bounds__(256) merge_fused_kernel(const NestArgs a, doub
   // loads: own survivor, the range's upper bound, the k new ll, and the first element of the
   // walkers' new points this thread copies into the slots they replace -- all in flight together
   // (the next walk reads the copied points after this kernel; nothing here reads them).  Element
-  // g of the k x D block goes to thread g mod (nblk * 256) of the merge workgroups.
+  // g of the k x D block goes to thread g mod (nblk * BS) of the merge workgroups.
   const int64_t D = a.row_bytes / 8, kD = a.fuse_retire ? a.k * D : 0;
-  const int64_t g0 = (int64_t)b * 256 + t, gstride = (int64_t)nblk * 256;
+  const int64_t g0 = (int64_t)b * BS + t, gstride = (int64_t)nblk * BS;
   int sj0 = 0;
   double cx0 = 0.0, cl0 = 0.0, cp0 = 0.0;
   int64_t d0 = -1;
@@ -580,14 +587,14 @@ __global__ void __launch_bounds__(256) merge_fused_kernel(const NestArgs a, doub
     kt = stie[i0 + t];
     ks = sslot[i0 + t];
   }
-  const bool has_hi = i0 + 256 < ns;
-  const double hi_l = has_hi ? sll[i0 + 256] : 0.0;
-  const long long hi_t = has_hi ? stie[i0 + 256] : 0;
-  constexpr int kPer = kSmallSort / 256;
+  const bool has_hi = i0 + BS < ns;
+  const double hi_l = has_hi ? sll[i0 + BS] : 0.0;
+  const long long hi_t = has_hi ? stie[i0 + BS] : 0;
+  constexpr int kPer = kSmallSort / BS;
   double nv[kPer];
 #pragma unroll
   for (int r = 0; r < kPer; ++r) {
-    const int64_t j = (int64_t)r * 256 + t;
+    const int64_t j = (int64_t)r * BS + t;
     nv[r] = a.newk_ll[j < k ? j : k - 1];
   }
   if (g0 < kD) {
@@ -613,14 +620,14 @@ __global__ void __launch_bounds__(256) merge_fused_kernel(const NestArgs a, doub
   }
 #pragma unroll
   for (int r = 0; r < kPer; ++r) {
-    const int64_t j = (int64_t)r * 256 + t;
+    const int64_t j = (int64_t)r * BS + t;
     if (j < k) s_nl[j] = nv[r];
   }
   __syncthreads();
   NT_STAMP(3, 1);
   const double lo_l = s_sv_l[0];
   const long long lo_t = s_sv_t[0];
-  // classify this thread's new keys j = r * 256 + t: below the range, or inside it.  Subset
+  // classify this thread's new keys j = r * BS + t: below the range, or inside it.  Subset
   // offsets come from wave ballots (the r-th key of every lane: its rank among the wave's set
   // bits), the wave totals go through LDS; c_lo is summed the same way (integers: exact in any
   // order).  The subset order does not matter: it is ranked by counting below.
@@ -628,7 +635,7 @@ __global__ void __launch_bounds__(256) merge_fused_kernel(const NestArgs a, doub
   int wsub = 0, wbelow = 0;                               // wave-uniform
 #pragma unroll MCG_MERGE_UNROLL
   for (int r = 0; r < kPer; ++r) {
-    const int64_t j = (int64_t)r * 256 + t;
+    const int64_t j = (int64_t)r * BS + t;
     const bool ok = j < k;
     const double x = nv[r];
     const long long xt = tie0 - j;
@@ -642,27 +649,30 @@ __global__ void __launch_bounds__(256) merge_fused_kernel(const NestArgs a, doub
   const int lane = t & 63, wv = t >> 6;
   if (lane == 0) {
     s_scan[wv] = wsub;                                    // wave totals
-    s_scan[4 + wv] = wbelow;
+    s_scan[NW + wv] = wbelow;
   }
   __syncthreads();
-  int o = 0;
+  int o = 0, m = 0;
+  int64_t c_lo = 0;
 #pragma unroll
-  for (int w2 = 0; w2 < 4; ++w2) o += w2 < wv ? s_scan[w2] : 0;
-  const int m = s_scan[0] + s_scan[1] + s_scan[2] + s_scan[3];
-  const int64_t c_lo = (int64_t)s_scan[4] + s_scan[5] + s_scan[6] + s_scan[7];
+  for (int w2 = 0; w2 < NW; ++w2) {
+    o += w2 < wv ? s_scan[w2] : 0;
+    m += s_scan[w2];
+    c_lo += s_scan[NW + w2];
+  }
 #pragma unroll MCG_MERGE_UNROLL
   for (int r = 0; r < kPer; ++r) {
     const bool in = (inmask >> r) & 1u;
     const unsigned long long bm = __ballot(in);
     const int below_lane = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
-    if (in) s_sub[o + below_lane] = (short)(r * 256 + t);
+    if (in) s_sub[o + below_lane] = (short)(r * BS + t);
     o += __popcll(bm);
   }
   __syncthreads();
   NT_STAMP(3, 2);
   // rank the subset among itself (counting), place it sorted, write the subset keys out
-  for (int e = t; e < m; e += 256) {
+  for (int e = t; e < m; e += BS) {
     const int j = s_sub[e];
     const double x = s_nl[j];
     const long long xt = tie0 - j;
@@ -720,8 +730,20 @@ __global__ void __launch_bounds__(256) merge_fused_kernel(const NestArgs a, doub
 
 hipError_t launch_merge_fused(const NestArgs& a, double* oll, long long* otie, int* oslot, hipStream_t s) {
   if (a.k > kSmallSort || a.k < 1 || !a.est_in_rank) return hipErrorInvalidValue;
-  const unsigned nblk = (unsigned)((a.n - a.k + 255) / 256);
-  hipLaunchKernelGGL(merge_fused_kernel, dim3(nblk + 1), dim3(256), 0, s, a, oll, otie, oslot);
+  // survivors per workgroup (MCG_NESTED_MERGE_BS): every workgroup stages and classifies all k
+  // new keys, so fewer, wider workgroups divide that work over more threads
+  static const int bs = [] {
+    const char* e = std::getenv("MCG_NESTED_MERGE_BS");
+    const int v = e ? std::atoi(e) : kMergeBS;
+    return (v == 256 || v == 512 || v == 1024) ? v : kMergeBS;
+  }();
+  const unsigned nblk = (unsigned)((a.n - a.k + bs - 1) / bs);
+  if (bs == 1024)
+    hipLaunchKernelGGL(merge_fused_kernel<1024>, dim3(nblk + 1), dim3(1024), 0, s, a, oll, otie, oslot);
+  else if (bs == 512)
+    hipLaunchKernelGGL(merge_fused_kernel<512>, dim3(nblk + 1), dim3(512), 0, s, a, oll, otie, oslot);
+  else
+    hipLaunchKernelGGL(merge_fused_kernel<256>, dim3(nblk + 1), dim3(256), 0, s, a, oll, otie, oslot);
   return hipGetLastError();
 }
 
