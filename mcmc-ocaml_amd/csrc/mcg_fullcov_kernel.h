@@ -94,6 +94,13 @@ __device__ __forceinline__ void transpose_quadrants(double* v) {
 #ifndef MCG_FC_NRM_BATCH
 #define MCG_FC_NRM_BATCH 1   // the four normals of a Philox call gather together (one LDS wait)
 #endif
+#ifndef MCG_FC_SELECT_UNCOND
+// experiment: the accept select reads the park unconditionally.  Left as `acc ? park : x` the
+// compiler sinks each read under its own exec-masked branch (16 branch pairs, ~80 SALU a step),
+// but only accepting lanes read: same-box A/B 10.67 (branches) vs 11.04 ms (unconditional) per
+// launch -- the park reads cost more LDS time than the branches cost issue slots
+#define MCG_FC_SELECT_UNCOND 0
+#endif
 #ifndef MCG_FC_PIPE
 #define MCG_FC_PIPE 0        // experiment: each normal's table rows gathered one normal ahead
 #endif
@@ -322,7 +329,8 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
     const bool acc = lu < ratio;
 #pragma unroll
     for (int kb = 0; kb < NL; ++kb) {
-      const double yv = ypark[kb * kFcBlock];
+      double yv = ypark[kb * kFcBlock];
+      if constexpr (MCG_FC_SELECT_UNCOND) asm volatile("" : "+v"(yv));
       x[kb] = acc ? yv : x[kb];
     }
     if (acc) {
