@@ -101,6 +101,9 @@ __device__ __forceinline__ void transpose_quadrants(double* v) {
 // launch -- the park reads cost more LDS time than the branches cost issue slots
 #define MCG_FC_SELECT_UNCOND 0
 #endif
+#ifndef MCG_FC_RNG_AHEAD
+#define MCG_FC_RNG_AHEAD 1
+#endif
 #ifndef MCG_FC_PIPE
 #define MCG_FC_PIPE 0        // experiment: each normal's table rows gathered one normal ahead
 #endif
@@ -234,6 +237,13 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
   }
 
   double lu_own = 0.0;
+#if MCG_FC_RNG_AHEAD
+  // Philox words one call ahead: call m + 1's (or the next step's call 0) are drawn right after
+  // call m's normals, so their serial rounds issue between call m's MFMAs (the matrix pipe takes
+  // one per ~66 clocks from a wave) instead of ahead of the next call's normals.  The words depend
+  // only on (chain, step, call), never on the chain state.
+  u32x4 w_ahead = rng(gid, (uint32_t)a.step_base, (uint32_t)q, TAG_MH, (uint32_t)(a.step_base >> 32));
+#endif
   for (int64_t t = 0; t < a.nsteps; ++t) {
     const uint64_t T = a.step_base + (uint64_t)t;
     const uint32_t tlo = (uint32_t)T, thi = (uint32_t)(T >> 32);
@@ -276,7 +286,11 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
       }
       wcur = wnext;
 #else
+#if MCG_FC_RNG_AHEAD
+      const u32x4 w = w_ahead;
+#else
       const u32x4 w = rng(gid, tlo, (uint32_t)(4 * m + q), TAG_MH, thi);
+#endif
 #if MCG_FC_NRM_BATCH
       pnormal4_lds(w, s_nt, v);
 #else
@@ -284,6 +298,14 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
       v[1] = pnormal(w.y, s_nt);
       v[2] = pnormal(w.z, s_nt);
       v[3] = pnormal(w.w, s_nt);
+#endif
+#if MCG_FC_RNG_AHEAD
+      if (m + 1 < F::NM) {
+        w_ahead = rng(gid, tlo, (uint32_t)(4 * (m + 1) + q), TAG_MH, thi);
+      } else {
+        const uint64_t T1 = T + 1;
+        w_ahead = rng(gid, (uint32_t)T1, (uint32_t)q, TAG_MH, (uint32_t)(T1 >> 32));
+      }
 #endif
 #endif
       transpose_quadrants(v);                 // v[k'] = z[16 m + 4 k' + q]
