@@ -546,11 +546,11 @@ __global__ void __launch_bounds__(BS) merge_fused_kernel(const NestArgs a, doubl
     estimate_body<BS>(a);
     return;
   }
-  __shared__ double s_nl[kSmallSort];                     // new ll by walker index j
   __shared__ double s_sv_l[BS];                           // this block's survivors
   __shared__ long long s_sv_t[BS];
-  __shared__ short s_sub[kSubCap];                        // subset (new-key indices), then sorted
-  __shared__ short s_srt[kSubCap];
+  __shared__ double s_subl[kSubCap];                      // subset: new ll and walker index j,
+  __shared__ short s_sub[kSubCap];                        // in gather order
+  __shared__ short s_srt[kSubCap];                        // subset positions in key order
   constexpr int NW = BS / 64;                             // waves
   __shared__ int s_scan[2 * NW];
   const int b = blockIdx.x;
@@ -587,6 +587,8 @@ __global__ void __launch_bounds__(BS) merge_fused_kernel(const NestArgs a, doubl
     kt = stie[i0 + t];
     ks = sslot[i0 + t];
   }
+  const double lo_l = sll[i0];                            // the range: [s[i0], s[i0 + BS])
+  const long long lo_t = stie[i0];
   const bool has_hi = i0 + BS < ns;
   const double hi_l = has_hi ? sll[i0 + BS] : 0.0;
   const long long hi_t = has_hi ? stie[i0 + BS] : 0;
@@ -614,19 +616,8 @@ __global__ void __launch_bounds__(BS) merge_fused_kernel(const NestArgs a, doubl
       a.lp[sj] = a.nlp[j];
     }
   }
-  if (t < nsb) {
-    s_sv_l[t] = kl;
-    s_sv_t[t] = kt;
-  }
-#pragma unroll
-  for (int r = 0; r < kPer; ++r) {
-    const int64_t j = (int64_t)r * BS + t;
-    if (j < k) s_nl[j] = nv[r];
-  }
-  __syncthreads();
-  NT_STAMP(3, 1);
-  const double lo_l = s_sv_l[0];
-  const long long lo_t = s_sv_t[0];
+  // the new ll stay in registers: classified as they land, and only the block's subset goes to
+  // LDS (no staging of all k of them, and no barrier before the classification)
   // classify this thread's new keys j = r * BS + t: below the range, or inside it.  Subset
   // offsets come from wave ballots (the r-th key of every lane: its rank among the wave's set
   // bits), the wave totals go through LDS; c_lo is summed the same way (integers: exact in any
@@ -645,6 +636,11 @@ __global__ void __launch_bounds__(BS) merge_fused_kernel(const NestArgs a, doubl
     inmask |= (in ? 1u : 0u) << r;
     wsub += __popcll(__ballot(in));
     wbelow += __popcll(__ballot(ok & !ge_lo));
+  }
+  NT_STAMP(3, 1);
+  if (t < nsb) {
+    s_sv_l[t] = kl;
+    s_sv_t[t] = kt;
   }
   const int lane = t & 63, wv = t >> 6;
   if (lane == 0) {
@@ -666,7 +662,10 @@ __global__ void __launch_bounds__(BS) merge_fused_kernel(const NestArgs a, doubl
     const unsigned long long bm = __ballot(in);
     const int below_lane = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
-    if (in) s_sub[o + below_lane] = (short)(r * BS + t);
+    if (in) {
+      s_sub[o + below_lane] = (short)(r * BS + t);
+      s_subl[o + below_lane] = nv[r];
+    }
     o += __popcll(bm);
   }
   __syncthreads();
@@ -674,15 +673,13 @@ __global__ void __launch_bounds__(BS) merge_fused_kernel(const NestArgs a, doubl
   // rank the subset among itself (counting), place it sorted, write the subset keys out
   for (int e = t; e < m; e += BS) {
     const int j = s_sub[e];
-    const double x = s_nl[j];
+    const double x = s_subl[e];
     const long long xt = tie0 - j;
     int lr = 0;
 #pragma unroll 8
-    for (int q = 0; q < m; ++q) {                         // broadcast LDS reads, 8 in flight
-      const int jq = s_sub[q];
-      lr += key_less(s_nl[jq], tie0 - jq, x, xt) ? 1 : 0;
-    }
-    s_srt[lr] = (short)j;
+    for (int q = 0; q < m; ++q)                           // broadcast LDS reads, independent
+      lr += key_less(s_subl[q], tie0 - s_sub[q], x, xt) ? 1 : 0;
+    s_srt[lr] = (short)e;
     int lo = 0, hi = nsb;                                 // block survivors below x
     while (lo < hi) {
       const int md = (lo + hi) >> 1;
@@ -708,8 +705,8 @@ __global__ void __launch_bounds__(BS) merge_fused_kernel(const NestArgs a, doubl
     int lo = 0, hi = m;
     while (lo < hi) {
       const int md = (lo + hi) >> 1;
-      const int jm = s_srt[md];
-      if (key_less(s_nl[jm], tie0 - jm, kl, kt)) lo = md + 1;
+      const int em = s_srt[md];
+      if (key_less(s_subl[em], tie0 - s_sub[em], kl, kt)) lo = md + 1;
       else hi = md;
     }
     const int64_t pos = i0 + t + c_lo + lo;
