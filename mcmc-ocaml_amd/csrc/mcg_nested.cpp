@@ -374,6 +374,12 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   if (const char* e = std::getenv("MCG_NEST_LANES"))
     a.lanes_hint = !std::strcmp(e, "wide") ? -1 : !std::strcmp(e, "narrow") ? -2 : std::atoi(e);
   a.fuse_retire = a.est_in_rank && std::getenv("MCG_NESTED_RETIRE_KERNEL") == nullptr;
+  // walker steps resolved in pairs across lane quads (nest_walk_pair_kernel) where the target
+  // allows it (box-folded register targets at 4 lanes, e.g. the shell at D = 16)
+  {
+    const char* e = std::getenv("MCG_NESTED_PAIR");
+    a.walk_pair = e ? std::atoi(e) : 0;
+  }
   // pipelined merges (MCG_NESTED_PIPE=1): the full n-key merge of generation g
   // runs on a second stream beside rank count g + 1 and the next walk reads only the k lowest
   // keys (a 2k-key head merge).  Measured slower than the serial merge (the cross-stream event

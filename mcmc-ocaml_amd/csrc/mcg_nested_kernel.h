@@ -79,6 +79,7 @@ struct NestArgs {
                             // put the new points into the freed slots
   int32_t sym_box;          // box prior with lo[d] == -hi[d] for every d: tested as |y| <= hi
   int32_t lanes_hint;       // lanes per walker requested by MCG_NEST_LANES (0: the default)
+  int32_t walk_pair;        // nest_walk_pair_kernel where it applies (MCG_NESTED_PAIR)
   int32_t pipe;             // pipelined key merges: the walk reads the head keys
                             // (the k lowest), the full merge runs on a second stream beside the
                             // next walk and skips generations past st->stop_gen only
@@ -858,6 +859,241 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   }
 }
 
+// ---- walker steps in resolved pairs across lanes (MCG_NEST_PAIR) ----
+// The same constrained DE walk as nest_walk_kernel (TAB, box-folded register target, 4 lanes per
+// walker), two steps at a time: step u's proposal y0 = cur + d_u and the two candidates of step
+// u + 1 -- ya = y0 + d_{u+1} if step u accepts, yr = cur + d_{u+1} if it rejects -- are judged
+// at once by three lane quads of the walker's 16-lane row (role 0: y0, 1: ya, 2: yr; role 3
+// repeats y0), and the two decisions resolve in order from one ballot of the three verdicts.
+// Every candidate is the arithmetic the serial walk would do, so the states are the same bit
+// for bit; a lane evaluates one candidate per PAIR of steps, so the serial chain per step is
+// halved.  A wave holds 4 walkers (16 per 512-thread workgroup: waves 0-3); waves 4-7 fill the
+// next generation's draw table and retire the workgroup's dead rows, at priority 0 on the SIMDs
+// the walkers hold at priority 3.
+template <int D, int LIK, bool SYM>
+__global__ void __launch_bounds__(512) nest_walk_pair_kernel(const NestArgs a) {
+  constexpr int P = 4;
+  using Lay = WalkLayout<D, P>;
+  using Tgt = WalkTarget<D, P, LIK, SYM>;
+  static_assert(Tgt::kFold && Lay::W == 4, "pair walker: box-folded 4-dim-block register targets");
+  constexpr int NL = Lay::NL;
+  constexpr int W = Lay::W;
+  constexpr int PD = kNestPrefetch;
+  static_assert(PD % 2 == 0, "pairs of steps");
+  NT_STAMP(0, 0);
+  __shared__ double2 s_lt[kLogTabN];
+  const bool walker = threadIdx.x < 256;                  // waves 0-3; wave-uniform
+  const int lane = threadIdx.x & 63;
+  const int sub = lane & 3, role = (lane >> 2) & 3;
+  const int rowb = lane & ~15;                            // first lane of the walker's row
+  const int64_t w = (int64_t)blockIdx.x * 16 + ((threadIdx.x & 255) >> 4);
+  const bool active = w < a.k;
+  const int64_t wc = active ? w : 0;
+  const Rng rng{a.k0, a.k1};
+  const uint32_t wid = (uint32_t)(a.mrep + wc);
+  const uint32_t n = (uint32_t)a.n;
+  // first loads before the table staging and the stop test (as nest_walk_kernel)
+  const bool stopped0 = nest_stopped(a.st);
+  const double st_lv = a.st->log_vol, st_mx = a.st->max_ll, st_est = a.st->est;
+  const bool st_err = __hip_atomic_load(&a.st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  const int64_t tbase = walk_tab_base(a, a.mrep);
+  const double2* const tsc_lane = a.rt_sc + tbase + wc;
+  const unsigned long long* const tix_lane = a.rt_ix + tbase + wc;
+  const uint32_t tk = (uint32_t)a.k;
+  auto tab_off = [&](int64_t st) -> uint32_t { return (uint32_t)st * tk; };
+  double thr = 0.0, ll_first = -__builtin_inf(), lp_first = 0.0;
+  int ret_slot = 0;
+  uint32_t s_first = 0;
+  double row_first[NL];
+  unsigned long long tix_cur[PD], tix_ring[PD];
+  double2 tsc_cur[PD];
+  Tgt tgt;
+  if (walker) {
+    tgt.load(a.m, sub);
+    thr = a.key_ll[a.k - 1];
+    ret_slot = a.key_slot[wc];
+    const u32x4 r = rng(wid, 0u, CALL_START, TAG_NEST_WALK, 0u);
+    s_first = randint(r.x, r.y, n);
+    ll_first = a.ll[s_first];
+    lp_first = a.lp[s_first];
+    const double* __restrict__ src = a.x + (int64_t)s_first * D;
+#pragma unroll
+    for (int i = 0; i < Lay::NCL; ++i)
+#pragma unroll
+      for (int q = 0; q < W; ++q) row_first[W * i + q] = src[Lay::dim(sub, i, q)];
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+      tix_ring[u] = tix_lane[tab_off(u)];
+      tsc_cur[u] = tsc_lane[tab_off(u)];
+      tix_cur[u] = tix_lane[tab_off(PD + u)];
+    }
+  }
+  for (int i = threadIdx.x; i < kLogTabN; i += blockDim.x) s_lt[i] = kLogTab[i];
+  __syncthreads();
+  NT_STAMP(0, 1);
+  if (stopped0) return;
+  if (a.mrep > 0) {
+    // the previous generation's stop test, as nest_walk_kernel
+    const double live = st_lv + st_mx;
+    if (live - plse(st_est, live, s_lt) <= a.log_epsrel || st_err) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        __hip_atomic_store(&a.st->stop_gen, (long long)(a.mrep / a.k) - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        nest_set(&a.st->stopped);
+      }
+      return;
+    }
+  }
+  if (!walker) {
+    // waves 4-7: retire this workgroup's 16 walkers' points, then the next generation's table
+    if (a.fuse_retire) {
+      const int64_t w0 = (int64_t)blockIdx.x * 16;
+      for (int64_t e = threadIdx.x - 256; e < 16 * D; e += 256) {
+        const int64_t wj = w0 + e / D;
+        const int d = (int)(e % D);
+        if (wj >= a.k) break;
+        const int rs = a.key_slot[wj];
+        const int64_t m = a.mrep + wj;
+        a.dead_x[m * D + d] = a.x[(int64_t)rs * D + d];
+        if (d == 0) {
+          const double lls = a.ll[rs];
+          a.dead_ll[m] = lls;
+          a.dead_lp[m] = a.lp[rs];
+          const double lv = a.st->log_vol + a.prefix[wj];
+          __hip_atomic_store(a.tv + wj, lls + (lv + a.qadd[wj]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          a.rank[wj] = 0;
+        }
+      }
+    }
+    walk_draws_fill(a, a.mrep + a.k, (int64_t)blockIdx.x * 256 + (threadIdx.x - 256), (int64_t)gridDim.x * 256, s_lt);
+    return;
+  }
+  __builtin_amdgcn_s_setprio(3);
+  const bool first_ok = ll_first >= thr;
+  int64_t start = first_ok ? (int64_t)s_first : -1;
+  if (!first_ok) {
+    for (uint32_t att = 1; att < 4096; ++att) {
+      const u32x4 r = rng(wid, att, CALL_START, TAG_NEST_WALK, 0u);
+      const uint32_t sx = randint(r.x, r.y, n);
+      if (a.ll[sx] >= thr) {
+        start = sx;
+        break;
+      }
+    }
+  }
+  if (start < 0) start = a.key_slot[a.k - 1];
+  NT_STAMP(0, 2);
+  const char* const xb = (const char*)a.x;
+  const uint32_t lane_b = 8u * W * (uint32_t)sub;
+  auto refill = [&](double* dst, uint32_t v) {
+    const char* src = xb + (v + lane_b);
+#pragma unroll
+    for (int i = 0; i < Lay::NCL; ++i)
+#pragma unroll
+      for (int q = 0; q < W; ++q) dst[W * i + q] = *(const double*)(src + 8 * (W * P * i + q));
+  };
+  tgt.setup_constraint(thr);
+  double cur[NL];
+  double cur_l;
+  if (first_ok) {
+#pragma unroll
+    for (int d = 0; d < NL; ++d) cur[d] = row_first[d];
+    cur_l = lp_first;
+  } else {
+    const double* __restrict__ src = a.x + start * D;
+#pragma unroll
+    for (int i = 0; i < Lay::NCL; ++i)
+#pragma unroll
+      for (int q = 0; q < W; ++q) cur[W * i + q] = src[Lay::dim(sub, i, q)];
+    cur_l = (a.ll[start] >= thr) ? a.lp[start] : -__builtin_inf();
+  }
+  unsigned long long tix_next[PD];
+  double2 tsc_next[PD];
+  double bi[PD][NL], bj[PD][NL];
+#pragma unroll
+  for (int u = 0; u < PD; ++u) {
+    refill(bi[u], (uint32_t)tix_ring[u]);
+    refill(bj[u], (uint32_t)(tix_ring[u] >> 32));
+  }
+  const double lpb = tgt.lp_box();
+  const int nm = (int)a.nmcmc;
+  NT_STAMP(0, 3);
+  for (int s0 = 0; s0 < nm; s0 += PD) {
+    double dsc_g[PD], lu_g[PD];
+    uint32_t ip_g[PD], jp_g[PD];
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+      dsc_g[u] = tsc_cur[u].x;
+      lu_g[u] = tsc_cur[u].y;
+      ip_g[u] = (uint32_t)tix_cur[u];
+      jp_g[u] = (uint32_t)(tix_cur[u] >> 32);
+    }
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+      tsc_next[u] = tsc_lane[tab_off(s0 + PD + u)];
+      tix_next[u] = tix_lane[tab_off(s0 + 2 * PD + u)];
+    }
+#pragma unroll
+    for (int u = 0; u < PD; u += 2) {
+      const bool live0 = s0 + u < nm, live1 = s0 + u + 1 < nm;
+      double y0[NL], ya[NL], yr[NL], yc[NL];
+#pragma unroll
+      for (int d = 0; d < NL; ++d) {
+        const double du = dsc_g[u] * (bj[u][d] - bi[u][d]);
+        const double dv = dsc_g[u + 1] * (bj[u + 1][d] - bi[u + 1][d]);
+        y0[d] = cur[d] + du;                          // step u from the current point
+        ya[d] = y0[d] + dv;                           // step u + 1 after an accept
+        yr[d] = cur[d] + dv;                          // step u + 1 after a reject
+        yc[d] = role == 1 ? ya[d] : role == 2 ? yr[d] : y0[d];
+      }
+      refill(bi[u], ip_g[u]);
+      refill(bj[u], jp_g[u]);
+      refill(bi[u + 1], ip_g[u + 1]);
+      refill(bj[u + 1], jp_g[u + 1]);
+      // mcmc.ml:47-48 as in nest_walk_kernel: ml is lp_box when the proposal passes, -inf when
+      // it fails; after an accept cur_l is lp_box, so step u + 1's test is lu < lp_box - lp_box
+      const bool pre0 = live0 && lu_g[u] < lpb - cur_l;
+      const bool pre1r = live1 && lu_g[u + 1] < lpb - cur_l;
+      const bool pre1a = live1 && lu_g[u + 1] < lpb - lpb;
+      const bool ok = tgt.constraint_box(yc, sub, thr);
+      const unsigned long long bm = __ballot(ok);
+      const bool okA = (bm >> (rowb + sub)) & 1ull;
+      const bool okB = (bm >> (rowb + 4 + sub)) & 1ull;
+      const bool okC = (bm >> (rowb + 8 + sub)) & 1ull;
+      const bool acc0 = okA && pre0;
+      const bool acc1 = acc0 ? (okB && pre1a) : (okC && pre1r);
+#pragma unroll
+      for (int d = 0; d < NL; ++d) {
+        const double c1 = acc0 ? y0[d] : cur[d];
+        cur[d] = acc1 ? (acc0 ? ya[d] : yr[d]) : c1;
+      }
+      cur_l = (acc0 || acc1) ? lpb : cur_l;
+    }
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+      tsc_cur[u] = tsc_next[u];
+      tix_cur[u] = tix_next[u];
+    }
+  }
+  NT_STAMP(0, 4);
+  const double nl = tgt.lik(cur, sub, a.m);
+  const double np = tgt.prior(cur, sub, a.m);
+  if (!active || role != 0) return;
+#pragma unroll
+  for (int i = 0; i < Lay::NCL; ++i)
+#pragma unroll
+    for (int q = 0; q < W; ++q) a.nx[w * D + Lay::dim(sub, i, q)] = cur[W * i + q];
+  if (sub == 0) {
+    a.nll[w] = nl;
+    a.nlp[w] = np;
+    if (a.fuse_retire) {
+      a.newk_ll[w] = nl;
+      a.newk_tie[w] = -(long long)(a.mrep + w + 1);
+      a.newk_slot[w] = ret_slot;
+    }
+    if (!(nl >= thr)) nest_set(&a.st->error);
+  }
+}
+
 // ---- prior draws of the initial live set (nested.ml:126-129, Stats.draw_uniform) ----
 template <int D, int LIK>
 __global__ void __launch_bounds__(256) nest_init_kernel(const NestArgs a, double* keys_ll,
@@ -884,6 +1120,14 @@ __global__ void __launch_bounds__(256) nest_init_kernel(const NestArgs a, double
   keys_slot[s] = (int)s;
 }
 
+// the pair walker applies to box-folded 4-dim-block register targets on 4 lanes (the layout is
+// checked before WalkTarget is instantiated: it static_asserts on invalid splits)
+template <int D, int LIK, int P>
+constexpr bool pair_walk_ok() {
+  if constexpr (P == 4 && D % 16 == 0 && LIK == MCG_LIK_GAUSS_SHELL) return WalkTarget<D, 4, LIK, true>::kFold;
+  else return false;
+}
+
 template <int D, int LIK, int P>
 hipError_t launch_nest_walk_p(const NestArgs& a, hipStream_t st) {
   // small workgroups: a generation has only k * P lanes, so one wave per workgroup spreads them
@@ -893,6 +1137,12 @@ hipError_t launch_nest_walk_p(const NestArgs& a, hipStream_t st) {
   // with the draw table: the same walker waves, each with three table-filling waves beside it
   const dim3 gt((unsigned)((a.k * P + 63) / 64)), bt(256);
   constexpr bool kSym = WalkTarget<D, P, LIK>::kReg;   // the |y| <= h form needs the register target
+  if constexpr (pair_walk_ok<D, LIK, P>()) {
+    if (a.rt_ix && a.sym_box && a.walk_pair) {
+      hipLaunchKernelGGL((nest_walk_pair_kernel<D, LIK, true>), dim3((unsigned)((a.k + 15) / 16)), dim3(512), 0, st, a);
+      return hipGetLastError();
+    }
+  }
   if (a.rt_ix && kSym && a.sym_box) hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, kSym>), gt, bt, 0, st, a);
   else if (a.rt_ix) hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, false>), gt, bt, 0, st, a);
   else hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, false, false>), dim3((unsigned)grid), dim3(block), 0, st, a);
