@@ -237,14 +237,15 @@ def test_nested_walker_box_forms_bit_exact(oracle, T, D, sym, diag):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("env", ["MCG_NESTED_NO_TABLE", "MCG_NESTED_RETIRE_KERNEL", "both", "MCG_NESTED_PIPE",
-                                 "MCG_NESTED_MERGE2"])
+                                 "MCG_NESTED_MERGE2", "MCG_NESTED_PAIR"])
 @pytest.mark.parametrize("D", [3, 16])
 def test_nested_alternate_paths_bit_exact(oracle, T, monkeypatch, env, D):
     """The paths the default run does not take: walkers drawing their own random numbers (no
     draw table: what a generation too big for the table uses), the separate retire kernel
-    (k > 4096 uses it), the pipelined head + full merges, and the two-launch counted-rank sort +
-    merge instead of the one-launch fused merge -- the same dead points as the oracle, bit for
-    bit."""
+    (k > 4096 uses it), the pipelined head + full merges, the two-launch counted-rank sort +
+    merge instead of the one-launch fused merge, and the walker with its steps resolved in pairs
+    across lane quads (D = 16: nest_walk_pair_kernel) -- the same dead points as the oracle, bit
+    for bit."""
     for var in (["MCG_NESTED_NO_TABLE", "MCG_NESTED_RETIRE_KERNEL"] if env == "both" else [env]):
         monkeypatch.setenv(var, "1")
     lik = T.gauss_shell(np.zeros(D), 1.0, 0.2)
