@@ -633,7 +633,7 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   for (auto& e : B.done)
     if (!e) HC(hipEventCreateWithFlags(&e, hipEventDisableTiming), "create event");
   int q = 0;
-  double t_launch = 0, t_wait = 0, t_fold = 0;
+  double t_launch = 0, t_wait = 0, t_fold = 0, t_first = -1;
   std::thread fw;                                     // fold worker (EvFold::advance)
   struct Joiner {
     std::thread& t;
@@ -650,6 +650,7 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   int64_t gstart[2] = {0, 0};
   bool inflight[2] = {false, false};
   gstart[q] = gen;
+  const double t_setup = ms(t_start, now());
   if ((rc = launch_batch(G, q))) return rc;
   inflight[q] = true;
   if (max_dead / k - gen > 0) {
@@ -664,6 +665,7 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
     const auto tw0 = now();
     HC(hipEventSynchronize(B.done[q]), "nested sync");
     t_wait += ms(tw0, now());
+    if (t_first < 0) t_first = ms(t_start, now());
     inflight[q] = false;
     st = hst[q];
     if (st.error) {
@@ -734,7 +736,9 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   }
 #endif
   if (prof)
-    std::fprintf(stderr, "mcg_nested: host launch %.1f ms, wait %.1f ms, fold join %.1f ms\n", t_launch, t_wait, t_fold);
+    std::fprintf(stderr, "mcg_nested: host launch %.1f ms, wait %.1f ms, fold join %.1f ms, setup %.2f ms, first batch done at %.2f ms, "
+                 "%lld generations launched for %lld run\n", t_launch, t_wait, t_fold, t_setup, t_first, (long long)gen,
+                 (long long)st.gen_done);
   // final: dead points in retirement order, then the live set ascending (nested.ml:143)
   const int64_t ndead = st.gen_done * k;
   const int64_t ntot = ndead + n;

@@ -489,8 +489,14 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
       }
     }
   }
-  for (int i = threadIdx.x; i < kLogTabN; i += blockDim.x) s_lt[i] = kLogTab[i];
-  __syncthreads();
+  // the log table: staged in LDS for the walkers that draw their own numbers; with the draw
+  // table the walkers need it only for the stop test and the filling waves gather from the
+  // global copy (as they do for the normal table), so there is no staging barrier to wait for
+  const double2* const lt = TAB ? kLogTab : s_lt;
+  if constexpr (!TAB) {
+    for (int i = threadIdx.x; i < kLogTabN; i += blockDim.x) s_lt[i] = kLogTab[i];
+    __syncthreads();
+  }
   NT_STAMP(0, 1);
   if (stopped0) return;
   if (a.mrep > 0) {
@@ -500,7 +506,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
     // starter would skip its share of the work), so no kernel reads the flag it may set
     const double live = st_lv + st_mx;
     const bool err = st_err;
-    if (live - plse(st_est, live, s_lt) <= a.log_epsrel || err) {
+    if (live - plse(st_est, live, lt) <= a.log_epsrel || err) {
       if (blockIdx.x == 0 && threadIdx.x == 0) {
         // the previous generation was the last: its pipelined full merge (still running on the
         // merge stream) completes; the ones after it skip
@@ -536,7 +542,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
           }
         }
       }
-      walk_draws_fill(a, a.mrep + a.k, (int64_t)blockIdx.x * nf + (threadIdx.x - 64), (int64_t)gridDim.x * nf, s_lt);
+      walk_draws_fill(a, a.mrep + a.k, (int64_t)blockIdx.x * nf + (threadIdx.x - 64), (int64_t)gridDim.x * nf, lt);
       return;
     }
   }
@@ -881,7 +887,6 @@ __global__ void __launch_bounds__(512) nest_walk_pair_kernel(const NestArgs a) {
   constexpr int PD = kNestPrefetch;
   static_assert(PD % 2 == 0, "pairs of steps");
   NT_STAMP(0, 0);
-  __shared__ double2 s_lt[kLogTabN];
   const bool walker = threadIdx.x < 256;                  // waves 0-3; wave-uniform
   const int lane = threadIdx.x & 63;
   const int sub = lane & 3, role = (lane >> 2) & 3;
@@ -928,14 +933,12 @@ __global__ void __launch_bounds__(512) nest_walk_pair_kernel(const NestArgs a) {
       tix_cur[u] = tix_lane[tab_off(PD + u)];
     }
   }
-  for (int i = threadIdx.x; i < kLogTabN; i += blockDim.x) s_lt[i] = kLogTab[i];
-  __syncthreads();
   NT_STAMP(0, 1);
   if (stopped0) return;
   if (a.mrep > 0) {
-    // the previous generation's stop test, as nest_walk_kernel
+    // the previous generation's stop test, as nest_walk_kernel (global log table: no staging)
     const double live = st_lv + st_mx;
-    if (live - plse(st_est, live, s_lt) <= a.log_epsrel || st_err) {
+    if (live - plse(st_est, live, kLogTab) <= a.log_epsrel || st_err) {
       if (blockIdx.x == 0 && threadIdx.x == 0) {
         __hip_atomic_store(&a.st->stop_gen, (long long)(a.mrep / a.k) - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         nest_set(&a.st->stopped);
@@ -964,7 +967,7 @@ __global__ void __launch_bounds__(512) nest_walk_pair_kernel(const NestArgs a) {
         }
       }
     }
-    walk_draws_fill(a, a.mrep + a.k, (int64_t)blockIdx.x * 256 + (threadIdx.x - 256), (int64_t)gridDim.x * 256, s_lt);
+    walk_draws_fill(a, a.mrep + a.k, (int64_t)blockIdx.x * 256 + (threadIdx.x - 256), (int64_t)gridDim.x * 256, kLogTab);
     return;
   }
   __builtin_amdgcn_s_setprio(3);
