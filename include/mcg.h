@@ -289,6 +289,19 @@ int mcg_nested_merge(int32_t nruns, const int64_t* n_total, const int64_t* nlive
                      const double* ll, int64_t* order, double* log_ev, double* log_dev,
                      double* log_wts);
 
+/* ---- evidence_error_and_weights (nested.ml:81-120) on the host ----
+   The fold mcg_nested runs beside the GPU, over a caller's points in nested_output order: ll
+   [ntot], the ntot - nlive dead points in retirement order then the nlive final live points
+   ascending; dead point i was retired with nlive - (i mod k) live points (k retirements per
+   generation; k = 1 is the reference's loop).  Writes log Z, log dZ and the normalised log
+   weights [ntot]: the same bits as mcg_nested's own (and the oracle's or_evidence_weights).
+   chunk > 0 streams the dead points in chunks of that many points first, as mcg_nested does
+   while the GPU runs (the result does not depend on the chunking); 0 folds everything at once.
+   Returns MCG_EINVAL unless 1 <= k < nlive <= ntot (as mcg_nested: retiring every live point in
+   one generation leaves no volume). */
+int mcg_evidence_weights(int64_t ntot, int64_t nlive, int64_t k, const double* ll, int64_t chunk,
+                         double* log_ev, double* log_dev, double* log_wts);
+
 /* ---- kD-tree evidence integrals over samples (Evidence.Make(MO), evidence.ml:66-221) ----
    pts [n][ndim] row-major, ll, lp [n]: one sample array (several chains: concatenated).
    evidence_direct ?n (evidence.ml:145-156): duplicates removed, kD tree of the samples

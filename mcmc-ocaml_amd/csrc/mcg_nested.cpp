@@ -918,6 +918,22 @@ int mcg_nested_get(mcg_ctx* ctx, double* pts, double* ll, double* lp, double* lo
   return MCG_OK;
 }
 
+int mcg_evidence_weights(int64_t ntot, int64_t nlive, int64_t k, const double* ll, int64_t chunk,
+                         double* log_ev, double* log_dev, double* log_wts) {
+  if (!ll || !log_ev || !log_dev || !log_wts || k < 1 || nlive <= k || ntot < nlive) return MCG_EINVAL;
+  try {
+    EvFold fold(nlive, k);
+    const int64_t ndead = ntot - nlive;
+    if (chunk > 0)
+      for (int64_t a = std::min(chunk, ndead); a <= ndead; a = (a == ndead) ? ndead + 1 : std::min(a + chunk, ndead))
+        fold.advance(ll, a, log_wts);
+    fold.finish(ll, ntot, log_wts, log_ev, log_dev);
+  } catch (const std::exception&) {
+    return MCG_EFAIL;
+  }
+  return MCG_OK;
+}
+
 // Run merging for nested replicas (one independent run per GPU).  A run with
 // constant live count n is n "threads"; merging runs adds their live counts at every likelihood
 // level, so R runs of n/R points each merge into one run of n points.  The volume and trapezoid

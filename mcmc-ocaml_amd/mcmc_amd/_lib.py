@@ -103,6 +103,7 @@ SIGNATURES = {
     "mcg_rj_get_models": ([C.c_void_p, C.POINTER(C.c_uint8), C.POINTER(C.c_uint8)], C.c_int),
     "mcg_rj_model_counts": ([C.c_void_p, _u64p, _u64p], C.c_int),
     "mcg_nested_merge": ([C.c_int32, _i64p, _i64p, _i64p, _dp, _i64p, _dp, _dp, _dp], C.c_int),
+    "mcg_evidence_weights": ([C.c_int64, C.c_int64, C.c_int64, _dp, C.c_int64, _dp, _dp, _dp], C.c_int),
     "mcg_get_kernel_timing": ([C.c_void_p, C.c_char_p, C.POINTER(McgKernelTiming)], C.c_int),
     "mcg_set_timing": ([C.c_void_p, C.c_int32], C.c_int),
     "mcg_sync": ([C.c_void_p], C.c_int),

@@ -88,6 +88,20 @@ def merge_runs(runs):
                         n_dead, n_gen, conv)
 
 
+def evidence_weights(ll, nlive, k=1, chunk=0):
+    """evidence_error_and_weights (nested.ml:81-120) on the host (include/mcg.h
+    mcg_evidence_weights): ll in nested_output order (dead points in retirement order, then the
+    nlive final live points ascending), k retirements per generation.  Returns (log Z, log dZ,
+    log weights) -- the fold mcg_nested runs beside the GPU; `chunk` > 0 streams the dead points
+    in chunks first, as the nested loop does."""
+    ll = np.ascontiguousarray(ll, np.float64)
+    w = np.zeros(len(ll))
+    le, ld = C.c_double(), C.c_double()
+    L.check(L.lib().mcg_evidence_weights(len(ll), int(nlive), int(k), L.dptr(ll), int(chunk), C.byref(le),
+                                         C.byref(ld), L.dptr(w)))
+    return le.value, ld.value, w
+
+
 def _ll(o):
     return np.asarray(o.ll if hasattr(o, "ll") else o[4], np.float64)
 
