@@ -514,10 +514,11 @@ __global__ void __launch_bounds__(256) merge_new_kernel(const NestArgs a, double
 }
 
 // One-kernel sort + merge of a generation's k <= 4096 unsorted new keys into the n - k survivors
-// (DESIGN.md §5.3, round 3).  Survivor block b (256 consecutive survivors s[256b, 256b + 256))
+// (DESIGN.md §5.3, round 3).  Survivor block b (BS = 256 consecutive survivors s[256b, 256b + 256))
 // owns the key range [s[256b], s[256b + 256]) (block 0 from -inf, the last block to +inf), so
-// every new key belongs to exactly one block.  Each block stages the k new ll in LDS (a new key's
-// tie, -(mrep + j + 1), is known from its index j) and finds
+// every new key belongs to exactly one block.  Each block loads the k new ll into registers (a
+// new key's tie, -(mrep + j + 1), is known from its index j), classifies them as they land (wave
+// ballots), and finds
 //   c_lo = #new keys below its range          (every new key below s[256b]),
 //   its subset: the new keys inside its range, ranked among themselves by counting;
 // then survivor i goes to  i + c_lo + #subset below it,  and subset key x to
