@@ -106,6 +106,21 @@ struct NestArgs {
 #define NT_STAMP(kid, slot) do {} while (0)
 #endif
 
+#ifndef MCG_MERGE_WT
+#define MCG_MERGE_WT 1   // the fused merge's outputs as sc1 (write-through) stores
+#endif
+#ifndef MCG_WALK_WT
+#define MCG_WALK_WT 0    // experiment: the walk's outputs and retired rows as sc1 stores
+#endif
+// an output store read by a later kernel: plain, or sc1 (a relaxed agent-scope atomic store:
+// written through and dropped from the XCD's L2, so less is left to write back when the kernel
+// ends)
+template <int WT, class T>
+__device__ __forceinline__ void wt_store(T* p, T v) {
+  if constexpr (WT != 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
 #ifndef MCG_NEST_PREFETCH
 #define MCG_NEST_PREFETCH 4
 #endif
@@ -531,11 +546,11 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
           if (wj >= a.k) break;
           const int rs = a.key_slot[wj];
           const int64_t m = a.mrep + wj;
-          a.dead_x[m * D + d] = a.x[(int64_t)rs * D + d];
+          wt_store<MCG_WALK_WT>(&a.dead_x[m * D + d], a.x[(int64_t)rs * D + d]);
           if (d == 0) {
             const double lls = a.ll[rs];
-            a.dead_ll[m] = lls;
-            a.dead_lp[m] = a.lp[rs];
+            wt_store<MCG_WALK_WT>(&a.dead_ll[m], lls);
+            wt_store<MCG_WALK_WT>(&a.dead_lp[m], a.lp[rs]);
             const double lv = a.st->log_vol + a.prefix[wj];
             __hip_atomic_store(a.tv + wj, lls + (lv + a.qadd[wj]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             a.rank[wj] = 0;
@@ -852,14 +867,14 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   for (int i = 0; i < Lay::NCL; ++i)
 #pragma unroll
     for (int q = 0; q < W; ++q)
-      if (Lay::valid(sub, i, q)) a.nx[w * D + Lay::dim(sub, i, q)] = cur[W * i + q];
+      if (Lay::valid(sub, i, q)) wt_store<MCG_WALK_WT>(&a.nx[w * D + Lay::dim(sub, i, q)], cur[W * i + q]);
   if (sub == 0) {
-    a.nll[w] = nl;
-    a.nlp[w] = np;
+    wt_store<MCG_WALK_WT>(&a.nll[w], nl);
+    wt_store<MCG_WALK_WT>(&a.nlp[w], np);
     if (a.fuse_retire) {                               // the new point's key
-      a.newk_ll[w] = nl;
-      a.newk_tie[w] = -(long long)(a.mrep + w + 1);
-      a.newk_slot[w] = ret_slot;
+      wt_store<MCG_WALK_WT>(&a.newk_ll[w], nl);
+      wt_store<MCG_WALK_WT>(&a.newk_tie[w], -(long long)(a.mrep + w + 1));
+      wt_store<MCG_WALK_WT>(&a.newk_slot[w], ret_slot);
     }
     if (!(nl >= thr)) nest_set(&a.st->error);        // nested.ml:70-72 -> Failure
   }

@@ -601,20 +601,20 @@ __global__ void __launch_bounds__(BS) merge_fused_kernel(const NestArgs a, doubl
     nv[r] = a.newk_ll[j < k ? j : k - 1];
   }
   if (g0 < kD) {
-    a.x[(int64_t)sj0 * D + d0] = cx0;
+    wt_store<MCG_MERGE_WT>(&a.x[(int64_t)sj0 * D + d0], cx0);
     if (d0 == 0) {
-      a.ll[sj0] = cl0;
-      a.lp[sj0] = cp0;
+      wt_store<MCG_MERGE_WT>(&a.ll[sj0], cl0);
+      wt_store<MCG_MERGE_WT>(&a.lp[sj0], cp0);
     }
   }
   for (int64_t g = g0 + gstride; g < kD; g += gstride) {   // k * D beyond one element a thread
     const int64_t j = g / D;
     const int64_t d = g - j * D;
     const int sj = a.newk_slot[j];
-    a.x[(int64_t)sj * D + d] = a.nx[g];
+    wt_store<MCG_MERGE_WT>(&a.x[(int64_t)sj * D + d], a.nx[g]);
     if (d == 0) {
-      a.ll[sj] = a.nll[j];
-      a.lp[sj] = a.nlp[j];
+      wt_store<MCG_MERGE_WT>(&a.ll[sj], a.nll[j]);
+      wt_store<MCG_MERGE_WT>(&a.lp[sj], a.nlp[j]);
     }
   }
   // the new ll stay in registers: classified as they land, and only the block's subset goes to
@@ -688,9 +688,9 @@ __global__ void __launch_bounds__(BS) merge_fused_kernel(const NestArgs a, doubl
       else hi = md;
     }
     const int64_t pos = i0 + lo + c_lo + lr;
-    oll[pos] = x;
-    otie[pos] = xt;
-    oslot[pos] = a.newk_slot[j];
+    wt_store<MCG_MERGE_WT>(&oll[pos], x);
+    wt_store<MCG_MERGE_WT>(&otie[pos], xt);
+    wt_store<MCG_MERGE_WT>(&oslot[pos], a.newk_slot[j]);
     if (pos % kKeySample == kKeySample - 1) {
       a.out_samp_ll[pos / kKeySample] = x;
       a.out_samp_tie[pos / kKeySample] = xt;
@@ -711,9 +711,9 @@ __global__ void __launch_bounds__(BS) merge_fused_kernel(const NestArgs a, doubl
       else hi = md;
     }
     const int64_t pos = i0 + t + c_lo + lo;
-    oll[pos] = kl;
-    otie[pos] = kt;
-    oslot[pos] = ks;
+    wt_store<MCG_MERGE_WT>(&oll[pos], kl);
+    wt_store<MCG_MERGE_WT>(&otie[pos], kt);
+    wt_store<MCG_MERGE_WT>(&oslot[pos], ks);
     if (pos % kKeySample == kKeySample - 1) {
       a.out_samp_ll[pos / kKeySample] = kl;
       a.out_samp_tie[pos / kKeySample] = kt;
