@@ -109,6 +109,9 @@ struct NestArgs {
 #ifndef MCG_MERGE_WT
 #define MCG_MERGE_WT 1   // the fused merge's outputs as sc1 (write-through) stores
 #endif
+#ifndef MCG_TAB_WT
+#define MCG_TAB_WT 0     // experiment: the draw table (9.8 MB a generation at C3) as sc1 stores
+#endif
 #ifndef MCG_WALK_WT
 #define MCG_WALK_WT 0    // experiment: the walk's outputs and retired rows as sc1 stores
 #endif
@@ -177,8 +180,15 @@ __device__ __forceinline__ void walk_draws_fill(const NestArgs& a, int64_t mrep,
     // byte offsets of the two rows: the walker adds them to the live set's base with no 64-bit
     // address arithmetic
     ix = (unsigned long long)((uint32_t)ix * a.row_bytes) | ((unsigned long long)((uint32_t)(ix >> 32) * a.row_bytes) << 32);
-    a.rt_ix[base + e] = ix;
-    a.rt_sc[base + e] = sc;
+    if constexpr (MCG_TAB_WT) {
+      wt_store<1>(&a.rt_ix[base + e], ix);
+      double* p = (double*)(a.rt_sc + base + e);
+      wt_store<1>(p, sc.x);
+      wt_store<1>(p + 1, sc.y);
+    } else {
+      a.rt_ix[base + e] = ix;
+      a.rt_sc[base + e] = sc;
+    }
   }
 }
 
