@@ -568,6 +568,10 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
         }
       }
       walk_draws_fill(a, a.mrep + a.k, (int64_t)blockIdx.x * nf + (threadIdx.x - 64), (int64_t)gridDim.x * nf, lt);
+#ifdef MCG_NEST_TRACE
+      if (a.trace && threadIdx.x == 64 && blockIdx.x < 1024)   // the table-filling waves' end
+        a.trace[((size_t)0 * 1024 + blockIdx.x) * 8 + 5] = wall_clock64();
+#endif
       return;
     }
   }
