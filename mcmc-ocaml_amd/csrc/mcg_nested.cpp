@@ -176,7 +176,9 @@ class EvFold {
   }
 
   // all ntot points known (ilive dead ones): fold the rest, combine, normalise
-  void finish(const double* ll, int64_t ntot, double* wts, double* log_ev, double* log_dev) {
+  // (normalise = false leaves wts[m] = log w_m + log Z: the caller subtracts *log_ev when it
+  // copies them out, the same subtraction as here)
+  void finish(const double* ll, int64_t ntot, double* wts, double* log_ev, double* log_dev, bool normalise = true) {
     const int64_t ilive = ntot - n_;
     View v{this, ll, ilive, 0.0};
     v.ntot = ntot;
@@ -201,6 +203,7 @@ class EvFold {
     }
     *log_ev = kLogHalf + lse_host(low, high);
     *log_dev = high + std::log1p(-std::exp(low - high));
+    if (!normalise) return;
     const double le = *log_ev;
     parallel_for(0, threads_, threads_, [&](int64_t t) {
       for (int64_t m = t * ntot / threads_; m < (t + 1) * ntot / threads_; ++m) wts[m] -= le;
@@ -788,7 +791,9 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
                  (long long)unsorted);
   }
   const auto t_copy = now();
-  fold.finish(R.ll.data(), ntot, R.wts.data(), &R.log_ev, &R.log_dev);
+  // the weights' normalisation (w - log Z) happens in mcg_nested_get's copy, not in a pass here
+  fold.finish(R.ll.data(), ntot, R.wts.data(), &R.log_ev, &R.log_dev, false);
+  R.wts_shift = R.log_ev;
   if (prof)
     std::fprintf(stderr, "mcg_nested: generations %.1f ms, final copies %.1f ms, weights %.1f ms\n",
                  ms(t_start, t_gen), ms(t_gen, t_copy), ms(t_copy, now()));
@@ -896,10 +901,13 @@ int mcg_nested_get(mcg_ctx* ctx, double* pts, double* ll, double* lp, double* lo
       if (a1 > a0) (void)madvise((void*)a0, a1 - a0, MADV_HUGEPAGE);
     }
     constexpr int kT = 8;
+    const double sh = R.wts_shift;
     auto work = [&](int t) {
       const size_t c0 = n * t / kT, c1 = n * (t + 1) / kT;
-      for (int q = 0; q < 3; ++q)
+      for (int q = 0; q < 2; ++q)
         if (dst[q]) std::copy(srcs[q] + c0, srcs[q] + c1, dst[q] + c0);
+      if (dst[2])                                     // log weights: normalised here (EvFold::finish)
+        for (size_t i = c0; i < c1; ++i) dst[2][i] = srcs[2][i] - sh;
     };
     if (n < ((size_t)1 << 16)) {
       work(0);

@@ -37,6 +37,7 @@ struct NestedState {
   // last run: ll, lp, wts of every point (dead in retirement order, then live ascending); the
   // rows of every point stay in the device dead buffer (the live rows gathered behind the dead)
   std::vector<double> ll, lp, wts;
+  double wts_shift = 0.0;                 // wts hold log weights + log Z; mcg_nested_get subtracts it
   int64_t n_total = 0, n_dead = 0, n_gen = 0, nlive = 0, ndim = 0;
   double log_ev = 0.0, log_dev = 0.0;
   bool converged = false;       // the stop test fired (false: max_dead reached first)
