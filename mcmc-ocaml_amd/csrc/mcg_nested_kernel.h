@@ -124,6 +124,9 @@ __device__ __forceinline__ void wt_store(T* p, T v) {
   else *p = v;
 }
 
+#ifndef MCG_NEST_BOX_SKIP
+#define MCG_NEST_BOX_SKIP 1   // the walker skips its box test once the constraint implies it
+#endif
 #ifndef MCG_NEST_PREFETCH
 #define MCG_NEST_PREFETCH 4
 #endif
@@ -343,8 +346,23 @@ struct WalkTarget {
       else { s_in_lo = inf; s_in_hi = -inf; }
       s_out_lo = (r_lo - band > 0.0) ? (r_lo - band) * (r_lo - band) : -inf;
       s_out_hi = (r_hi + band) * (r_hi + band);
+      // A point the band test can pass has S <= s_out_hi, so each |y_k - c_k| <= sqrt(S) up to
+      // the sum's rounding (< 1e-14 relative at D <= 64).  Once the box holds that whole ball
+      // (late generations: the shell well inside the prior box), no such point is outside the
+      // box and the box test cannot change a decision: the walk skips it (wave-uniform).
+      if constexpr (MCG_NEST_BOX_SKIP) {
+        const double R = sqrt(s_out_hi) * (1.0 + 1e-9) + 1e-300;
+        bool ok = s_out_hi >= 0.0 && R < inf;
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+          if constexpr (SYM) ok = ok && (__builtin_fabs(m0[j]) + R <= hi[j]);
+          else ok = ok && (m0[j] - R >= lo[j]) && (m0[j] + R <= hi[j]);
+        }
+        box_test = __ballot(!ok) != 0;
+      }
     }
   }
+  bool box_test = true;
 
   // lik(y) >= thr, exactly as the comparison of the evaluated likelihood (mcmc_logl, nested.ml:54-59)
   __device__ __forceinline__ bool constraint(const double* y, int sub, const MhArgs& a, double thr) const {
@@ -388,17 +406,8 @@ struct WalkTarget {
   // decision is constraint() && prior() > -inf exactly.  W = 4 register targets (the shell).
   static constexpr bool kFold = kReg && LIK == MCG_LIK_GAUSS_SHELL && W == 4 && MCG_NEST_PFOLD;
   __device__ __forceinline__ double lp_box() const { return (SYM || box) ? lp_in : 0.0; }
+  template <bool BOXT = true>   // BOXT = false: the box test is implied (box_test false)
   __device__ __forceinline__ bool constraint_box(const double* y, int sub, double thr) const {
-    double pen = 0.0;
-    if (SYM || box) {
-      int inb = 1;
-#pragma unroll
-      for (int j = 0; j < NL; ++j) {
-        if constexpr (SYM) inb &= (int)(__builtin_fabs(y[j]) <= hi[j]);
-        else inb &= (int)(y[j] >= lo[j]) & (int)(y[j] <= hi[j]);
-      }
-      pen = inb ? 0.0 : __builtin_nan("");
-    }
     double A[Lay::NA];
 #pragma unroll
     for (int j = 0; j < Lay::NA; ++j) A[j] = 0.0;
@@ -411,7 +420,16 @@ struct WalkTarget {
         const double e = y[j] - m0[j];
         A[i % Lay::NA] = fma(e, e, A[i % Lay::NA]);
       }
-    A[Lay::NA - 1] = A[Lay::NA - 1] + pen;
+    if (BOXT && (SYM || box)) {
+      int inb = 1;
+#pragma unroll
+      for (int j = 0; j < NL; ++j) {
+        if constexpr (SYM) inb &= (int)(__builtin_fabs(y[j]) <= hi[j]);
+        else inb &= (int)(y[j] >= lo[j]) & (int)(y[j] <= hi[j]);
+      }
+      const double pen = inb ? 0.0 : __builtin_nan("");
+      A[Lay::NA - 1] = A[Lay::NA - 1] + pen;
+    }
     const double S = reduce_canon<P>(A);
     bool in = (S >= s_in_lo) & (S <= s_in_hi);
     const bool out = !(S >= s_out_lo) | !(S <= s_out_hi);   // NaN: out
@@ -718,6 +736,10 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   // host caps it)
   const int nm = (int)a.nmcmc;
   NT_STAMP(0, 3);
+  // two copies of the loop: with the box test, and without it once the constraint implies it
+  // (setup_constraint: box_test is wave-uniform)
+  auto walk_loop = [&](auto box_t) {
+  constexpr bool kBoxT = decltype(box_t)::value;
   for (int s0 = 0; s0 < nm; s0 += PD) {
     double dsc_g[PD], lu_g[PD];
     uint32_t ip_g[PD], jp_g[PD];
@@ -845,7 +867,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
         // lu < lp_box - cur_l: that half is ready before the reduction, off the serial chain
         const double lpb = tgt.lp_box();
         const bool pre = live && lu_g[u] < lpb - cur_l;
-        if (tgt.constraint_box(y, sub, thr) && pre) {
+        if (tgt.template constraint_box<kBoxT>(y, sub, thr) && pre) {
 #pragma unroll
           for (int d = 0; d < NL; ++d) cur[d] = y[d];
           cur_l = lpb;
@@ -873,6 +895,9 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
       gcur = gnext;
     }
   }
+  };
+  if (tgt.box_test) walk_loop(std::true_type{});
+  else walk_loop(std::false_type{});
   NT_STAMP(0, 4);
   const double nl = tgt.lik(cur, sub, a.m);
   const double np = tgt.prior(cur, sub, a.m);

@@ -236,6 +236,33 @@ def test_nested_walker_box_forms_bit_exact(oracle, T, D, sym, diag):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("sym", [True, False])
+def test_nested_walker_box_skip_near_the_box_bit_exact(oracle, T, sym):
+    """The walker drops its box test once every point the constraint can pass lies inside the
+    box (setup_constraint's box_test, MCG_NEST_BOX_SKIP).  A shell off the origin whose outer
+    radius (1 + delta, shrinking as the threshold rises) reaches 1.5, the distance to the nearest
+    face, about ten generations before the stop: the run crosses from the tested to the skipped
+    regime near the boundary.  The dead points, stop generation, log Z and weights equal the
+    oracle's, which always tests the box.  (The origin-centred shells of the other tests sit
+    well inside their boxes and take the skip for most of their generations.)"""
+    D = 16
+    c = np.zeros(D)
+    c[0] = 0.8
+    lik = T.gauss_shell(c, 1.0, 0.2)
+    if sym:
+        pri = T.box(-2.3 * np.ones(D), 2.3 * np.ones(D))
+    else:
+        lo = -2.4 * np.ones(D)
+        hi = 2.4 * np.ones(D)
+        lo[3], hi[0] = -1.5, 2.3
+        pri = T.box(lo, hi)
+    g = gpu_nested(lik, pri, 41, nlive=400, nmcmc=15, mode_hopping_frac=0.1, k=40)
+    o = oracle_nested(oracle, lik, pri, 41, nlive=400, nmcmc=15, mode_hop=0.1, k=40)
+    assert g.converged
+    assert_nested_same(g, o)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("env", ["MCG_NESTED_NO_TABLE", "MCG_NESTED_RETIRE_KERNEL", "both", "MCG_NESTED_PIPE",
                                  "MCG_NESTED_MERGE2", "MCG_NESTED_PAIR"])
 @pytest.mark.parametrize("D", [3, 16])
