@@ -52,7 +52,7 @@ def analytic_log_z(mu, sg, lo=-10.0, hi=10.0):
 
 
 def cpu_baseline(args, mu, sg, s):
-    """Oracle (C restatement, -O2) on a bounded sample of the same workload, all granted cores."""
+    """Oracle (C restatement, -O3 -march=x86-64-v3) on a bounded sample of the same workload, all granted cores."""
     import oracle as O
     D = args.ndim
     threads = int(os.environ.get("MCG_CPU_THREADS", min(16, os.cpu_count() or 1)))
@@ -309,8 +309,8 @@ def log_evidence_line(nest, log_z_hm, lz_true):
 
 
 def ctx_lanes(ctx):
-    import os as _os
-    return int(_os.environ.get("MCG_LANES_PER_CHAIN", "0")) or "auto"
+    """Lanes per chain the timed launches used (the runtime's choice unless --lanes / env)."""
+    return ctx.lanes()
 
 
 if __name__ == "__main__":

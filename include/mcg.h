@@ -167,6 +167,8 @@ int mcg_run(mcg_ctx* ctx, const mcg_run_opts* opts);
 int mcg_get_records(mcg_ctx* ctx, double* rec_x, double* rec_ll, double* rec_lp,
                     uint64_t* accept_bits);
 int64_t mcg_last_run_steps(const mcg_ctx* ctx);
+/* lanes per chain the last MH run used (1, 2, 4 or 8; the auto choice or opts.lanes_per_chain) */
+int mcg_last_run_lanes(const mcg_ctx* ctx);
 
 /* ---- reversible-jump MCMC between two models (Mcmc.make_rjmcmc_sampler / rjmcmc_array,
    mcmc.ml:84-153) ----

@@ -760,6 +760,7 @@ int mcg_run(mcg_ctx* ctx, const mcg_run_opts* o) {
 }
 
 int64_t mcg_last_run_steps(const mcg_ctx* ctx) { return ctx ? ctx->last_nsteps : -1; }
+int mcg_last_run_lanes(const mcg_ctx* ctx) { return ctx ? ctx->lanes : -1; }
 
 int mcg_get_records(mcg_ctx* ctx, double* rec_x, double* rec_ll, double* rec_lp,
                     uint64_t* accept_bits) {

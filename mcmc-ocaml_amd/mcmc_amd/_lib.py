@@ -80,6 +80,7 @@ SIGNATURES = {
     "mcg_run": ([C.c_void_p, C.POINTER(McgRunOpts)], C.c_int),
     "mcg_get_records": ([C.c_void_p, _dp, _dp, _dp, _u64p], C.c_int),
     "mcg_last_run_steps": ([C.c_void_p], C.c_int64),
+    "mcg_last_run_lanes": ([C.c_void_p], C.c_int),
     "mcg_get_counters": ([C.c_void_p, _u64p, _u64p], C.c_int),
     "mcg_reset_counters": ([C.c_void_p], C.c_int),
     "mcg_num_tiles": ([C.c_void_p], C.c_int64),

@@ -116,6 +116,10 @@ class Context:
             bits = bits[:nsteps]
         return rx, rll, rlp, bits
 
+    def lanes(self):
+        """Lanes per chain of the last MH run (the runtime's auto choice unless set)."""
+        return int(L.lib().mcg_last_run_lanes(self._p))
+
     def counters(self):
         a = np.zeros(1, np.uint64); r = np.zeros(1, np.uint64)
         self._check(L.lib().mcg_get_counters(self._p, L.u64ptr(a), L.u64ptr(r)))

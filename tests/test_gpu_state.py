@@ -190,3 +190,18 @@ def test_failed_set_rjmcmc_leaves_counters_unchanged(oracle, T):
     assert ctx.counters() == before
     assert ctx.counters() == before                    # reading twice changes nothing either
     ctx.close()
+
+
+def test_last_run_lanes_reports_the_lane_split(T):
+    """mcg_last_run_lanes: the lanes per chain the last MH run used -- the runtime's auto choice
+    (4 for a D = 32 Gaussian that does not fill the chip on fewer lanes), or the caller's."""
+    from mcmc_amd import Context
+    lik, pri, prop, mu, sg = c2_model(T, D=32)
+    x0 = np.random.default_rng(5).normal(mu[:, None], sg[:, None], size=(32, 1024))
+    for want, expect in ((0, 4), (1, 1), (2, 2)):
+        with Context(seed=1, lanes_per_chain=want) as ctx:
+            ctx.set_model(lik, pri, prop)
+            ctx.init(x0)
+            ctx.run(nbin=4, nskip=1, n_rec=1, record_x=False, record_llp=False,
+                    record_accept=False, accumulate=False)
+            assert ctx.lanes() == expect
