@@ -104,20 +104,27 @@ __device__ __forceinline__ void transpose_quadrants(double* v) {
 #ifndef MCG_FC_RNG_AHEAD
 #define MCG_FC_RNG_AHEAD 1
 #endif
+#ifndef MCG_FC_YREG
+// column blocks of the proposed point kept in registers (the accept select is then a v_cndmask
+// pair per dim, no LDS write and exec-masked read); the rest is parked in LDS.  Since the
+// round-3 register savings the whole point fits beside the chain state at two waves per SIMD
+// (254 VGPRs, no scratch): same-box A/B at C5, 16 in registers 10.53 -> 10.19 ms per launch
+// (6.21e9 -> 6.42e9), 8 in registers 10.34 ms (profiles/r03/c5_yreg); bit-exact either way
+#define MCG_FC_YREG 64
+#endif
 #ifndef MCG_FC_PIPE
 #define MCG_FC_PIPE 0        // experiment: each normal's table rows gathered one normal ahead
 #endif
 
 // 512-thread workgroups, one per CU: eight waves = two per SIMD, sharing one copy of the tables
-// (the proposed point's 64 KB LDS park, below, leaves no room for two workgroups per CU)
 constexpr int kFcBlock = 512;
 
 // Per step: the lane's four Philox calls one at a time -> 4 normals -> quadrant
 // transpose -> 4 proposed coordinates; each coordinate's residual r = y - mu goes straight into
 // the matrix core (row blocks ib with 4 ib <= kb, four accumulators, kb ascending per block, so
-// every e_i is still the oracle's fma chain), and y itself is parked in LDS until the accept
-// test.  The proposed point thus never occupies registers: chain state, Welford accumulators
-// and the four MFMA accumulators fit the 256 registers of two waves per SIMD without spilling.
+// every e_i is still the oracle's fma chain), and y itself is kept until the accept test: in
+// registers (MCG_FC_YREG, default), or parked in LDS.  Chain state, Welford accumulators, the
+// proposed point and the four MFMA accumulators fit the 256 registers of two waves per SIMD.
 // UNI: one proposal scale and one box for every dim (MhArgs::uni): scalars, no per-step loads;
 // UNI == 2: the box is symmetric, [-h, h], tested as |y| <= h (mcg_mh_kernel.h)
 template <int D, int UNI>
@@ -130,7 +137,8 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
   // mu by lane quadrant, [q][kb] = mu[4 kb + q], then the likelihood normaliser C and the prior
   // box's log density (per-step global loads of these were in-order vmcnt waits on every step)
   __shared__ double s_mu[D + 2];
-  __shared__ double s_y[NL * kFcBlock];                  // proposed point, [kb][thread]
+  constexpr int YR = MCG_FC_YREG < NL ? MCG_FC_YREG : NL;  // column blocks kept in registers
+  __shared__ double s_y[(NL - YR > 0 ? NL - YR : 1) * kFcBlock];   // parked rest, [kb - YR][thread]
   for (int i = threadIdx.x; i < kLogTabN; i += blockDim.x) s_lt[i] = kLogTab[i];
   for (int i = threadIdx.x; i < kNrmTabN; i += blockDim.x) s_nt[i] = kNrmTab[i];
   for (int i = threadIdx.x; i < D; i += blockDim.x) s_mu[(i & 3) * (D / 4) + (i >> 2)] = a.lik[i];
@@ -161,7 +169,7 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
   const Rng rng{a.k0, a.k1};
   const uint32_t gid = a.chain_offset + (uint32_t)c;
   auto dim = [&](int kb) { return 4 * kb + q; };
-  double* const ypark = s_y + threadIdx.x;              // ypark[kb * kFcBlock]
+  double* const ypark = s_y + threadIdx.x;              // ypark[(kb - YR) * kFcBlock]
 
   double x[NL];
 #pragma unroll
@@ -255,6 +263,7 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
     asm volatile("" : "+s"(qpri), "+s"(qprop));
     // ---- proposal y = x + s z (mcmc.ml:41) fused with e = U (y - mu) on the matrix cores ----
     bool ok = true;
+    double yreg[YR > 0 ? YR : 1];
     dbl4 e[F::NIB];
 #pragma unroll
     for (int ib = 0; ib < F::NIB; ++ib) e[ib] = dbl4{0.0, 0.0, 0.0, 0.0};
@@ -314,7 +323,8 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
         const int kb = 4 * m + k2;
         const int d = dim(kb);
         const double yv = fma(UNI ? a.uni_s : qprop[d], v[k2], x[kb]);
-        ypark[kb * kFcBlock] = yv;
+        if (kb < YR) yreg[kb < YR ? kb : 0] = yv;
+        else ypark[(kb - YR) * kFcBlock] = yv;
         if constexpr (UNI == 2) ok = ok & (__builtin_fabs(yv) <= a.uni_hi);
         else ok = ok & (yv >= (UNI ? a.uni_lo : qpri[d])) & (yv <= (UNI ? a.uni_hi : qpri[D + d]));
         const double rv = yv - s_mu[q * NL + kb];
@@ -350,8 +360,10 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
     const double lu = __shfl(lu_own, (lane & 15) | (qq << 4), 64);
     const bool acc = lu < ratio;
 #pragma unroll
-    for (int kb = 0; kb < NL; ++kb) {
-      double yv = ypark[kb * kFcBlock];
+    for (int kb = 0; kb < YR; ++kb) x[kb] = acc ? yreg[kb] : x[kb];
+#pragma unroll
+    for (int kb = YR; kb < NL; ++kb) {
+      double yv = ypark[(kb - YR) * kFcBlock];
       if constexpr (MCG_FC_SELECT_UNCOND) asm volatile("" : "+v"(yv));
       x[kb] = acc ? yv : x[kb];
     }
