@@ -112,6 +112,13 @@ __device__ __forceinline__ void transpose_quadrants(double* v) {
 // (6.21e9 -> 6.42e9), 8 in registers 10.34 ms (profiles/r03/c5_yreg); bit-exact either way
 #define MCG_FC_YREG 64
 #endif
+#ifndef MCG_FC_M2LDS
+// experiment: the Welford M2 accumulators live in LDS ([kb / 2][thread] double2; 64 KB per
+// 512-thread workgroup) instead of 32 registers (223 VGPRs, still two waves per SIMD): same-box
+// A/B 10.21 -> 10.77 ms per launch, and 11.0 ms with MCG_FC_PIPE on top (profiles/r03/c5_m2lds);
+// bit-exact, left off
+#define MCG_FC_M2LDS 0
+#endif
 #ifndef MCG_FC_PIPE
 #define MCG_FC_PIPE 0        // experiment: each normal's table rows gathered one normal ahead
 #endif
@@ -184,12 +191,25 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
   auto hcs = [&](int l) -> double& { return s_hm[(2 * l + 1) * kFcBlock + threadIdx.x]; };
   double hm_pv = 0.0;
   bool hm_pok = false;
-  double rmean[NL], rm2[NL];
+  double rmean[NL];
+#if MCG_FC_M2LDS
+  static_assert(NL % 2 == 0, "M2 pairs");
+  __shared__ double2 s_m2[(NL / 2) * kFcBlock];
+  double2* const m2p = s_m2 + threadIdx.x;              // m2p[(kb / 2) * kFcBlock]
+#else
+  double rm2[NL];
+#endif
   if (accum) {
 #pragma unroll
     for (int kb = 0; kb < NL; ++kb) {
       rmean[kb] = a.mean[(int64_t)dim(kb) * N + c];
+#if MCG_FC_M2LDS
+      const double v2 = a.m2[(int64_t)dim(kb) * N + c];
+      if (kb & 1) m2p[(kb / 2) * kFcBlock].y = v2;
+      else m2p[(kb / 2) * kFcBlock].x = v2;
+#else
       rm2[kb] = a.m2[(int64_t)dim(kb) * N + c];
+#endif
     }
 #pragma unroll
     for (int l = 0; l < NH; ++l) {
@@ -224,6 +244,21 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
     if (accum) {
       const double inv = inv_pf;
       inv_pf = a.inv_n[R + 1 - a.next_r0];
+#if MCG_FC_M2LDS
+#pragma unroll
+      for (int kp = 0; kp < NL / 2; ++kp) {
+        double2 m2 = m2p[kp * kFcBlock];
+        const double d0 = x[2 * kp] - rmean[2 * kp];
+        const double n0 = fma(d0, inv, rmean[2 * kp]);
+        m2.x = fma(d0, x[2 * kp] - n0, m2.x);
+        rmean[2 * kp] = n0;
+        const double d1 = x[2 * kp + 1] - rmean[2 * kp + 1];
+        const double n1 = fma(d1, inv, rmean[2 * kp + 1]);
+        m2.y = fma(d1, x[2 * kp + 1] - n1, m2.y);
+        rmean[2 * kp + 1] = n1;
+        m2p[kp * kFcBlock] = m2;
+      }
+#else
 #pragma unroll
       for (int kb = 0; kb < NL; ++kb) {
         const double delta = x[kb] - rmean[kb];
@@ -231,6 +266,7 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
         rm2[kb] = fma(delta, x[kb] - mnew, rm2[kb]);
         rmean[kb] = mnew;
       }
+#endif
       const int jr = (int)(R & (P - 1));
       if (q == jr) {
         hm_pv = -ll;
@@ -404,7 +440,11 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
 #pragma unroll
     for (int kb = 0; kb < NL; ++kb) {
       a.mean[o + 4 * kb * n] = rmean[kb];
+#if MCG_FC_M2LDS
+      a.m2[o + 4 * kb * n] = (kb & 1) ? m2p[(kb / 2) * kFcBlock].y : m2p[(kb / 2) * kFcBlock].x;
+#else
       a.m2[o + 4 * kb * n] = rm2[kb];
+#endif
     }
     hm_flush((r - 1) & ~(int64_t)(P - 1));
 #pragma unroll
