@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define MCG_ABI_VERSION 2
+#define MCG_ABI_VERSION 3
 
 /* ---- status codes ---- */
 enum {
@@ -49,6 +49,13 @@ enum {
                                           Stats.log_gaussian (bin/gaussian_cauchy.ml:149-164)
    CAUCHY_DATA   : nd, data[nsamp*nd]     same with Stats.log_cauchy
    FLAT          : (none)                 ll = 0
+   GAUSS_MIX     : m, then per component  ll = log (sum_i exp g_i), g_i = Stats.log_multi_gaussian
+                   mu_i[D], sigma_i[D]    mu_i sigma_i x: the multimodal target of
+                                          test/nested_test.ml:41-64 (1 <= m <= MCG_LIK_MIX_MAX)
+   Any ndim >= 1 works for FLAT, DIAG_GAUSS, GAUSS_SHELL and GAUSS_MIX (FULLCOV_GAUSS: ndim <= 64):
+   a dimension without compiled kernels runs on the next compiled width with zero-padded dims
+   (zero likelihood terms, zero proposal steps, unbounded box); the padding never crosses this
+   boundary.  The DATA kinds take nd <= 4, the kD proposal the compiled widths only.
 */
 enum {
   MCG_LIK_FLAT = 0,
@@ -56,8 +63,10 @@ enum {
   MCG_LIK_FULLCOV_GAUSS = 2,
   MCG_LIK_GAUSS_SHELL = 3,
   MCG_LIK_GAUSS_DATA = 4,
-  MCG_LIK_CAUCHY_DATA = 5
+  MCG_LIK_CAUCHY_DATA = 5,
+  MCG_LIK_GAUSS_MIX = 6
 };
+#define MCG_LIK_MIX_MAX 64
 
 /* ---- prior kinds (replace the log_prior closure) ----
    FLAT     : (none)              lp = 0

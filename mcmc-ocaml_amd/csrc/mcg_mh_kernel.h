@@ -246,6 +246,36 @@ __device__ __forceinline__ double eval_lik(const double* y, int sub, const MhArg
       A[k] = fma(t, t, A[k]);
     }
     return q[D] - 0.5 * canon8(A);
+  } else if constexpr (LIK == MCG_LIK_GAUSS_MIX) {
+    // log (sum_i exp g_i) over a.data_n components (test/nested_test.ml:52-57), g_i the DIAG
+    // canonical form of component i (q + i (2D + 1): mu/sigma[D], 1/sigma[D], C_i), folded by a
+    // one-pass max-shifted log-sum-exp in component order: s = sum_i exp(g_i - M) with the
+    // running max M rescaling s when it moves (the reference's exp overflows above g = 709)
+    double M = -__builtin_inf(), s = 0.0;
+    const int nc = (int)a.data_n;
+    for (int c = 0; c < nc; ++c) {
+      const auto qc = q + c * (2 * D + 1);
+      double A[L::NA];
+#pragma unroll
+      for (int j = 0; j < L::NA; ++j) A[j] = 0.0;
+#pragma unroll
+      for (int i = 0; i < L::NCL; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (!L::valid(sub, i, k)) continue;
+          const int d = L::dim(sub, i, k);
+          const double e = fma(y[4 * i + k], qc[D + d], -qc[d]);
+          A[i % L::NA] = fma(e, e, A[i % L::NA]);
+        }
+      const double g = qc[2 * D] - 0.5 * reduce_canon<P>(A);
+      if (g > M) {
+        s = s * pexp(M - g) + 1.0;
+        M = g;
+      } else {
+        s = s + pexp(g - M);
+      }
+    }
+    return M == -__builtin_inf() ? M : M + plog(s);
   } else {
     // GAUSS_DATA / CAUCHY_DATA (bin/gaussian_cauchy.ml:149-164), D = 2 nd, y = (mu, sigma)
     static_assert(P == 1, "DATA: one lane per chain");

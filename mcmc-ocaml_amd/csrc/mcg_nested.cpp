@@ -287,8 +287,11 @@ extern "C" {
 int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res,
                mcg_observer_fn observer, void* user) {
   if (!ctx || !opts) return MCG_EINVAL;
-  const int D = ctx->D;
+  // D: the kernel width of the live rows [n][D] (the caller's ndim Dr, zero-padded to a
+  // compiled width; the padding is stripped from every point handed back)
+  const int D = ctx->Dk, Dr = ctx->D;
   if (D < 1) return set_error(ctx, MCG_ESTATE, "set the likelihood first");
+  if (ctx->rj_active) return set_error(ctx, MCG_ESTATE, "nested sampling after mcg_set_rjmcmc: set a likelihood first");
   if (ctx->prior_kind != MCG_PRIOR_BOX && ctx->prior_kind != MCG_PRIOR_OPEN_BOX)
     return set_error(ctx, MCG_EINVAL, "nested sampling needs a box prior (draw_prior = uniform in the box)");
   const int64_t n = opts->nlive > 0 ? opts->nlive : 1000;
@@ -302,7 +305,7 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   const int64_t max_dead = opts->max_dead > 0 ? opts->max_dead : 1000 * n;
   nest_walk_fn walk = find_nest_walk(D, ctx->lik_kind);
   nest_init_fn init = find_nest_init(D, ctx->lik_kind);
-  if (!walk || !init) return set_error(ctx, MCG_EINVAL, "no compiled nested kernel for D=%d likelihood=%d", D, ctx->lik_kind);
+  if (!walk || !init) return set_error(ctx, MCG_EINVAL, "no compiled nested kernel for ndim %d (width %d) likelihood=%d", Dr, D, ctx->lik_kind);
   (void)hipSetDevice(ctx->opts.device);
   // forget the previous run up front: a run that fails below must not leave mcg_nested_get
   // sizing its copies from the previous run's counts over this run's partial data
@@ -425,7 +428,7 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   a.nmcmc = nmcmc;
   a.tv_len = p2;
   a.mode_hop = opts->mode_hop;
-  a.sigma_de = 2.38 / std::sqrt(2.0 * (double)D);     // mcmc.ml:212
+  a.sigma_de = 2.38 / std::sqrt(2.0 * (double)Dr);    // mcmc.ml:212 (the caller's ndim)
   a.log_epsrel = std::log(epsrel);
   a.k0 = (uint32_t)ctx->opts.seed;
   a.k1 = (uint32_t)(ctx->opts.seed >> 32);
@@ -510,17 +513,38 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
     if (check && (e = launch_check_sorted(x.l(), x.t(), n, gm, (long long*)B.chk.p + 1, B.s2)) != hipSuccess) return e;
     return hipEventRecord(B.ev_full[gm & 1], B.s2);
   };
-  // dead buffers replaced while batches were in flight: freed after the stream drains
+  // Dead buffers replaced while batches were in flight, tagged with the sequence number of the
+  // batch whose launch replaced them.  Once that batch is done, every kernel and grow copy that
+  // touched the old buffer has finished (stream order), and so has the earlier batch whose
+  // observer copy may read it (batches are handled in launch order): it is freed then (ADVICE
+  // r3), the rest when the run ends.
   struct RetiredBufs {
     hipStream_t s;
-    std::vector<void*> bufs;
+    std::vector<std::pair<int64_t, void*>> bufs;
+    // (a stream-ordered free: hipFree would wait for the batch in flight; where the runtime
+    // refuses hipFreeAsync on this allocation the buffer stays listed until the end)
+    void release_upto(int64_t seq) {
+      size_t w = 0;
+      for (auto& e : bufs) {
+        if (e.first <= seq && hipFreeAsync(e.second, s) == hipSuccess) continue;
+        bufs[w++] = e;
+      }
+      bufs.resize(w);
+    }
     ~RetiredBufs() {
       if (bufs.empty()) return;
       (void)hipStreamSynchronize(s);
-      for (void* p : bufs) (void)hipFree(p);
+      for (auto& e : bufs) (void)hipFree(e.second);
     }
   } retired_dead{s, {}};
+  int64_t batch_seq = 0;                              // batches launched so far
+  int64_t slot_seq[2] = {-1, -1};                     // the batch in each slot
   // enqueue generations [gen, gen + G) and the copies of their state / dead ll, lp into slot q
+  // the dead-row buffer each in-flight batch's kernels write: once the batch's done event has
+  // fired it holds every row up to the batch's end (earlier rows were written there or copied in
+  // by a grow copy queued ahead of the batch), while B.dead_x may already be a newer buffer whose
+  // grow copy is still queued behind the other batch
+  double* slot_dead_x[2] = {nullptr, nullptr};
   auto launch_batch = [&](int64_t G, int q) -> int {
     const int64_t need = (gen + G) * k;
     if (need > B.dead_cap) {
@@ -543,7 +567,7 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
       std::swap(B.dead_ll.p, nlb.p); std::swap(B.dead_ll.bytes, nlb.bytes);
       std::swap(B.dead_lp.p, npb.p); std::swap(B.dead_lp.bytes, npb.bytes);
       for (DevBuf* o : {&nxb, &nlb, &npb}) {
-        retired_dead.bufs.push_back(o->p);
+        retired_dead.bufs.push_back({batch_seq, o->p});
         o->p = nullptr;
         o->bytes = 0;
       }
@@ -552,6 +576,8 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
     a.dead_x = (double*)B.dead_x.p;
     a.dead_ll = (double*)B.dead_ll.p;
     a.dead_lp = (double*)B.dead_lp.p;
+    slot_dead_x[q] = a.dead_x;
+    slot_seq[q] = batch_seq++;
     for (int64_t g = gen; g < gen + G; ++g) {
       KeyBuf& cur = B.keys[(base + g) % 2];
       KeyBuf& nxt = B.keys[(base + g + 1) % 2];
@@ -685,6 +711,8 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
       R.ll.insert(R.ll.end(), B.h_stage[2 * q], B.h_stage[2 * q] + (d1 - d0));
       R.lp.insert(R.lp.end(), B.h_stage[2 * q + 1], B.h_stage[2 * q + 1] + (d1 - d0));
     }
+    const double* done_dead_x = slot_dead_x[q];      // (before the refill below replaces it)
+    const int64_t done_seq = slot_seq[q];
     const int64_t remaining = max_dead / k - gen;
     if (!st.stopped && remaining > 0) {               // the slot is free again: refill it
       batch = std::min<int64_t>(batch * 2, kMaxBatch);
@@ -697,11 +725,14 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
     const int64_t ndead = d1;
     if (observer && ndead > reported) {
       const int64_t m = ndead - reported;
-      hx.resize(m * D);
-      HC(hipMemcpy(hx.data(), (double*)B.dead_x.p + reported * D, m * D * 8, hipMemcpyDeviceToHost), "observer copy");
+      hx.resize(m * Dr);
+      // the rows of this finished batch's buffer (complete up to its end: no stream wait needed)
+      HC(hipMemcpy2D(hx.data(), (size_t)Dr * 8, done_dead_x + reported * D, (size_t)D * 8, (size_t)Dr * 8, m,
+                     hipMemcpyDeviceToHost), "observer copy");
       observer(user, hx.data(), R.ll.data() + reported, R.lp.data() + reported, m);
       reported = ndead;
     }
+    retired_dead.release_upto(done_seq);
     if (st.stopped) {
       // a batch enqueued past the stop retires nothing; let it drain before the final copies
       if (inflight[q ^ 1]) HC(hipEventSynchronize(B.done[q ^ 1]), "nested sync");
@@ -800,7 +831,8 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   R.n_total = ntot;
   R.converged = st.stopped != 0;
   R.n_dead = ndead;
-  R.ndim = D;
+  R.ndim = Dr;
+  R.ndim_k = D;
   R.n_gen = st.gen_done;
   R.nlive = n;
   if (res) {
@@ -883,8 +915,15 @@ int mcg_nested_get(mcg_ctx* ctx, double* pts, double* ll, double* lp, double* lo
   const auto t0 = std::chrono::steady_clock::now();
   if (pts) {
     NestedBufs& B = ctx->nested_bufs->b;
-    int rc = hip_check(ctx, copy_d2h_large(B, pts, B.dead_x.p, (size_t)(R.n_total * R.ndim) * 8, ctx->stream),
-                       "copy points");
+    int rc;
+    if (R.ndim_k == R.ndim) {
+      rc = hip_check(ctx, copy_d2h_large(B, pts, B.dead_x.p, (size_t)(R.n_total * R.ndim) * 8, ctx->stream),
+                     "copy points");
+    } else {
+      // rows [n_total][ndim_k] on the device: their leading ndim columns
+      rc = hip_check(ctx, hipMemcpy2D(pts, (size_t)R.ndim * 8, B.dead_x.p, (size_t)R.ndim_k * 8, (size_t)R.ndim * 8,
+                                      (size_t)R.n_total, hipMemcpyDeviceToHost), "copy points");
+    }
     if (rc) return rc;
   }
   const auto t1 = std::chrono::steady_clock::now();

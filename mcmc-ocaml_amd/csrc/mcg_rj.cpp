@@ -15,47 +15,6 @@ namespace {
 
 const double kNegHalfLog2Pi = -0.91893853320467274178;
 
-// pad a likelihood block packed at D to the layout at DM (zeros: +0 terms in every sum)
-std::vector<double> pad_lik(int32_t kind, int D, int DM, const std::vector<double>& v) {
-  std::vector<double> o;
-  switch (kind) {
-    case MCG_LIK_DIAG_GAUSS:              // mu/s[D], 1/s[D], C
-      o.assign(2 * (size_t)DM + 1, 0.0);
-      for (int d = 0; d < D; ++d) { o[d] = v[d]; o[DM + d] = v[D + d]; }
-      o[2 * DM] = v[2 * D];
-      break;
-    case MCG_LIK_GAUSS_SHELL:             // c[D], R, iw, C
-      o.assign((size_t)DM + 3, 0.0);
-      for (int d = 0; d < D; ++d) o[d] = v[d];
-      o[DM] = v[D]; o[DM + 1] = v[D + 1]; o[DM + 2] = v[D + 2];
-      break;
-    case MCG_LIK_FULLCOV_GAUSS:           // mu[D], C, U[D*D]
-      o.assign((size_t)DM + 1 + (size_t)DM * DM, 0.0);
-      for (int d = 0; d < D; ++d) o[d] = v[d];
-      o[DM] = v[D];
-      for (int i = 0; i < D; ++i)
-        for (int j = 0; j < D; ++j) o[DM + 1 + (size_t)i * DM + j] = v[D + 1 + (size_t)i * D + j];
-      break;
-    default:
-      o.assign(1, 0.0);
-  }
-  return o;
-}
-
-// prior block [check_lo, check_hi, lp_in, lo, hi] at DM; padded dims are unbounded
-std::vector<double> pad_prior(int D, int DM, const std::vector<double>& v) {
-  std::vector<double> o(4 * (size_t)DM + 1);
-  for (int d = 0; d < DM; ++d) {
-    const bool in = d < D;
-    o[d] = in ? v[d] : -HUGE_VAL;
-    o[DM + d] = in ? v[D + d] : HUGE_VAL;
-    o[2 * DM + 1 + d] = in ? v[2 * D + 1 + d] : -HUGE_VAL;
-    o[3 * DM + 1 + d] = in ? v[3 * D + 1 + d] : HUGE_VAL;
-  }
-  o[2 * DM] = v[2 * D];
-  return o;
-}
-
 int pack_jump(mcg_ctx* ctx, int32_t kind, int D, int DM, const double* p, size_t n, bool into,
               bool has_tree, std::vector<double>& o) {
   o.clear();
@@ -156,7 +115,7 @@ int mcg_set_rjmcmc(mcg_ctx* ctx, const mcg_rj_model* a, const mcg_rj_model* b) {
     };
     const std::vector<double> plik = pad_lik(q->lik_kind, D, DM, lik);
     // (dev grows below: re-take the header pointer afterwards)
-    const double o_lik = put(plik), o_pri = put(pad_prior(D, DM, pri)), o_j = put(jmp), o_i = put(into);
+    const double o_lik = put(plik), o_pri = put(pad_prior(D, DM, pri, -HUGE_VAL, HUGE_VAL)), o_j = put(jmp), o_i = put(into);
     double* hh = &dev[16 * (size_t)k];
     hh[7] = o_lik; hh[8] = o_pri; hh[9] = o_j; hh[10] = o_i;
   }
@@ -164,6 +123,7 @@ int mcg_set_rjmcmc(mcg_ctx* ctx, const mcg_rj_model* a, const mcg_rj_model* b) {
   if ((rc = hip_check(ctx, ctx->d_rj.ensure(dev.size() * 8), "alloc rj"))) return rc;
   if ((rc = hip_check(ctx, hipMemcpy(ctx->d_rj.p, dev.data(), dev.size() * 8, hipMemcpyHostToDevice), "copy rj"))) return rc;
   ctx->D = DM;
+  ctx->Dk = DM;
   ctx->lik_kind = MCG_LIK_FLAT;
   ctx->rj_active = true;
   ctx->N = 0;

@@ -144,13 +144,14 @@ static const double kNegHalfLog2Pi = -0.91893853320467274178;
 //   GAUSS: s[D], 1/s[D]  (C = sum_d (-1/2 log 2pi - log s_d))
 //   SHIFT_UNIFORM: a[D], b[D], b - a[D]  (C = -sum_d log(b_d - a_d))
 //   WRAP_UNIFORM: lo[D], hi[D], dx[D]
+// (at the kernel width Dk: padded dims get zero steps, zero bounds and no density term)
 static int pack_mixture(mcg_ctx* ctx, const double* params, size_t n, std::vector<double>& dev) {
-  const int D = ctx->D;
+  const int D = ctx->D, Dk = ctx->Dk;
   if (!params || n < 1) return mcg::set_error(ctx, MCG_EINVAL, "MIXTURE: ncomp, components...");
   const int nc = (int)params[0];
   if (nc < 1 || nc > MCG_MIX_MAX_COMPONENTS || (double)nc != params[0])
     return mcg::set_error(ctx, MCG_EINVAL, "MIXTURE: 1 <= ncomp <= %d", MCG_MIX_MAX_COMPONENTS);
-  const size_t stride = 5 + 3 * (size_t)D;
+  const size_t stride = 5 + 3 * (size_t)Dk;
   dev.assign(1 + nc * stride, 0.0);
   dev[0] = nc;
   double ptot = 0.0;
@@ -188,7 +189,7 @@ static int pack_mixture(mcg_ctx* ctx, const double* params, size_t n, std::vecto
       for (int d = 0; d < D; ++d) {
         if (!(u[d] > 0.0)) return mcg::set_error(ctx, MCG_EINVAL, "MIXTURE: GAUSS scale must be > 0");
         q[5 + d] = u[d];
-        q[5 + D + d] = 1.0 / u[d];
+        q[5 + Dk + d] = 1.0 / u[d];
         C = C + (kNegHalfLog2Pi - std::log(u[d]));
       }
       o += 3 + D;
@@ -196,13 +197,14 @@ static int pack_mixture(mcg_ctx* ctx, const double* params, size_t n, std::vecto
       for (int d = 0; d < D; ++d) {
         if (!(u[D + d] > u[d])) return mcg::set_error(ctx, MCG_EINVAL, "MIXTURE: SHIFT_UNIFORM needs a < b");
         q[5 + d] = u[d];
-        q[5 + D + d] = u[D + d];
-        q[5 + 2 * D + d] = u[D + d] - u[d];
+        q[5 + Dk + d] = u[D + d];
+        q[5 + 2 * Dk + d] = u[D + d] - u[d];
         C = C - std::log(u[D + d] - u[d]);
       }
       o += 3 + 2 * D;
     } else if (ck == MCG_MIX_WRAP_UNIFORM) {
-      for (int j = 0; j < 3 * D; ++j) q[5 + j] = u[j];
+      for (int j = 0; j < 3; ++j)
+        for (int d = 0; d < D; ++d) q[5 + j * Dk + d] = u[j * D + d];
       o += 3 + 3 * D;
     } else {
       o += 3;
@@ -314,6 +316,30 @@ int pack_likelihood(mcg_ctx* ctx, int32_t kind, int D, const double* params, siz
       dev.insert(dev.end(), U, U + (size_t)D * D);
       break;
     }
+    case MCG_LIK_GAUSS_MIX: {
+      // m, then per component mu[D], sigma[D] -> per component the DIAG block [mu/sigma[D],
+      // 1/sigma[D], C_i] (stride 2D + 1); the component count rides in data_n
+      if (D < 1 || !params || n < 1) return set_error(ctx, MCG_EINVAL, "GAUSS_MIX: params = m, (mu[D], sigma[D]) x m");
+      const int m = (int)params[0];
+      if (!(m >= 1 && m <= MCG_LIK_MIX_MAX) || (double)m != params[0] || n != 1 + (size_t)m * 2 * D)
+        return set_error(ctx, MCG_EINVAL, "GAUSS_MIX: params = m (1 <= m <= %d), (mu[D], sigma[D]) x m", MCG_LIK_MIX_MAX);
+      dev.assign((size_t)m * (2 * D + 1), 0.0);
+      for (int c = 0; c < m; ++c) {
+        const double* mu = params + 1 + (size_t)c * 2 * D;
+        const double* sg = mu + D;
+        double* o = &dev[(size_t)c * (2 * D + 1)];
+        double C = 0.0;
+        for (int d = 0; d < D; ++d) {
+          if (!(sg[d] > 0.0)) return set_error(ctx, MCG_EINVAL, "GAUSS_MIX: sigma > 0");
+          o[D + d] = 1.0 / sg[d];
+          o[d] = mu[d] * o[D + d];
+          C = C + (kNegHalfLog2Pi - std::log(sg[d]));
+        }
+        o[2 * D] = C;
+      }
+      data_n = m;
+      break;
+    }
     case MCG_LIK_GAUSS_DATA:
     case MCG_LIK_CAUCHY_DATA: {
       if (!params || n < 2) return set_error(ctx, MCG_EINVAL, "DATA: params = nd, data[nsamp*nd]");
@@ -333,6 +359,83 @@ int pack_likelihood(mcg_ctx* ctx, int32_t kind, int D, const double* params, siz
   return MCG_OK;
 }
 
+int pad_width(int32_t lik_kind, int D) {
+  // the widths gen_instances.py compiles for every likelihood / proposal pair that pads
+  static const int kSep[] = {1, 2, 3, 4, 5, 6, 7, 8, 12, 16, 24, 32, 48, 64};
+  static const int kFull[] = {1, 2, 3, 4, 5, 6, 7, 8, 16, 32, 48, 64};
+  auto first_ge = [D](const int* w, int n) {
+    for (int i = 0; i < n; ++i)
+      if (w[i] >= D) return w[i];
+    return D;
+  };
+  switch (lik_kind) {
+    case MCG_LIK_FLAT:
+    case MCG_LIK_DIAG_GAUSS:
+    case MCG_LIK_GAUSS_SHELL:
+    case MCG_LIK_GAUSS_MIX: return first_ge(kSep, (int)(sizeof kSep / sizeof kSep[0]));
+    case MCG_LIK_FULLCOV_GAUSS: return first_ge(kFull, (int)(sizeof kFull / sizeof kFull[0]));
+    default: return D;                        // DATA kinds: (mu, sigma) halves, no padding
+  }
+}
+
+std::vector<double> pad_lik(int32_t kind, int D, int DM, const std::vector<double>& v) {
+  if (D == DM) return v;
+  std::vector<double> o;
+  switch (kind) {
+    case MCG_LIK_DIAG_GAUSS:              // mu/s[D], 1/s[D], C
+      o.assign(2 * (size_t)DM + 1, 0.0);
+      for (int d = 0; d < D; ++d) { o[d] = v[d]; o[DM + d] = v[D + d]; }
+      o[2 * DM] = v[2 * D];
+      break;
+    case MCG_LIK_GAUSS_MIX: {             // per component mu/s[D], 1/s[D], C_i
+      const size_t m = v.size() / (2 * (size_t)D + 1);
+      o.assign(m * (2 * (size_t)DM + 1), 0.0);
+      for (size_t c = 0; c < m; ++c) {
+        const double* src = &v[c * (2 * D + 1)];
+        double* dst = &o[c * (2 * DM + 1)];
+        for (int d = 0; d < D; ++d) { dst[d] = src[d]; dst[DM + d] = src[D + d]; }
+        dst[2 * DM] = src[2 * D];
+      }
+      break;
+    }
+    case MCG_LIK_GAUSS_SHELL:             // c[D], R, iw, C
+      o.assign((size_t)DM + 3, 0.0);
+      for (int d = 0; d < D; ++d) o[d] = v[d];
+      o[DM] = v[D]; o[DM + 1] = v[D + 1]; o[DM + 2] = v[D + 2];
+      break;
+    case MCG_LIK_FULLCOV_GAUSS:           // mu[D], C, U[D*D]
+      o.assign((size_t)DM + 1 + (size_t)DM * DM, 0.0);
+      for (int d = 0; d < D; ++d) o[d] = v[d];
+      o[DM] = v[D];
+      for (int i = 0; i < D; ++i)
+        for (int j = 0; j < D; ++j) o[DM + 1 + (size_t)i * DM + j] = v[D + 1 + (size_t)i * D + j];
+      break;
+    default:                              // FLAT
+      o.assign(1, 0.0);
+  }
+  return o;
+}
+
+std::vector<double> pad_prior(int D, int DM, const std::vector<double>& v, double pad_draw_lo, double pad_draw_hi) {
+  if (D == DM) return v;
+  std::vector<double> o(4 * (size_t)DM + 1);
+  for (int d = 0; d < DM; ++d) {
+    const bool in = d < D;
+    o[d] = in ? v[d] : -HUGE_VAL;
+    o[DM + d] = in ? v[D + d] : HUGE_VAL;
+    o[2 * DM + 1 + d] = in ? v[2 * D + 1 + d] : pad_draw_lo;
+    o[3 * DM + 1 + d] = in ? v[3 * D + 1 + d] : pad_draw_hi;
+  }
+  o[2 * DM] = v[2 * D];
+  return o;
+}
+
+std::vector<double> pad_rows(const double* rows, int64_t n, int D, int DM) {
+  std::vector<double> o((size_t)n * DM, 0.0);
+  for (int64_t i = 0; i < n; ++i) std::copy(rows + i * D, rows + (i + 1) * D, o.begin() + i * DM);
+  return o;
+}
+
 }  // namespace mcg
 
 extern "C" {
@@ -346,10 +449,15 @@ int mcg_set_likelihood(mcg_ctx* ctx, int32_t kind, int32_t ndim, const double* p
   int64_t data_n = 0;
   int prc = pack_likelihood(ctx, kind, D, params, n, dev, &is_cauchy, &data_n);
   if (prc) return prc;
-  ctx->rj_active = false;
-  if (ctx->D != 0 && ctx->D != D && ctx->N > 0)
+  const int Dk = pad_width(kind, D);
+  if (ctx->D != 0 && (ctx->D != D || ctx->Dk != Dk) && ctx->N > 0)
     return set_error(ctx, MCG_ESTATE, "ndim changed after mcg_init");
+  dev = pad_lik(kind, D, Dk, dev);
+  ctx->rj_active = false;
+  // the proposal and prior descriptors are laid out at the old width: re-set them below
+  const bool width_changed = ctx->Dk != Dk || ctx->D != D;
   ctx->D = D;
+  ctx->Dk = Dk;
   ctx->lik_kind = kind;
   ctx->is_cauchy = is_cauchy;
   ctx->data_n = data_n;
@@ -359,10 +467,18 @@ int mcg_set_likelihood(mcg_ctx* ctx, int32_t kind, int32_t ndim, const double* p
   rc = hip_check(ctx, hipMemcpy(ctx->d_lik.p, dev.data(), dev.size() * 8, hipMemcpyHostToDevice), "copy likelihood");
   if (rc) return rc;
   // keep a padded flat prior / default proposal consistent with D
-  if (ctx->pri_host.size() != (size_t)(4 * D + 1)) {
+  if (width_changed || ctx->pri_host.size() != (size_t)(4 * Dk + 1)) {
     double z = 0.0;
     rc = mcg_set_prior(ctx, MCG_PRIOR_FLAT, &z, 0);
     if (rc) return rc;
+  }
+  if (width_changed) {
+    // every proposal descriptor (and a kD tree) was laid out for the old ndim -- a DE proposal
+    // over samples of the old width would read past its rows: back to the default proposal, a
+    // unit Gaussian step at the new width, until the caller sets one of this ndim
+    ctx->kd.built = false;
+    double one = 1.0;
+    if ((rc = mcg_set_proposal(ctx, MCG_PROP_GAUSS, &one, 1))) return rc;
   }
   return MCG_OK;
 }
@@ -409,6 +525,8 @@ int mcg_set_prior(mcg_ctx* ctx, int32_t kind, const double* params, size_t n) {
   std::vector<double> dev;
   int prc = pack_prior(ctx, kind, D, params, n, dev);
   if (prc) return prc;
+  // padded dims: unbounded in the box test, drawn at 0 by nested sampling's prior draws
+  dev = pad_prior(D, ctx->Dk, dev, 0.0, 0.0);
   ctx->prior_kind = kind;
   ctx->pri_host = dev;
   int rc = hip_check(ctx, ctx->d_pri.ensure(dev.size() * 8), "alloc prior");
@@ -421,14 +539,21 @@ int mcg_set_proposal(mcg_ctx* ctx, int32_t kind, const double* params, size_t n)
   if (int qrc = quiesce(ctx)) return qrc;
   int D = ctx->D;
   if (D < 1) return set_error(ctx, MCG_ESTATE, "set the likelihood (ndim) first");
+  const int Dk = ctx->Dk;
   std::vector<double> dev;
   if (kind == MCG_PROP_GAUSS) {
     if (!params || (n != 1 && n != (size_t)D)) return set_error(ctx, MCG_EINVAL, "GAUSS: s[1] or s[D]");
-    dev.resize(D);
+    dev.assign(Dk, 0.0);                       // padded dims: step 0 (they stay at 0)
     for (int d = 0; d < D; ++d) dev[d] = params[n == 1 ? 0 : d];
   } else if (kind == MCG_PROP_WRAP_UNIFORM) {
     if (!params || n != (size_t)(3 * D)) return set_error(ctx, MCG_EINVAL, "WRAP_UNIFORM: lo[D], hi[D], dx[D]");
-    dev.assign(params, params + n);
+    // padded dims: the interval [0, 0) with dx 0 wraps 0 onto itself
+    dev.assign(3 * (size_t)Dk, 0.0);
+    for (int d = 0; d < D; ++d) {
+      dev[d] = params[d];
+      dev[Dk + d] = params[D + d];
+      dev[2 * Dk + d] = params[2 * D + d];
+    }
   } else if (kind == MCG_PROP_KD_INTERP) {
     if (!ctx->kd.built) return set_error(ctx, MCG_ESTATE, "call mcg_set_kd_proposal first");
     dev.push_back(0.0);
@@ -459,6 +584,8 @@ int mcg_set_kd_proposal(mcg_ctx* ctx, const double* pts, int64_t M, const double
   int D = ctx->D;
   if (D < 1) return set_error(ctx, MCG_ESTATE, "set the likelihood (ndim) first");
   if (M < 1) return set_error(ctx, MCG_EINVAL, "Interpolate_pdf.make: no points");
+  if (ctx->Dk != D)
+    return set_error(ctx, MCG_EINVAL, "KD_INTERP: ndim %d has no compiled kD kernel (widths 1-8, 16)", D);
   int rc = kd_build(ctx, pts, M, D, low, high);
   if (rc) return rc;
   double z = 0.0;
@@ -474,8 +601,16 @@ int mcg_set_de_proposal(mcg_ctx* ctx, const double* samples, int64_t M, double m
   if (M < 2) return set_error(ctx, MCG_EINVAL, "differential_evolution_proposal: need >= 2 samples");
   if (M > (int64_t)0xFFFFFFFF) return set_error(ctx, MCG_EINVAL, "differential_evolution_proposal: too many samples");
   int rc;
-  if ((rc = hip_check(ctx, ctx->d_de_pts.ensure((size_t)M * D * 8), "alloc DE samples"))) return rc;
-  if ((rc = hip_check(ctx, hipMemcpy(ctx->d_de_pts.p, samples, (size_t)M * D * 8, hipMemcpyHostToDevice), "copy DE samples"))) return rc;
+  const int Dk = ctx->Dk;
+  // rows at the kernel width (padded dims 0: the DE step y_j - x_i is 0 there)
+  std::vector<double> padded;
+  const double* rows = samples;
+  if (Dk != D) {
+    padded = pad_rows(samples, M, D, Dk);
+    rows = padded.data();
+  }
+  if ((rc = hip_check(ctx, ctx->d_de_pts.ensure((size_t)M * Dk * 8), "alloc DE samples"))) return rc;
+  if ((rc = hip_check(ctx, hipMemcpy(ctx->d_de_pts.p, rows, (size_t)M * Dk * 8, hipMemcpyHostToDevice), "copy DE samples"))) return rc;
   ctx->de_M = M;
   ctx->de_D = D;
   return mcg_set_proposal(ctx, MCG_PROP_DE, &mode_hopping_frac, 1);
@@ -487,7 +622,7 @@ int mcg_init(mcg_ctx* ctx, int64_t nchains, const double* x_soa, const double* l
   if (ctx->D < 1) return set_error(ctx, MCG_ESTATE, "set the likelihood first");
   if (nchains > (int64_t)0x7FFFFFFF) return set_error(ctx, MCG_EINVAL, "too many chains");
   (void)hipSetDevice(ctx->opts.device);
-  const int D = ctx->D;
+  const int D = ctx->D, Dk = ctx->Dk;
   const size_t N = (size_t)nchains;
   int rc;
   // the uploads below are blocking copies on the null stream, which does not order against the
@@ -496,14 +631,16 @@ int mcg_init(mcg_ctx* ctx, int64_t nchains, const double* x_soa, const double* l
   // Mcmc's counters are global until reset_counters (mcmc.ml:27-35): fold this set of chains'
   // tallies into the context totals before the per-chain device counters restart
   if ((rc = mcg::fold_counters(ctx))) return rc;
-  if ((rc = hip_check(ctx, ctx->d_x.ensure(N * D * 8), "alloc x"))) return rc;
+  if ((rc = hip_check(ctx, ctx->d_x.ensure(N * Dk * 8), "alloc x"))) return rc;
   if ((rc = hip_check(ctx, ctx->d_ll.ensure(N * 8), "alloc ll"))) return rc;
   if ((rc = hip_check(ctx, ctx->d_lp.ensure(N * 8), "alloc lp"))) return rc;
   if ((rc = hip_check(ctx, ctx->d_nacc.ensure(N * 8), "alloc counters"))) return rc;
   // zero the (possibly new) counters before anything else can fail: mcg_get_counters reads
   // them with the old N if a later copy errors out
   if ((rc = hip_check(ctx, hipMemset(ctx->d_nacc.p, 0, N * 8), "zero counters"))) return rc;
+  // [D][N] is the leading block of the [Dk][N] state; the padded rows are 0
   if ((rc = hip_check(ctx, hipMemcpy(ctx->d_x.p, x_soa, N * D * 8, hipMemcpyHostToDevice), "copy x"))) return rc;
+  if (Dk > D && (rc = hip_check(ctx, hipMemset((double*)ctx->d_x.p + N * D, 0, N * (Dk - D) * 8), "zero pad rows"))) return rc;
   ctx->N = nchains;
   // steps_done is NOT reset: the Philox step counter runs on across inits like the reference's
   // global Random state (a re-init must not replay the previous draws); mcg_reseed restarts it
@@ -515,7 +652,7 @@ int mcg_init(mcg_ctx* ctx, int64_t nchains, const double* x_soa, const double* l
     if ((rc = hip_check(ctx, hipMemcpy(ctx->d_lp.p, lp, N * 8, hipMemcpyHostToDevice), "copy lp"))) return rc;
     return MCG_OK;
   }
-  eval_launch_fn fn = find_eval_kernel(D, ctx->lik_kind);
+  eval_launch_fn fn = find_eval_kernel(Dk, ctx->lik_kind);
   if (!fn) return set_error(ctx, MCG_EINVAL, "no compiled kernel for likelihood %d at D=%d", ctx->lik_kind, D);
   MhArgs a = base_args(ctx);
   if ((rc = hip_check(ctx, fn(a, ctx->stream), "eval launch"))) return rc;
@@ -528,6 +665,7 @@ int mcg_get_state(mcg_ctx* ctx, double* x_soa, double* ll, double* lp) {
   const size_t N = (size_t)ctx->N;
   int rc;
   if ((rc = hip_check(ctx, hipStreamSynchronize(ctx->stream), "sync"))) return rc;
+  // (the leading [D][N] block of the padded [Dk][N] state)
   if (x_soa && (rc = hip_check(ctx, hipMemcpy(x_soa, ctx->d_x.p, N * ctx->D * 8, hipMemcpyDeviceToHost), "copy x"))) return rc;
   if (ll && (rc = hip_check(ctx, hipMemcpy(ll, ctx->d_ll.p, N * 8, hipMemcpyDeviceToHost), "copy ll"))) return rc;
   if (lp && (rc = hip_check(ctx, hipMemcpy(lp, ctx->d_lp.p, N * 8, hipMemcpyDeviceToHost), "copy lp"))) return rc;
@@ -565,14 +703,16 @@ MhArgs base_args(mcg_ctx* ctx) {
   a.de_M = ctx->de_M;
   if (ctx->rj_active) rj_args(ctx, a);
   // one proposal scale and one box for every dim (bitwise): the fused step takes them as scalars
-  const int D = ctx->D;
+  // (the descriptors are laid out at the kernel width Dk; with padding the dims D..Dk-1 hold 0
+  // for the whole run, so a box applied to every dim must contain 0)
+  const int D = ctx->Dk, Dr = ctx->D;
   const auto& sp = ctx->prop_host;
   const auto& bx = ctx->pri_host;
   // one box for every dim (bitwise), any proposal: eval_prior compares against kernel arguments
   // instead of loading 2D bounds per step
   if (ctx->prior_kind != MCG_PRIOR_FLAT && D >= 1 && (int)bx.size() >= 2 * D && !ctx->rj_active) {
-    bool same = true;
-    for (int d = 1; d < D && same; ++d)
+    bool same = Dr == D || (bx[0] <= 0.0 && 0.0 <= bx[D]);
+    for (int d = 1; d < Dr && same; ++d)
       same = !std::memcmp(&bx[d], &bx[0], 8) && !std::memcmp(&bx[D + d], &bx[D], 8);
     if (same) {
       a.ubox = 1;
@@ -580,7 +720,7 @@ MhArgs base_args(mcg_ctx* ctx) {
       a.box_hi = bx[D];
     }
   }
-  if (ctx->prop_kind == MCG_PROP_GAUSS && D >= 1 && (int)sp.size() >= D && (int)bx.size() >= 2 * D) {
+  if (ctx->prop_kind == MCG_PROP_GAUSS && D >= 1 && Dr == D && (int)sp.size() >= D && (int)bx.size() >= 2 * D) {
     bool same = true;
     for (int d = 1; d < D && same; ++d)
       same = !std::memcmp(&sp[d], &sp[0], 8) && !std::memcmp(&bx[d], &bx[0], 8) &&
@@ -598,7 +738,7 @@ MhArgs base_args(mcg_ctx* ctx) {
 // lanes per chain: enough lanes to put >= 4 waves on every SIMD, as long as the dimensions split
 // evenly into 4-dim Philox blocks (separable likelihoods with a Gaussian proposal only).
 int choose_lanes(mcg_ctx* ctx) {
-  const int D = ctx->D;
+  const int D = ctx->Dk;
   const bool separable = (ctx->lik_kind == MCG_LIK_DIAG_GAUSS || ctx->lik_kind == MCG_LIK_GAUSS_SHELL ||
                           ctx->lik_kind == MCG_LIK_FLAT) && ctx->prop_kind == MCG_PROP_GAUSS;
   const char* env = std::getenv("MCG_LANES_PER_CHAIN");
@@ -638,11 +778,18 @@ int mcg_run(mcg_ctx* ctx, const mcg_run_opts* o) {
   if (o->append && ctx->nrec_total == 0 && o->accumulate)
     return set_error(ctx, MCG_ESTATE, "append needs a previous run with records");
   (void)hipSetDevice(ctx->opts.device);
-  const int D = ctx->D;
+  const int D = ctx->Dk;                   // the kernel width (the state's rows, padded)
   const int64_t N = ctx->N;
+  if (!ctx->rj_active && ctx->prop_kind == MCG_PROP_DE && ctx->de_D != ctx->D)
+    return set_error(ctx, MCG_ESTATE, "DE proposal samples have ndim %d, the model %d", ctx->de_D, ctx->D);
   const int P = ctx->rj_active ? 1 : choose_lanes(ctx);
   mh_launch_fn fn = ctx->rj_active ? find_rj_kernel(D) : find_mh_kernel(D, P, ctx->lik_kind, ctx->prop_kind);
-  if (!fn) return set_error(ctx, MCG_EINVAL, "no compiled MH kernel for D=%d likelihood=%d proposal=%d", D, ctx->lik_kind, ctx->prop_kind);
+  if (!fn) {
+    if (D != ctx->D)
+      return set_error(ctx, MCG_EINVAL, "no compiled MH kernel for ndim %d (padded to %d) likelihood=%d proposal=%d",
+                       ctx->D, D, ctx->lik_kind, ctx->prop_kind);
+    return set_error(ctx, MCG_EINVAL, "no compiled MH kernel for D=%d likelihood=%d proposal=%d", D, ctx->lik_kind, ctx->prop_kind);
+  }
   ctx->lanes = P;
   // mcmc_array schedule: records at run-local step counts s_r = nbin + r*nskip (r < n_rec);
   // append mode records at nskip, 2 nskip, ... (no initial record).
@@ -770,7 +917,13 @@ int mcg_get_records(mcg_ctx* ctx, double* rec_x, double* rec_ll, double* rec_lp,
   const size_t N = (size_t)ctx->N, R = (size_t)ctx->rec_stored;
   if (rec_x) {
     if (!ctx->rec_x_valid) return set_error(ctx, MCG_ESTATE, "last run did not record x");
-    if ((rc = hip_check(ctx, hipMemcpy(rec_x, ctx->d_rec_x.p, R * ctx->D * N * 8, hipMemcpyDeviceToHost), "copy rec_x"))) return rc;
+    if (ctx->Dk == ctx->D) {
+      if ((rc = hip_check(ctx, hipMemcpy(rec_x, ctx->d_rec_x.p, R * ctx->D * N * 8, hipMemcpyDeviceToHost), "copy rec_x"))) return rc;
+    } else if (R > 0) {
+      // record r is [Dk][N] on the device: its leading [D][N] block
+      if ((rc = hip_check(ctx, hipMemcpy2D(rec_x, (size_t)ctx->D * N * 8, ctx->d_rec_x.p, (size_t)ctx->Dk * N * 8,
+                                           (size_t)ctx->D * N * 8, R, hipMemcpyDeviceToHost), "copy rec_x"))) return rc;
+    }
   }
   if (rec_ll || rec_lp) {
     if (!ctx->rec_llp_valid) return set_error(ctx, MCG_ESTATE, "last run did not record ll/lp");

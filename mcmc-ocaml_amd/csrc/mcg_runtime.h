@@ -39,6 +39,7 @@ struct NestedState {
   std::vector<double> ll, lp, wts;
   double wts_shift = 0.0;                 // wts hold log weights + log Z; mcg_nested_get subtracts it
   int64_t n_total = 0, n_dead = 0, n_gen = 0, nlive = 0, ndim = 0;
+  int64_t ndim_k = 0;                     // the device rows' width (ndim zero-padded)
   double log_ev = 0.0, log_dev = 0.0;
   bool converged = false;       // the stop test fired (false: max_dead reached first)
 };
@@ -55,8 +56,10 @@ struct mcg_ctx {
   int num_cus = 256;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  // model
+  // model: D = the caller's ndim; Dk = the compiled width the kernels run at (D <= Dk, the dims
+  // D..Dk-1 zero-padded on the device and stripped at every copy out; pad_width)
   int D = 0;
+  int Dk = 0;
   int32_t lik_kind = -1, prior_kind = MCG_PRIOR_FLAT, prop_kind = MCG_PROP_GAUSS;
   int32_t is_cauchy = 0;
   int64_t data_n = 0;
@@ -117,6 +120,19 @@ int kd_build(mcg_ctx* ctx, const double* pts, int64_t M, int D, const double* lo
 int pack_likelihood(mcg_ctx* ctx, int32_t kind, int D, const double* params, size_t n,
                     std::vector<double>& dev, int32_t* is_cauchy, int64_t* data_n);
 int pack_prior(mcg_ctx* ctx, int32_t kind, int D, const double* params, size_t n, std::vector<double>& dev);
+// Zero padding of a model to a compiled width DM >= D (mcg.h "Any ndim"): a padded dim holds 0 for
+// the whole run and adds +0 to every canonical sum, so the real dims compute exactly as at D.
+// The smallest compiled width >= D for a likelihood kind (D itself when it is compiled or when no
+// compiled width is larger)
+int pad_width(int32_t lik_kind, int D);
+// a likelihood block packed at D laid out at DM (zeros)
+std::vector<double> pad_lik(int32_t kind, int D, int DM, const std::vector<double>& v);
+// a prior block [check_lo, check_hi, lp_in, lo, hi] packed at D laid out at DM: padded dims
+// unbounded in the check and drawn in [pad_draw, pad_draw] (0: nested sampling's prior draws
+// leave them at 0)
+std::vector<double> pad_prior(int D, int DM, const std::vector<double>& v, double pad_draw_lo, double pad_draw_hi);
+// rows [n][D] -> [n][DM] with zero pad columns
+std::vector<double> pad_rows(const double* rows, int64_t n, int D, int DM);
 typedef hipError_t (*rj_init_fn)(const MhArgs&, int draw_tags, const double* xa, const double* xb, hipStream_t);
 mh_launch_fn find_rj_kernel(int DM);
 rj_init_fn find_rj_init(int DM);

@@ -11,7 +11,8 @@ PKG_ROOT = os.path.dirname(HERE)
 LIB_PATH = os.environ.get("MCG_LIBRARY", os.path.join(PKG_ROOT, "lib", "libmcg.so"))
 
 MCG_OK, MCG_EINVAL, MCG_EFAIL, MCG_EDEVICE, MCG_ENOMEM, MCG_ESTATE = 0, -1, -2, -3, -4, -5
-LIK_FLAT, LIK_DIAG_GAUSS, LIK_FULLCOV_GAUSS, LIK_GAUSS_SHELL, LIK_GAUSS_DATA, LIK_CAUCHY_DATA = range(6)
+LIK_FLAT, LIK_DIAG_GAUSS, LIK_FULLCOV_GAUSS, LIK_GAUSS_SHELL, LIK_GAUSS_DATA, LIK_CAUCHY_DATA, LIK_GAUSS_MIX = range(7)
+LIK_MIX_MAX = 64
 PRIOR_FLAT, PRIOR_BOX, PRIOR_OPEN_BOX = 0, 1, 2
 PROP_GAUSS, PROP_WRAP_UNIFORM, PROP_KD_INTERP, PROP_DE, PROP_MIXTURE = 1, 2, 3, 4, 5
 MIX_GAUSS, MIX_SHIFT_UNIFORM, MIX_WRAP_UNIFORM, MIX_KD_INTERP = 1, 2, 3, 4

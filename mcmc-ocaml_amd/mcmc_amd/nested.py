@@ -115,12 +115,26 @@ def log_total_error_estimate(log_ev, log_dev, nlive):
     return L.lib().mcg_log_total_error_estimate(log_ev, log_dev, nlive)
 
 
+_default_ctx = {}
+
+
+def _posterior_context(seed):
+    """The context posterior draws use when the caller passes none: one per seed for the
+    process, so repeated calls advance its draw counter and return new samples, as the
+    reference's global Random state does (a fresh context per call would replay call 0)."""
+    c = _default_ctx.get(seed)
+    if c is None:
+        c = _default_ctx[seed] = Context(seed=seed)
+    return c
+
+
 def posterior_indices(n, log_wts, ctx=None, seed=0):
     """The draws of Nested.posterior_samples (nested.ml:167-178) as indices into the points:
     cumulative weights and the reference's weight_binary_search_index (:152-165) on the device,
     one Philox draw per sample (include/mcg.h mcg_posterior_samples).  Repeated calls on one
-    context draw new samples (the reference's global Random state advances)."""
-    ctx = ctx or Context(seed=seed)
+    context -- the caller's, or without one the process-wide context of `seed` -- draw new
+    samples (the reference's global Random state advances)."""
+    ctx = ctx or _posterior_context(seed)
     w = np.ascontiguousarray(log_wts, dtype=np.float64)
     idx = np.zeros(int(n), np.int64)
     L.check(L.lib().mcg_posterior_samples(ctx.ptr, L.dptr(w), len(w), int(n), L.i64ptr(idx)), ctx.ptr)

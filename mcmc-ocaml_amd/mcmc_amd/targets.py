@@ -55,6 +55,18 @@ def gauss_shell(center, radius, width):
     return Likelihood(L.LIK_GAUSS_SHELL, len(c), np.concatenate([c, [radius, width]]))
 
 
+def gauss_mix(mus, sigmas):
+    """log (sum_i exp (Stats.log_multi_gaussian mu_i sigma_i x)): the four-Gaussian target of
+    test/nested_test.ml:41-64 (mus, sigmas: (m, D) arrays, or one sigma row for every component)."""
+    mus = np.atleast_2d(np.asarray(mus, dtype=np.float64))
+    sigmas = np.broadcast_to(np.atleast_2d(np.asarray(sigmas, dtype=np.float64)), mus.shape)
+    m, D = mus.shape
+    if not 1 <= m <= L.LIK_MIX_MAX:
+        raise ValueError("gauss_mix: 1 <= components <= %d" % L.LIK_MIX_MAX)
+    blocks = np.concatenate([mus, sigmas], axis=1).ravel()
+    return Likelihood(L.LIK_GAUSS_MIX, D, np.concatenate([[m], blocks]))
+
+
 def gauss_data(data):
     """bin/gaussian_cauchy.ml log_like_gaussian: state = (mu[nd], sigma[nd])."""
     data = np.asarray(data, dtype=np.float64)

@@ -275,6 +275,7 @@ typedef struct {
   int nmix; struct mix_comp* mix; int mix_kd;  /* MIXTURE (combine_jump_proposals) */
   double de_mh, de_sigma; int64_t de_M; const double* de_pts;   /* DE: samples [M][D] */
   const double* raw_lik;                       /* the caller's likelihood parameters */
+  int ngm; double* gm;                         /* GAUSS_MIX: per component mu/s[D], 1/s[D], C */
 } prep_t;
 
 /* one component of Mcmc.combine_jump_proposals (mcmc.ml:165-185): normalised weight p, log p,
@@ -288,7 +289,7 @@ struct mix_comp {
 };
 
 static void prep_free(prep_t* p) {
-  free(p->mu); free(p->isig); free(p->ctr); free(p->s);
+  free(p->mu); free(p->isig); free(p->ctr); free(p->s); free(p->gm);
   for (int c = 0; c < p->nmix; ++c) { free(p->mix[c].inv_s); free(p->mix[c].width); }
   free(p->mix);
 }
@@ -331,6 +332,23 @@ static int prep_model(const or_model* m, prep_t* p) {
       p->nd = (int)q[0];
       p->data = q + 1;
       p->nsamp = (m->n_lik_params - 1) / p->nd;
+      break;
+    case MCG_LIK_GAUSS_MIX:
+      /* m, then per component mu[D], sigma[D]; each component's DIAG constants as above */
+      p->ngm = (int)q[0];
+      if (p->ngm < 1 || p->ngm > MCG_LIK_MIX_MAX || m->n_lik_params != 1 + (int64_t)p->ngm * 2 * D) return -1;
+      p->gm = (double*)malloc(sizeof(double) * (size_t)p->ngm * (2 * D + 1));
+      for (int c = 0; c < p->ngm; ++c) {
+        const double* mu = q + 1 + (size_t)c * 2 * D;
+        double* o = p->gm + (size_t)c * (2 * D + 1);
+        double C = 0.0;
+        for (int d = 0; d < D; ++d) {
+          o[D + d] = 1.0 / mu[D + d];
+          o[d] = mu[d] * o[D + d];
+          C = C + (NEG_HALF_LOG_2PI - log(mu[D + d]));
+        }
+        o[2 * D] = C;
+      }
       break;
     default: return -1;
   }
@@ -446,12 +464,30 @@ static double lik_literal(const prep_t* p, const double* x) {
     double dx = (sqrt(ss) - q[D]) / q[D + 1];
     return (-0.91893853320467274178 - log(q[D + 1])) - 0.5 * dx * dx;
   }
+  if (p->lik == MCG_LIK_GAUSS_MIX) {
+    /* test/nested_test.ml:52-57: log ((exp g1) +. (exp g2) +. ...), left to right, each g_i
+       Stats.log_multi_gaussian mu_i sigma_i x (stats.ml:103-108) */
+    double sum = 0.0;
+    for (int c = 0; c < p->ngm; ++c) {
+      const double* mu = q + 1 + (size_t)c * 2 * D;
+      const double* sg = mu + D;
+      double result = 0.0;
+      for (int i = 0; i < D; ++i) {
+        double dx = (x[i] - mu[i]) / sg[i];
+        result = result + ((-0.91893853320467274178 - log(sg[i])) - 0.5 * dx * dx);
+      }
+      const double e = exp(result + 0.0);
+      sum = c == 0 ? e : sum + e;
+    }
+    return log(sum);
+  }
   return NAN;
 }
 
 static double lik_eval(const prep_t* p, const double* x) {
   int D = p->D;
-  if (g_literal && (p->lik == MCG_LIK_DIAG_GAUSS || p->lik == MCG_LIK_GAUSS_SHELL)) return lik_literal(p, x);
+  if (g_literal && (p->lik == MCG_LIK_DIAG_GAUSS || p->lik == MCG_LIK_GAUSS_SHELL || p->lik == MCG_LIK_GAUSS_MIX))
+    return lik_literal(p, x);
   double A[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   switch (p->lik) {
     case MCG_LIK_FLAT: return 0.0;
@@ -474,6 +510,27 @@ static double lik_eval(const prep_t* p, const double* x) {
         A[k] = fma(t, t, A[k]);
       }
       return p->C - 0.5 * canon8(A);
+    }
+    case MCG_LIK_GAUSS_MIX: {
+      /* canonical: each component's DIAG canonical sum, folded by a one-pass max-shifted
+         log-sum-exp in component order (csrc/mcg_mh_kernel.h eval_lik) */
+      double M = -INFINITY, sacc = 0.0;
+      for (int c = 0; c < p->ngm; ++c) {
+        const double* qc = p->gm + (size_t)c * (2 * D + 1);
+        double B[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int d = 0; d < D; ++d) {
+          double e = fma(x[d], qc[D + d], -qc[d]);
+          B[(d >> 2) & 7] = fma(e, e, B[(d >> 2) & 7]);
+        }
+        const double g = qc[2 * D] - 0.5 * canon8(B);
+        if (g > M) {
+          sacc = sacc * or_exp(M - g) + 1.0;
+          M = g;
+        } else {
+          sacc = sacc + or_exp(g - M);
+        }
+      }
+      return M == -INFINITY ? M : M + or_log(sacc);
     }
     case MCG_LIK_GAUSS_SHELL: {
       for (int d = 0; d < D; ++d) {
@@ -751,7 +808,8 @@ static int mh_step(const prep_t* p, uint64_t seed, uint32_t gid, uint64_t T, cha
  * canonical MH steps (what the GPU does) from (x [D][N], ll, lp) at global step step0; at every
  * step the SAME proposal is also judged with the literal arithmetic (literal ll of the current
  * and proposed points, glibc log of the same uniform).  flips[c] counts the steps whose accept
- * decision differs; max_rel_ll = max over all proposals of |ll_literal - ll_canonical| / |ll|;
+ * decision differs; max_rel_ll = max over all proposals of |ll_literal - ll_canonical| /
+ * max(|ll|, 1) (relative, but absolute where ll crosses 0: near a peak the O(1) terms cancel);
  * min_margin = the smallest |log u - ratio| seen (how close any decision came to a flip). */
 int or_mh_literal_shadow(const or_model* m, uint64_t seed, int64_t N, uint64_t step0, int64_t nsteps,
                          const double* x, const double* ll, const double* lp, int64_t* flips,
@@ -759,7 +817,10 @@ int or_mh_literal_shadow(const or_model* m, uint64_t seed, int64_t N, uint64_t s
   prep_t p;
   if (prep_model(m, &p) != 0 || g_literal) return -1;
   const int D = p.D;
-  if (!(p.lik == MCG_LIK_DIAG_GAUSS || p.lik == MCG_LIK_GAUSS_SHELL) || D > 256) { prep_free(&p); return -1; }
+  if (!(p.lik == MCG_LIK_DIAG_GAUSS || p.lik == MCG_LIK_GAUSS_SHELL || p.lik == MCG_LIK_GAUSS_MIX) || D > 256) {
+    prep_free(&p);
+    return -1;
+  }
   step_probe* pr = (step_probe*)malloc(sizeof(step_probe));
   double mrel = 0.0, mmar = INFINITY;
   for (int64_t i = 0; i < N; ++i) {
@@ -771,8 +832,8 @@ int or_mh_literal_shadow(const or_model* m, uint64_t seed, int64_t N, uint64_t s
       const double llx_lit = lik_literal(&p, c.x), lpx = c.lp;
       mh_step(&p, seed, (uint32_t)i, step0 + (uint64_t)t, &c, pr);
       const double lly_lit = lik_literal(&p, pr->y);
-      if (isfinite(pr->lly) && pr->lly != 0.0) {
-        const double rel = fabs(lly_lit - pr->lly) / fabs(pr->lly);
+      if (isfinite(pr->lly)) {
+        const double rel = fabs(lly_lit - pr->lly) / fmax(fabs(pr->lly), 1.0);
         if (rel > mrel) mrel = rel;
       }
       const double ratio_lit = (lly_lit + pr->lpy) - (llx_lit + lpx);

@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol(gpu_lib):
 
 def test_abi_version_and_arch(gpu_lib):
     L = gpu_lib.lib()
-    assert L.mcg_abi_version() == 2
+    assert L.mcg_abi_version() == 3
     assert L.mcg_device_arch() == b"gfx950"
 
 

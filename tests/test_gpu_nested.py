@@ -113,14 +113,27 @@ def test_nested_single_gaussian_reference_test(T):
 
 
 @pytest.mark.gpu
-def test_nested_observer_sees_every_dead_point(T):
+@pytest.mark.parametrize("grow", [False, True])
+def test_nested_observer_sees_every_dead_point(T, grow):
+    """The observer (nested.ml:136) sees every dead point -- row, ll and lp -- in retirement
+    order.  grow=True: a D = 6 Gaussian of width 0.01 retires ~25 nlive points, past the dead
+    buffer's first capacity (16 nlive), so the buffer grows while two batches are in flight: the
+    observer must read each batch's rows from the buffer that batch wrote."""
     from mcmc_amd import Context, nested
-    lik, pri = unit_square_gauss(T)
+    if grow:
+        D = 6
+        lik, pri = T.diag_gauss(0.5 * np.ones(D), 0.01 * np.ones(D)), T.box(np.zeros(D), np.ones(D))
+    else:
+        lik, pri = unit_square_gauss(T)
     seen = []
     out = nested.nested_evidence(lik, pri, nlive=200, nmcmc=20, k=8, ctx=Context(seed=4),
-                                 observer=lambda s: seen.append(s[1]))
+                                 observer=lambda s: seen.append(s))
     assert len(seen) == out.n_dead
-    np.testing.assert_array_equal(np.array(seen), out.ll[:out.n_dead])
+    if grow:
+        assert out.n_dead > 16 * 200
+    np.testing.assert_array_equal(np.array([s[0] for s in seen]), out[2][:out.n_dead])
+    np.testing.assert_array_equal(np.array([s[1] for s in seen]), out.ll[:out.n_dead])
+    np.testing.assert_array_equal(np.array([s[2] for s in seen]), out.lp[:out.n_dead])
 
 
 def shell_log_z(D, r, w, half):

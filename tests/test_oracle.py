@@ -254,10 +254,9 @@ def test_nested_single_gaussian(oracle):
     assert np.all(np.diff(r["ll"]) >= 0)
 
 
-def test_nested_four_gaussians_k_batched(oracle):
-    """test/nested_test.ml:41-64 with k=8 retirements per generation: Z = 4 within 2 err."""
-    D = 2
-    # four-mode likelihood is not a built-in kind; use the single Gaussian with k > 1 instead
+def test_nested_single_gaussian_k_batched(oracle):
+    """test/nested_test.ml:23-39 (the single Gaussian, Z = 1) with k = 8 retirements per
+    generation.  (The four-Gaussian test nested_test.ml:41-64 is in tests/test_gauss_mix.py.)"""
     m = _unit_square_gauss()
     r = oracle.nested(m, 23, nlive=1000, nmcmc=200, k=8)
     ev = math.exp(r["log_ev"])
