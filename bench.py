@@ -52,16 +52,30 @@ def analytic_log_z(mu, sg, lo=-10.0, hi=10.0):
 
 
 def cpu_baseline(args, mu, sg, s):
-    """Oracle (C restatement, -O3 -march=x86-64-v3) on a bounded sample of the same workload, all granted cores."""
+    """The oracle (C restatement of the reference's MH step) on a bounded sample of the same
+    workload: every CPU this process may use (sched_getaffinity, capped at OMP_NUM_THREADS -- the
+    GPU box grants 16 CPUs per GPU and exports OMP_NUM_THREADS=16, while its affinity mask shows
+    the whole machine), built with -march=native on this host (oracle/Makefile `native`; the
+    portable library otherwise), median of 3 timed repeats.  Baseline only."""
+    import subprocess
     import oracle as O
     D = args.ndim
-    threads = int(os.environ.get("MCG_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    nproc = len(os.sched_getaffinity(0))
+    granted = int(os.environ.get("OMP_NUM_THREADS", nproc) or nproc)
+    threads = int(os.environ.get("MCG_CPU_THREADS", min(nproc, granted)))
+    build = "-O3 -march=native (built on this host)"
+    try:
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "native"], check=True,
+                       capture_output=True, timeout=180)
+        O.LIB_PATH = os.path.join(ROOT, "oracle", "_native", "liboracle.so")
+    except (OSError, subprocess.SubprocessError) as e:
+        build = "-O3 -march=x86-64-v3 (native build failed: %s)" % type(e).__name__
     m = O.Model(D, 1, np.concatenate([mu, sg]), 1,
                 np.concatenate([-10 * np.ones(D), 10 * np.ones(D), [-D * math.log(20.0)]]),
                 1, [s])
     rng = np.random.default_rng(7)
 
-    def run(nch, nsteps, nthreads=threads):
+    def run(nch, nsteps, nthreads):
         x0 = rng.normal(mu[:, None], sg[:, None], size=(D, nch))
         ll = np.array([m.loglik(x0[:, i]) for i in range(nch)])
         lp = np.full(nch, m.logprior(x0[:, 0]))
@@ -70,21 +84,23 @@ def cpu_baseline(args, mu, sg, s):
                  record_accept=False, accumulate=False, nthreads=nthreads)
         return time.perf_counter() - t
 
+    def median_rate(nch, nthreads, seconds):
+        dt = run(nch, 20, nthreads)                       # size the sample
+        nsteps = max(20, int(seconds * (nch * 20 / dt) / nch))
+        rates = sorted(nch * nsteps / run(nch, nsteps, nthreads) for _ in range(3))
+        return rates[1], nsteps, rates
+
     nch = 64 * threads * 4
-    dt = run(nch, 20)
-    rate = nch * 20 / dt
-    nsteps = max(20, int(args.cpu_seconds * rate / nch))
-    dt = run(nch, nsteps)
-    # one core: the single-threaded ocamlopt-equivalent proxy, ~3 s sample
+    rate, nsteps, reps = median_rate(nch, threads, args.cpu_seconds)
+    # one core: the single-threaded ocamlopt-equivalent proxy
     n1 = 256
-    d1 = run(n1, 20, 1)
-    s1 = max(20, int(3.0 * (n1 * 20 / d1) / n1))
-    d1 = run(n1, s1, 1)
-    return dict(value=nch * nsteps / dt, unit="MH steps/s", cores=threads, kind="port",
-                sample="%d chains x %d steps of the C2 target (oracle/oracle.c, -O3 -march=x86-64-v3, %d threads)"
-                       % (nch, nsteps, threads),
-                single_core_value=n1 * s1 / d1,
-                single_core_sample="%d chains x %d steps, 1 thread" % (n1, s1))
+    rate1, s1, reps1 = median_rate(n1, 1, 1.0)
+    return dict(value=rate, unit="MH steps/s", cores=threads, kind="port", nproc=nproc,
+                repeats=[float(r) for r in reps], statistic="median of 3",
+                sample="%d chains x %d steps of the C2 target per repeat (oracle/oracle.c, %s, %d threads "
+                       "of %d in the affinity mask)" % (nch, nsteps, build, threads, nproc),
+                single_core_value=rate1, single_core_repeats=[float(r) for r in reps1],
+                single_core_sample="%d chains x %d steps, 1 thread, median of 3" % (n1, s1))
 
 
 def pmc_traffic(D, N, S):
@@ -146,21 +162,26 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
     # MCG_BENCH_BACKEND=gloo rehearses the multi-rank flow with CPU collectives (e.g. several ranks
-    # sharing one GPU: MCG_BENCH_DEVICE=0); the driver's runs use RCCL ("nccl"), one GPU per rank
+    # sharing one GPU: MCG_BENCH_DEVICE=0); the driver's runs use RCCL ("nccl"), one GPU per rank.
+    # With RCCL the process group is up at N = 1 too (a one-rank group on an in-process store), so
+    # the timed region's all-gather of the tile partials runs over RCCL at every N.
     backend = os.environ.get("MCG_BENCH_BACKEND", "nccl")
+    dist = world > 1 or backend == "nccl"
     if os.environ.get("MCG_BENCH_DEVICE"):
         local = int(os.environ["MCG_BENCH_DEVICE"])
     if dist:
         import torch.distributed as tdist
         torch.cuda.set_device(local)
-        tdist.init_process_group(backend)
+        if world > 1:
+            tdist.init_process_group(backend)
+        else:
+            tdist.init_process_group(backend, store=tdist.HashStore(), rank=0, world_size=1)
     dev = torch.device("cuda", local)
     comm = dev if backend == "nccl" else None      # device of the collectives' tensors
 
     from mcmc_amd import Context, targets as T
-    from mcmc_amd.parallel import reduce_stats
+    from mcmc_amd.parallel import reduce_stats, reduce_stats_device
 
     D, N, S = args.ndim, args.chains, args.sweeps
     mu, sg, s = c2_target(D)
@@ -181,13 +202,19 @@ def main():
     ctx.run(nbin=args.warmup * S, nskip=1, n_rec=1, record_x=False, record_llp=False,
             record_accept=False, accumulate=True)
     ctx.set_timing(True)
+    if dist:      # the communicator is created by its first collective: not inside the timed region
+        tdist.all_reduce(torch.zeros(1, dtype=torch.float64, device=comm))
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         ctx.run(nbin=0, nskip=1, n_rec=S, record_x=False, record_llp=False, record_accept=False,
                 accumulate=True, append=True)
-    # end-of-run reduction: tile kernel -> RCCL all-gather of tile partials -> host combine
-    mean, sd, log_z_hm = reduce_stats(D, ctx.tile_stats(), device=comm)
+    # end-of-run reduction: tile kernel into a device buffer -> RCCL all-gather of the tile
+    # partials (device to device) -> host combine; gloo rehearsals gather host tiles
+    if comm is not None:
+        mean, sd, log_z_hm = reduce_stats_device(ctx, comm)
+    else:
+        mean, sd, log_z_hm = reduce_stats(D, ctx.tile_stats(), device=comm)
     barrier()
     elapsed = time.perf_counter() - t0
     if dist:

@@ -232,8 +232,13 @@ int mcg_reset_counters(mcg_ctx* ctx);
    bit-identical results on 1/2/4/8 GPUs. */
 int64_t mcg_num_tiles(const mcg_ctx* ctx);
 int mcg_tile_stats(mcg_ctx* ctx, double* tiles /*[ntiles][2D+3]*/);
-/* device pointer of the tile partials (for a device-side all-gather, e.g. RCCL) */
+/* device pointer of the tile partials (for a device-side all-gather, e.g. RCCL); the tile
+   kernel is enqueued on the context's stream (mcg_sync before another stream reads them) */
 int mcg_tile_stats_device(mcg_ctx* ctx, void** dev_ptr, int64_t* ntiles);
+/* the tile partials written straight into a caller-owned device buffer of at least
+   mcg_num_tiles(ctx) x (2D+3) doubles on the context's device (e.g. the send buffer of an RCCL
+   all-gather), complete when this returns */
+int mcg_tile_stats_into(mcg_ctx* ctx, double* dev_tiles);
 /* Stats.multi_mean / multi_std (stats.ml:58-87, std with n-1) and the harmonic-mean evidence
    (evidence.ml:101-107) in log space: log Z = log n - logsumexp(-ll). */
 int mcg_combine_tiles(int32_t ndim, int64_t ntiles, const double* tiles, double* mean, double* sd,

@@ -57,28 +57,17 @@ __device__ __forceinline__ void swap16(double& a, double& b) {
 // v + v[lane ^ 32] and v + v[lane ^ 16] with the same two swaps (VALU, no ds_bpermute round
 // trip on the step's serial chain): after swap32(a, b) of two copies of v, a + b holds the pair
 // {v[i], v[i ^ 32]} in every lane (in either order: the sum is the same bits); likewise swap16
-#ifndef MCG_FC_SWAP_SUM
-#define MCG_FC_SWAP_SUM 1
-#endif
-__device__ __forceinline__ void swap32(double& a, double& b);
-__device__ __forceinline__ void swap16(double& a, double& b);
 __device__ __forceinline__ double sum_xor32(double v) {
-  if constexpr (!MCG_FC_SWAP_SUM) return v + __shfl_xor(v, 32, 64);
   double a = v, b = v;
   swap32(a, b);
   return a + b;
 }
 __device__ __forceinline__ double sum_xor16(double v) {
-  if constexpr (!MCG_FC_SWAP_SUM) return v + __shfl_xor(v, 16, 64);
   double a = v, b = v;
   swap16(a, b);
   return a + b;
 }
 __device__ __forceinline__ int and_xor32_16(int v) {
-  if constexpr (!MCG_FC_SWAP_SUM) {
-    v &= __shfl_xor(v, 32, 64);
-    return v & __shfl_xor(v, 16, 64);
-  }
   auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
   v = (int)r[0] & (int)r[1];
   auto t = __builtin_amdgcn_permlane16_swap(v, v, false, false);
@@ -91,47 +80,15 @@ __device__ __forceinline__ void transpose_quadrants(double* v) {
   swap16(v[2], v[3]);
 }
 
-#ifndef MCG_FC_NRM_BATCH
-#define MCG_FC_NRM_BATCH 1   // the four normals of a Philox call gather together (one LDS wait)
-#endif
-#ifndef MCG_FC_SELECT_UNCOND
-// experiment: the accept select reads the park unconditionally.  Left as `acc ? park : x` the
-// compiler sinks each read under its own exec-masked branch (16 branch pairs, ~80 SALU a step),
-// but only accepting lanes read: same-box A/B 10.67 (branches) vs 11.04 ms (unconditional) per
-// launch -- the park reads cost more LDS time than the branches cost issue slots
-#define MCG_FC_SELECT_UNCOND 0
-#endif
-#ifndef MCG_FC_RNG_AHEAD
-#define MCG_FC_RNG_AHEAD 1
-#endif
-#ifndef MCG_FC_YREG
-// column blocks of the proposed point kept in registers (the accept select is then a v_cndmask
-// pair per dim, no LDS write and exec-masked read); the rest is parked in LDS.  Since the
-// round-3 register savings the whole point fits beside the chain state at two waves per SIMD
-// (254 VGPRs, no scratch): same-box A/B at C5, 16 in registers 10.53 -> 10.19 ms per launch
-// (6.21e9 -> 6.42e9), 8 in registers 10.34 ms (profiles/r03/c5_yreg); bit-exact either way
-#define MCG_FC_YREG 64
-#endif
-#ifndef MCG_FC_M2LDS
-// experiment: the Welford M2 accumulators live in LDS ([kb / 2][thread] double2; 64 KB per
-// 512-thread workgroup) instead of 32 registers (223 VGPRs, still two waves per SIMD): same-box
-// A/B 10.21 -> 10.77 ms per launch, and 11.0 ms with MCG_FC_PIPE on top (profiles/r03/c5_m2lds);
-// bit-exact, left off
-#define MCG_FC_M2LDS 0
-#endif
-#ifndef MCG_FC_PIPE
-#define MCG_FC_PIPE 0        // experiment: each normal's table rows gathered one normal ahead
-#endif
-
 // 512-thread workgroups, one per CU: eight waves = two per SIMD, sharing one copy of the tables
 constexpr int kFcBlock = 512;
 
 // Per step: the lane's four Philox calls one at a time -> 4 normals -> quadrant
 // transpose -> 4 proposed coordinates; each coordinate's residual r = y - mu goes straight into
 // the matrix core (row blocks ib with 4 ib <= kb, four accumulators, kb ascending per block, so
-// every e_i is still the oracle's fma chain), and y itself is kept until the accept test: in
-// registers (MCG_FC_YREG, default), or parked in LDS.  Chain state, Welford accumulators, the
-// proposed point and the four MFMA accumulators fit the 256 registers of two waves per SIMD.
+// every e_i is still the oracle's fma chain), and y itself is kept in registers until the accept
+// test (a v_cndmask pair per dim).  Chain state, Welford accumulators, the proposed point and the
+// four MFMA accumulators fit the 256 registers of two waves per SIMD.
 // UNI: one proposal scale and one box for every dim (MhArgs::uni): scalars, no per-step loads;
 // UNI == 2: the box is symmetric, [-h, h], tested as |y| <= h (mcg_mh_kernel.h)
 template <int D, int UNI>
@@ -144,8 +101,6 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
   // mu by lane quadrant, [q][kb] = mu[4 kb + q], then the likelihood normaliser C and the prior
   // box's log density (per-step global loads of these were in-order vmcnt waits on every step)
   __shared__ double s_mu[D + 2];
-  constexpr int YR = MCG_FC_YREG < NL ? MCG_FC_YREG : NL;  // column blocks kept in registers
-  __shared__ double s_y[(NL - YR > 0 ? NL - YR : 1) * kFcBlock];   // parked rest, [kb - YR][thread]
   for (int i = threadIdx.x; i < kLogTabN; i += blockDim.x) s_lt[i] = kLogTab[i];
   for (int i = threadIdx.x; i < kNrmTabN; i += blockDim.x) s_nt[i] = kNrmTab[i];
   for (int i = threadIdx.x; i < D; i += blockDim.x) s_mu[(i & 3) * (D / 4) + (i >> 2)] = a.lik[i];
@@ -176,7 +131,6 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
   const Rng rng{a.k0, a.k1};
   const uint32_t gid = a.chain_offset + (uint32_t)c;
   auto dim = [&](int kb) { return 4 * kb + q; };
-  double* const ypark = s_y + threadIdx.x;              // ypark[(kb - YR) * kFcBlock]
 
   double x[NL];
 #pragma unroll
@@ -191,25 +145,12 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
   auto hcs = [&](int l) -> double& { return s_hm[(2 * l + 1) * kFcBlock + threadIdx.x]; };
   double hm_pv = 0.0;
   bool hm_pok = false;
-  double rmean[NL];
-#if MCG_FC_M2LDS
-  static_assert(NL % 2 == 0, "M2 pairs");
-  __shared__ double2 s_m2[(NL / 2) * kFcBlock];
-  double2* const m2p = s_m2 + threadIdx.x;              // m2p[(kb / 2) * kFcBlock]
-#else
-  double rm2[NL];
-#endif
+  double rmean[NL], rm2[NL];
   if (accum) {
 #pragma unroll
     for (int kb = 0; kb < NL; ++kb) {
       rmean[kb] = a.mean[(int64_t)dim(kb) * N + c];
-#if MCG_FC_M2LDS
-      const double v2 = a.m2[(int64_t)dim(kb) * N + c];
-      if (kb & 1) m2p[(kb / 2) * kFcBlock].y = v2;
-      else m2p[(kb / 2) * kFcBlock].x = v2;
-#else
       rm2[kb] = a.m2[(int64_t)dim(kb) * N + c];
-#endif
     }
 #pragma unroll
     for (int l = 0; l < NH; ++l) {
@@ -244,21 +185,6 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
     if (accum) {
       const double inv = inv_pf;
       inv_pf = a.inv_n[R + 1 - a.next_r0];
-#if MCG_FC_M2LDS
-#pragma unroll
-      for (int kp = 0; kp < NL / 2; ++kp) {
-        double2 m2 = m2p[kp * kFcBlock];
-        const double d0 = x[2 * kp] - rmean[2 * kp];
-        const double n0 = fma(d0, inv, rmean[2 * kp]);
-        m2.x = fma(d0, x[2 * kp] - n0, m2.x);
-        rmean[2 * kp] = n0;
-        const double d1 = x[2 * kp + 1] - rmean[2 * kp + 1];
-        const double n1 = fma(d1, inv, rmean[2 * kp + 1]);
-        m2.y = fma(d1, x[2 * kp + 1] - n1, m2.y);
-        rmean[2 * kp + 1] = n1;
-        m2p[kp * kFcBlock] = m2;
-      }
-#else
 #pragma unroll
       for (int kb = 0; kb < NL; ++kb) {
         const double delta = x[kb] - rmean[kb];
@@ -266,7 +192,6 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
         rm2[kb] = fma(delta, x[kb] - mnew, rm2[kb]);
         rmean[kb] = mnew;
       }
-#endif
       const int jr = (int)(R & (P - 1));
       if (q == jr) {
         hm_pv = -ll;
@@ -281,13 +206,11 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
   }
 
   double lu_own = 0.0;
-#if MCG_FC_RNG_AHEAD
   // Philox words one call ahead: call m + 1's (or the next step's call 0) are drawn right after
   // call m's normals, so their serial rounds issue between call m's MFMAs (the matrix pipe takes
   // one per ~66 clocks from a wave) instead of ahead of the next call's normals.  The words depend
   // only on (chain, step, call), never on the chain state.
   u32x4 w_ahead = rng(gid, (uint32_t)a.step_base, (uint32_t)q, TAG_MH, (uint32_t)(a.step_base >> 32));
-#endif
   for (int64_t t = 0; t < a.nsteps; ++t) {
     const uint64_t T = a.step_base + (uint64_t)t;
     const uint32_t tlo = (uint32_t)T, thi = (uint32_t)(T >> 32);
@@ -299,68 +222,31 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
     asm volatile("" : "+s"(qpri), "+s"(qprop));
     // ---- proposal y = x + s z (mcmc.ml:41) fused with e = U (y - mu) on the matrix cores ----
     bool ok = true;
-    double yreg[YR > 0 ? YR : 1];
+    double yreg[NL];
     dbl4 e[F::NIB];
 #pragma unroll
     for (int ib = 0; ib < F::NIB; ++ib) e[ib] = dbl4{0.0, 0.0, 0.0, 0.0};
-#if MCG_FC_PIPE
-    // the table gathers one normal ahead, across the Philox calls (the next call's words are
-    // drawn before its first normal's gathers go out)
-    u32x4 wcur = rng(gid, tlo, (uint32_t)q, TAG_MH, thi), wnext = wcur;
-    NrmPending pend = pnormal_issue(wcur.x, s_nt);
-#endif
 #pragma unroll
     for (int m = 0; m < F::NM; ++m) {
       // U fragments and mu are loop-invariant LDS reads: without a barrier the compiler hoists
       // all of them out of the step loop into ~110 registers
       asm volatile("" ::: "memory");
       double v[4];
-#if MCG_FC_PIPE
-      if (m + 1 < F::NM) wnext = rng(gid, tlo, (uint32_t)(4 * (m + 1) + q), TAG_MH, thi);
-      {
-        const uint32_t ww[4] = {wcur.x, wcur.y, wcur.z, wcur.w};
-        const uint32_t wn0 = wnext.x;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          NrmPending nx;
-          const bool more = k < 3 || m + 1 < F::NM;
-          if (more) nx = pnormal_issue(k < 3 ? ww[k + 1] : wn0, s_nt);
-          v[k] = pnormal_finish(pend);
-          if (more) pend = nx;
-        }
-      }
-      wcur = wnext;
-#else
-#if MCG_FC_RNG_AHEAD
       const u32x4 w = w_ahead;
-#else
-      const u32x4 w = rng(gid, tlo, (uint32_t)(4 * m + q), TAG_MH, thi);
-#endif
-#if MCG_FC_NRM_BATCH
-      pnormal4_lds(w, s_nt, v);
-#else
-      v[0] = pnormal(w.x, s_nt);
-      v[1] = pnormal(w.y, s_nt);
-      v[2] = pnormal(w.z, s_nt);
-      v[3] = pnormal(w.w, s_nt);
-#endif
-#if MCG_FC_RNG_AHEAD
+      pnormal4_lds(w, s_nt, v);            // the four normals' eight table gathers, one LDS wait
       if (m + 1 < F::NM) {
         w_ahead = rng(gid, tlo, (uint32_t)(4 * (m + 1) + q), TAG_MH, thi);
       } else {
         const uint64_t T1 = T + 1;
         w_ahead = rng(gid, (uint32_t)T1, (uint32_t)q, TAG_MH, (uint32_t)(T1 >> 32));
       }
-#endif
-#endif
       transpose_quadrants(v);                 // v[k'] = z[16 m + 4 k' + q]
 #pragma unroll
       for (int k2 = 0; k2 < 4; ++k2) {
         const int kb = 4 * m + k2;
         const int d = dim(kb);
         const double yv = fma(UNI ? a.uni_s : qprop[d], v[k2], x[kb]);
-        if (kb < YR) yreg[kb < YR ? kb : 0] = yv;
-        else ypark[(kb - YR) * kFcBlock] = yv;
+        yreg[kb] = yv;
         if constexpr (UNI == 2) ok = ok & (__builtin_fabs(yv) <= a.uni_hi);
         else ok = ok & (yv >= (UNI ? a.uni_lo : qpri[d])) & (yv <= (UNI ? a.uni_hi : qpri[D + d]));
         const double rv = yv - s_mu[q * NL + kb];
@@ -396,13 +282,7 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
     const double lu = __shfl(lu_own, (lane & 15) | (qq << 4), 64);
     const bool acc = lu < ratio;
 #pragma unroll
-    for (int kb = 0; kb < YR; ++kb) x[kb] = acc ? yreg[kb] : x[kb];
-#pragma unroll
-    for (int kb = YR; kb < NL; ++kb) {
-      double yv = ypark[(kb - YR) * kFcBlock];
-      if constexpr (MCG_FC_SELECT_UNCOND) asm volatile("" : "+v"(yv));
-      x[kb] = acc ? yv : x[kb];
-    }
+    for (int kb = 0; kb < NL; ++kb) x[kb] = acc ? yreg[kb] : x[kb];
     if (acc) {
       ll = lly;
       lp = lpy;
@@ -440,11 +320,7 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
 #pragma unroll
     for (int kb = 0; kb < NL; ++kb) {
       a.mean[o + 4 * kb * n] = rmean[kb];
-#if MCG_FC_M2LDS
-      a.m2[o + 4 * kb * n] = (kb & 1) ? m2p[(kb / 2) * kFcBlock].y : m2p[(kb / 2) * kFcBlock].x;
-#else
       a.m2[o + 4 * kb * n] = rm2[kb];
-#endif
     }
     hm_flush((r - 1) & ~(int64_t)(P - 1));
 #pragma unroll

@@ -304,92 +304,6 @@ __device__ __forceinline__ void pnormal4_lds(const u32x4 w, const double2* tab, 
   }
 }
 
-// Two Philox calls' eight normals: all sixteen gathers issued back to back; the first call's
-// four normals are evaluated after `lgkmcnt(8)` while the second call's gathers are still in
-// flight, the second's after `lgkmcnt(0)` (their latency hides behind the first call's
-// arithmetic).  The second call's rows are outputs of the issuing asm and inputs of the final
-// wait, so no instruction can read them before it.  Same operations as pnormal.
-#ifndef MCG_NRM_XP1
-#define MCG_NRM_XP1 0
-#endif
-typedef double dvec2 __attribute__((ext_vector_type(2)));
-struct Nrm4Rows {
-  dvec2 a[4], b[4];
-  double xp[4];
-  uint32_t sign[4];
-};
-// kXp: keep x' from the address computation (else it is recomputed from the word in finish,
-// three VALU per normal, to hold eight fewer VGPRs while the gathers are in flight)
-template <bool kXp>
-__device__ __forceinline__ double nrm_xp(uint32_t w) {
-  const double dv = (double)nrm_odd(w);
-  return __hiloint2double((int)nrm_frac_hi((uint32_t)__double2hiint(dv)), __double2loint(dv));
-}
-template <bool kXp>
-__device__ __forceinline__ void nrm4_addr(const u32x4 w, uint32_t base, uint32_t ad[4], Nrm4Rows& r) {
-  const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const double dv = (double)nrm_odd(ww[k]);
-    const uint32_t hi = (uint32_t)__double2hiint(dv);
-    ad[k] = base + ((hi >> 15) & (uint32_t)(kNrmSeg - 1)) * 16u;
-    if constexpr (kXp) r.xp[k] = __hiloint2double((int)nrm_frac_hi(hi), __double2loint(dv));
-    r.sign[k] = ww[k];
-  }
-}
-template <bool kXp>
-__device__ __forceinline__ void nrm4_finish(const Nrm4Rows& r, double z[4]) {
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    NrmPending q;
-    q.x = kXp ? r.xp[k] : nrm_xp<kXp>(r.sign[k]);
-    q.c32 = double2(r.a[k].x, r.a[k].y);
-    q.c10 = double2(r.b[k].x, r.b[k].y);
-    q.sign = r.sign[k];
-    z[k] = pnormal_finish(q);
-  }
-}
-// issue both calls' gathers; returns with the first call's rows landed (r0 usable)
-__device__ __forceinline__ void nrm8_issue(const u32x4 w0, const u32x4 w1, const double2* tab,
-                                           Nrm4Rows& r0, Nrm4Rows& r1) {
-  const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) double2*)tab;
-  uint32_t p[4], q[4];
-  nrm4_addr<true>(w0, base, p, r0);
-  nrm4_addr<MCG_NRM_XP1>(w1, base, q, r1);
-  asm volatile(
-      "ds_read_b128 %0, %16\n\t"
-      "ds_read_b128 %4, %16 offset:16384\n\t"
-      "ds_read_b128 %1, %17\n\t"
-      "ds_read_b128 %5, %17 offset:16384\n\t"
-      "ds_read_b128 %2, %18\n\t"
-      "ds_read_b128 %6, %18 offset:16384\n\t"
-      "ds_read_b128 %3, %19\n\t"
-      "ds_read_b128 %7, %19 offset:16384\n\t"
-      "ds_read_b128 %8, %20\n\t"
-      "ds_read_b128 %12, %20 offset:16384\n\t"
-      "ds_read_b128 %9, %21\n\t"
-      "ds_read_b128 %13, %21 offset:16384\n\t"
-      "ds_read_b128 %10, %22\n\t"
-      "ds_read_b128 %14, %22 offset:16384\n\t"
-      "ds_read_b128 %11, %23\n\t"
-      "ds_read_b128 %15, %23 offset:16384\n\t"
-      "s_waitcnt lgkmcnt(8)"
-      : "=&v"(r0.a[0]), "=&v"(r0.a[1]), "=&v"(r0.a[2]), "=&v"(r0.a[3]),
-        "=&v"(r0.b[0]), "=&v"(r0.b[1]), "=&v"(r0.b[2]), "=&v"(r0.b[3]),
-        "=&v"(r1.a[0]), "=&v"(r1.a[1]), "=&v"(r1.a[2]), "=&v"(r1.a[3]),
-        "=&v"(r1.b[0]), "=&v"(r1.b[1]), "=&v"(r1.b[2]), "=&v"(r1.b[3])
-      : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(q[0]), "v"(q[1]), "v"(q[2]), "v"(q[3])
-      : "memory");
-}
-// the second call's rows landed
-__device__ __forceinline__ void nrm8_wait(Nrm4Rows& r1) {
-  asm volatile("s_waitcnt lgkmcnt(0)"
-               : "+v"(r1.a[0]), "+v"(r1.a[1]), "+v"(r1.a[2]), "+v"(r1.a[3]),
-                 "+v"(r1.b[0]), "+v"(r1.b[1]), "+v"(r1.b[2]), "+v"(r1.b[3])
-               :
-               : "memory");
-}
-
 // log1p(r), r in [0,1] (Goldberg: r * log(1+r) / ((1+r)-1)); log-sum-exp on the portable
 // exp/log.  Drives the running nested-sampling estimate (nested.ml:139-142).
 __device__ __forceinline__ double plog1p(double r, const double2* tab = kLogTab) {
@@ -438,13 +352,9 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) {
 
 // value of lane ^ M.  M = 1, 2 stay inside a lane quad: a DPP quad_perm move (VALU, a few cycles)
 // instead of ds_bpermute (an LDS round trip on the serial chain of every MH / walker step).
-#ifndef MCG_DPP_XLANE
-#define MCG_DPP_XLANE 1
-#endif
 template <int M>
 __device__ __forceinline__ int xor_lane_i(int v) {
-  if constexpr (!MCG_DPP_XLANE) return __shfl_xor(v, M, 64);
-  else if constexpr (M == 1) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);   // [1,0,3,2]
+  if constexpr (M == 1) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);   // [1,0,3,2]
   else if constexpr (M == 2) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
   else if constexpr (M == 4) {
     // two row shifts, each writing one half of every 8-lane group (bank_mask: banks of 4 lanes):
@@ -456,7 +366,7 @@ __device__ __forceinline__ int xor_lane_i(int v) {
 }
 template <int M>
 __device__ __forceinline__ double xor_lane_d(double v) {
-  if constexpr (MCG_DPP_XLANE && (M == 1 || M == 2 || M == 4)) {
+  if constexpr (M == 1 || M == 2 || M == 4) {
     return __hiloint2double(xor_lane_i<M>(__double2hiint(v)), xor_lane_i<M>(__double2loint(v)));
   } else {
     return __shfl_xor(v, M, 64);

@@ -348,87 +348,33 @@ constexpr bool separable() {
          PROP == MCG_PROP_GAUSS;
 }
 
-#ifndef MCG_ACC_REG_MAX
-#define MCG_ACC_REG_MAX 8
-#endif
-
 template <int D, int P>
 struct AccumCfg {
-  // Welford accumulators of the lane's NL dims: in VGPRs when NL <= MCG_ACC_REG_MAX, else in LDS
-  // ([NL][256] doubles each, conflict-free) when they fit in 64 KiB per block, else
-  // read-modified-written in HBM at each record.
-  static constexpr bool kReg = Layout<D, P>::NL <= MCG_ACC_REG_MAX;
+  // Welford accumulators of the lane's NL dims: in VGPRs when NL <= 8, else in LDS ([NL][256]
+  // doubles each, conflict-free) when they fit in 64 KiB per block, else read-modified-written in
+  // HBM at each record.
+  static constexpr bool kReg = Layout<D, P>::NL <= 8;
   static constexpr bool kLds = !kReg && Layout<D, P>::NL <= 16;
   static constexpr int kLdsBytes = kLds ? 2 * Layout<D, P>::NL * 256 * 8 : 0;
 };
 
-#ifndef MCG_CONST_MODE
-#define MCG_CONST_MODE 1   // model constants of the fused step: 0 generic loads, 1 global, 2 LDS
-#endif
-
-#ifndef MCG_NRM_BATCH
-#define MCG_NRM_BATCH 1    // 1: the four normals of a Philox call gather together (one LDS wait);
-                           // 2: two calls' gathers in flight together (the second hides behind the first)
-#endif
-
-#ifndef MCG_NRM_PIPE
-#define MCG_NRM_PIPE 1     // three-wave kernels gather each normal's rows one normal ahead
-#endif
-
-#ifndef MCG_HM_LDS
-#define MCG_HM_LDS 1       // harmonic-mean partials of the record classes in LDS (not VGPRs)
-#endif
-
-#ifndef MCG_MH_MIN_WAVES
-#define MCG_MH_MIN_WAVES 1
-#endif
-
 // Waves per SIMD the kernel is built for.  The fused Gaussian step with at most 8 dims per lane
 // (C2: D 32 on 4 lanes) fits 168 registers -- three waves per SIMD -- when its normals are
-// evaluated one at a time (no batched gathers: their 32 in-flight registers would spill);
-// C2 1.87e10 -> 1.96e10 MH steps/s against two waves with batched gathers (A/B on one box).
-// Everything else is left to the compiler's register budget (two waves where it fits).
-#ifndef MCG_SCALAR_CONSTS
-#define MCG_SCALAR_CONSTS 1  // generic step: likelihood / prior constants through scalar loads
-#endif
-#ifndef MCG_UNI_NO_OPAQUE
-#define MCG_UNI_NO_OPAQUE 1
-#endif
-#ifndef MCG_KD_UAHEAD
-#define MCG_KD_UAHEAD 0    // experiment: the kD box-draw uniforms one step ahead (no change on C4)
-#endif
-#ifndef MCG_KD_PREFETCH
-#define MCG_KD_PREFETCH 1  // kD proposal: leaf two steps ahead, box and log q one step ahead
-#endif
-#ifndef MCG_PHILOX_SEQ
-#define MCG_PHILOX_SEQ 0   // experiment: the pipelined step's Philox calls computed one after another
-#endif
-#ifndef MCG_MH_NARROW_FOUR
-#define MCG_MH_NARROW_FOUR 0
-#endif
-#ifndef MCG_MH_THREE
-#define MCG_MH_THREE 1     // the fused Gaussian step with <= 8 dims per lane built for three waves per SIMD
-#endif
-#ifndef MCG_MH_FOUR
-#define MCG_MH_FOUR 0      // experiment: four waves per SIMD, UNI likelihood constants read from LDS
-#endif
+// evaluated one at a time, each normal's two table rows gathered one normal ahead (kPipe; batched
+// gathers' 32 in-flight registers would spill): C2 1.87e10 -> 1.96e10 MH steps/s against two
+// waves with batched gathers.  Everything else is left to the compiler's register budget, its
+// four normals of a Philox call gathered together (one LDS wait).
 template <int D, int P, int LIK, int PROP>
 struct MhShape {
-  static constexpr bool kThree = separable<LIK, PROP>() && Layout<D, P>::NL <= 8 && MCG_MH_MIN_WAVES <= 3 && MCG_MH_THREE;
-  // table gathers of the fused step one (or MCG_NRM_PIPE) normals ahead
-  static constexpr bool kPipe = MCG_NRM_PIPE != 0 && separable<LIK, PROP>() && Layout<D, P>::NL <= 8 &&
-                                (kThree || MCG_NRM_PIPE > 1);
-  static constexpr bool kFour = kThree && MCG_MH_FOUR;
-  // experiment: four waves per SIMD for the fused step with <= 4 dims per lane (D 32 on 8 lanes)
-  static constexpr bool kFourNarrow = kThree && MCG_MH_NARROW_FOUR && Layout<D, P>::NL <= 4;
-  static constexpr int kWaves = (kFour || kFourNarrow) ? 4 : kThree ? 3 : MCG_MH_MIN_WAVES;
-  // four waves per SIMD need two workgroups per CU within the LDS: 512 threads share the tables
-  static constexpr int kBlock = (kFour || kFourNarrow) ? 512 : 256;
-  static constexpr bool kBatchNormals = MCG_NRM_BATCH != 0 && !kThree;
+  static constexpr bool kThree = separable<LIK, PROP>() && Layout<D, P>::NL <= 8;
+  static constexpr bool kPipe = kThree;
+  static constexpr int kWaves = kThree ? 3 : 1;
+  static constexpr int kBlock = 256;
+  static constexpr bool kBatchNormals = !kThree;
   // harmonic-mean partials in LDS only where that was measured (C2: P = 4, three waves); a P = 1
   // instance would hold 2 x 8 x 256 doubles (32 KB) of LDS per workgroup for them, halving the
   // workgroups per CU of the small-D kD / mixture / generic kernels, so those keep them in VGPRs
-  static constexpr bool kHmLds = MCG_HM_LDS != 0 && (P >= 4 || kThree);
+  static constexpr bool kHmLds = P >= 4 || kThree;
 };
 
 // UNI: 0 = constants through pointers; 1 = isotropic proposal scale and one box [lo, hi] for
@@ -445,18 +391,6 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
   __shared__ double2 s_nt[kNrmTabN];
   for (int i = threadIdx.x; i < kLogTabN; i += blockDim.x) s_lt[i] = kLogTab[i];
   for (int i = threadIdx.x; i < kNrmTabN; i += blockDim.x) s_nt[i] = kNrmTab[i];
-#if MCG_CONST_MODE == 2
-  // model constants of the fused separable step staged in LDS: proposal scales [D], likelihood
-  // [2D + 1] (DIAG: mu/sigma, 1/sigma, C; SHELL: c, R, iw, C), prior box [2D + 1]
-  __shared__ double s_qp[kSeparable ? D : 1], s_ql[kSeparable ? 2 * D + 3 : 1], s_qr[kSeparable ? 2 * D + 1 : 1];
-  if constexpr (kSeparable) {
-    for (int i = threadIdx.x; i < D; i += blockDim.x) s_qp[i] = a.prop[i];
-    const int nl = LIK == MCG_LIK_DIAG_GAUSS ? 2 * D + 1 : LIK == MCG_LIK_GAUSS_SHELL ? D + 3 : 0;
-    for (int i = threadIdx.x; i < nl; i += blockDim.x) s_ql[i] = a.lik[i];
-    if (a.prior_kind != MCG_PRIOR_FLAT)
-      for (int i = threadIdx.x; i < 2 * D + 1; i += blockDim.x) s_qr[i] = a.pri[i];
-  }
-#endif
   __syncthreads();
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int sub = (int)(tid & (P - 1));
@@ -616,17 +550,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
   double lu_own = 0.0;
   // UNI (isotropic proposal scale, one box for every dim): the scale and the box are kernel
   // arguments (SGPRs), so the lane's likelihood constants fit in registers for the whole launch
-  constexpr bool kRcLds = MhShape<D, P, LIK, PROP>::kFour && UNI;
-  double rc_m[UNI && !kRcLds ? L::NL : 1], rc_i[UNI && !kRcLds ? L::NL : 1];
-  // kRcLds: (1/sigma, mu/sigma) of every dim staged in LDS, read per step (lanes of one `sub`
-  // read one address: a broadcast, conflict-free)
-  __shared__ double2 s_rc[kRcLds ? D : 1];
-  if constexpr (kRcLds) {
-    __syncthreads();
-    for (int d = threadIdx.x; d < D; d += blockDim.x)
-      s_rc[d] = double2(LIK == MCG_LIK_DIAG_GAUSS ? a.lik[D + d] : 0.0, LIK == MCG_LIK_FLAT ? 0.0 : a.lik[d]);
-    __syncthreads();
-  }
+  double rc_m[UNI ? L::NL : 1], rc_i[UNI ? L::NL : 1];
   // UNI: the likelihood normaliser and the box's log density in VGPRs too (a per-step cached
   // load of each put a vector-memory wait on every step's critical path)
   double rc_c = 0.0, rc_lp = 0.0;
@@ -635,7 +559,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
     rc_lp = a.prior_kind != MCG_PRIOR_FLAT ? a.pri[2 * D] : 0.0;
     asm volatile("" : "+v"(rc_c), "+v"(rc_lp));
 #pragma unroll
-    for (int i = 0; i < (kRcLds ? 0 : L::NCL); ++i)
+    for (int i = 0; i < L::NCL; ++i)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int d = L::valid(sub, i, k) ? L::dim(sub, i, k) : 0;
@@ -696,9 +620,8 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
         if (L::valid(sub, i, 2 * h + 1)) kd_u[j + 1] = u53(v.z, v.w);
       }
   };
-  if constexpr (PROP == MCG_PROP_KD_INTERP && MCG_KD_PREFETCH) {
+  if constexpr (PROP == MCG_PROP_KD_INTERP) {
     if (a.nsteps > 0) {
-      if constexpr (MCG_KD_UAHEAD) kd_uniforms(a.step_base);
       kd_leaf = kd_pick_leaf(a.step_base);
       kd_load_box(kd_leaf);
       kd_leaf_n = kd_pick_leaf(a.step_base + 1);
@@ -717,7 +640,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
     gconst* gpri = (gconst*)a.pri;
     gconst* gprop = (gconst*)a.prop;
     // (the fused step with UNI constants reads none of them: no per-step copies there)
-    if constexpr (!(kSeparable && UNI) || !MCG_UNI_NO_OPAQUE) asm volatile("" : "+s"(glik), "+s"(gpri), "+s"(gprop));
+    if constexpr (!(kSeparable && UNI)) asm volatile("" : "+s"(glik), "+s"(gpri), "+s"(gprop));
     const double* qlik = (const double*)glik;
     const double* qpri = (const double*)gpri;
     const double* qprop = (const double*)gprop;
@@ -725,17 +648,11 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
     if constexpr (kSeparable) {
       // fused: per Philox call -> 4 normals -> 4 proposed coordinates -> their terms of the
       // canonical sum and of the box test.  Keeps only x, y and 8/P accumulators live.
-#if MCG_CONST_MODE == 2
-      const double* qlik = s_ql;
-      const double* qpri = s_qr;
-      const double* qprop = s_qp;
-#elif MCG_CONST_MODE == 1
       typedef const __attribute__((address_space(1))) double gdouble;
       gdouble* qlik = (gdouble*)a.lik;
       gdouble* qpri = (gdouble*)a.pri;
       gdouble* qprop = (gdouble*)a.prop;
-      if constexpr (!UNI || !MCG_UNI_NO_OPAQUE) asm volatile("" : "+s"(qlik), "+s"(qpri), "+s"(qprop));
-#endif
+      if constexpr (!UNI) asm volatile("" : "+s"(qlik), "+s"(qpri), "+s"(qprop));
       double A[L::NA];
 #pragma unroll
       for (int j = 0; j < L::NA; ++j) A[j] = 0.0;
@@ -744,14 +661,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
       const bool box = a.prior_kind != MCG_PRIOR_FLAT;
       // the lane's Philox calls of this step (c2 = call index sub + P i) advanced together
       u32x4 wl[L::NCL];
-      // MCG_PHILOX_SEQ (pipelined path): the lane's calls one after the other, the first call's
-      // first gathers issued before the next call's rounds (which then hide their latency)
-      constexpr bool kSeqPhilox = MhShape<D, P, LIK, PROP>::kPipe && MCG_PHILOX_SEQ;
-      auto philox_call = [&](int i) {
-        const uint32_t ci = (uint32_t)(sub + P * i);
-        philox_multi<1>(&wl[i], gid, tlo, &ci, (TAG_MH << 16) | (thi & 0xFFFFu), rng.k0, rng.k1);
-      };
-      if constexpr (!kSeqPhilox) {
+      {
         uint32_t cidx[L::NCL];
 #pragma unroll
         for (int i = 0; i < L::NCL; ++i) cidx[i] = (uint32_t)(sub + P * i);
@@ -765,11 +675,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
         const double yv = fma(UNI ? a.uni_s : qprop[d], zk, x[4 * i + k]);
         y[4 * i + k] = yv;
         double rcm = 0.0, rci = 0.0;
-        if constexpr (kRcLds) {
-          const double2 rc = s_rc[d];
-          rci = rc.x;
-          rcm = rc.y;
-        } else if constexpr (UNI) {
+        if constexpr (UNI) {
           rcm = rc_m[4 * i + k];
           rci = rc_i[4 * i + k];
         }
@@ -796,11 +702,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
           const double yv = fma(UNI ? a.uni_s : qprop[d], z[k], x[4 * i + k]);
           y[4 * i + k] = yv;
           double rcm = 0.0, rci = 0.0;
-          if constexpr (kRcLds) {
-            const double2 rc = s_rc[d];
-            rci = rc.x;
-            rcm = rc.y;
-          } else if constexpr (UNI) {
+          if constexpr (UNI) {
             rcm = rc_m[4 * i + k];
             rci = rc_i[4 * i + k];
           }
@@ -822,7 +724,6 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
           }
         }
       };
-      constexpr int kStride = MCG_NRM_BATCH == 2 ? 2 : 1;
       if constexpr (MhShape<D, P, LIK, PROP>::kPipe) {
         // one normal at a time with its table rows gathered one normal ahead: the gathers of
         // normal m + 1 are in flight while normal m is finished and its dim's terms computed
@@ -832,37 +733,17 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
           return k == 0 ? w.x : k == 1 ? w.y : k == 2 ? w.z : w.w;
         };
         constexpr int NM = 4 * L::NCL;
-        constexpr int AH = MCG_NRM_PIPE;               // normals whose gathers are in flight
-        NrmPending q[AH + 1];
-        if constexpr (kSeqPhilox) philox_call(0);
-#pragma unroll
-        for (int m = 0; m < AH && m < NM; ++m) q[m] = pnormal_issue(word(m), s_nt);
-        if constexpr (kSeqPhilox) {
-#pragma unroll
-          for (int i = 1; i < L::NCL; ++i) philox_call(i);
-        }
+        NrmPending q[2];
+        q[0] = pnormal_issue(word(0), s_nt);
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
-          if (m + AH < NM) q[(m + AH) % (AH + 1)] = pnormal_issue(word(m + AH), s_nt);
-          dims1(m >> 2, m & 3, pnormal_finish(q[m % (AH + 1)]));
+          if (m + 1 < NM) q[(m + 1) & 1] = pnormal_issue(word(m + 1), s_nt);
+          dims1(m >> 2, m & 3, pnormal_finish(q[m & 1]));
         }
       } else
 #pragma unroll
-      for (int i = 0; i < L::NCL; i += kStride) {
+      for (int i = 0; i < L::NCL; ++i) {
         double z[4];
-        if constexpr (kStride == 2) {
-          if (i + 1 < L::NCL) {
-            // calls i and i + 1: sixteen gathers in flight, call i's arithmetic hides call i+1's
-            Nrm4Rows r0, r1;
-            nrm8_issue(wl[i], wl[i + 1], s_nt, r0, r1);
-            nrm4_finish<true>(r0, z);
-            dims(i, z);
-            nrm8_wait(r1);
-            nrm4_finish<MCG_NRM_XP1>(r1, z);
-            dims(i + 1, z);
-            continue;
-          }
-        }
         if constexpr (MhShape<D, P, LIK, PROP>::kBatchNormals) {
           pnormal4_lds(wl[i], s_nt, z);
         } else {
@@ -915,11 +796,11 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
             y[d + 1] = wrap_uniform(qprop[d + 1], qprop[D + d + 1], qprop[2 * D + d + 1], x[d + 1],
                                     u53(w.z, w.w));
         }
-      } else if constexpr (PROP == MCG_PROP_KD_INTERP && MCG_KD_PREFETCH) {
+      } else if constexpr (PROP == MCG_PROP_KD_INTERP) {
         static_assert(P == 1 || D % (4 * P) == 0, "KD: P lanes need D % 4P == 0");
         // Interpolate_pdf.draw (interpolate_pdf.ml:114-119) from the leaf and box loaded ahead;
         // dims 2c and 2c + 1 from call c (lane `sub`: the calls of its 4-dim blocks)
-        if constexpr (!MCG_KD_UAHEAD) kd_uniforms(T);
+        kd_uniforms(T);
         bool strict = true;
 #pragma unroll
         for (int j = 0; j < L::NL; ++j) {
@@ -927,7 +808,6 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
           y[j] = kd_lo[j] + (kd_hi[j] - kd_lo[j]) * kd_u[j];
           strict = strict && (y[j] > kd_lo[j]) && (y[j] < kd_hi[j]);
         }
-        if constexpr (MCG_KD_UAHEAD) kd_uniforms(T + 1);   // the next step's uniforms, off this step's chain
         if constexpr (P > 1) strict = and_lanes<P>(strict ? 1 : 0) != 0;
         // strictly inside its leaf box: that leaf (see below), whose log q came with the box
         lqy = kd_lqp;
@@ -953,31 +833,6 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
         kd_leaf = kd_leaf_n;
         kd_load_box(kd_leaf);
         kd_leaf_n = kd_pick_leaf(T + 2);
-        lf = lqy;   // log_jump_prob start proposed = log q(proposed)
-        lb = lq;    // log_jump_prob proposed start = log q(start)
-      } else if constexpr (PROP == MCG_PROP_KD_INTERP) {
-        static_assert(P == 1, "KD: one lane per chain");
-        // Interpolate_pdf.draw (interpolate_pdf.ml:114-119)
-        const u32x4 w = rng(gid, tlo, CALL_KD_PICK, TAG_MH, thi);
-        const uint32_t pick = randint(w.x, w.y, (uint32_t)a.kd_M);
-        const int leaf = a.kd_pt_leaf[pick];            // find_cell of the picked point
-        const double* __restrict__ bx = a.kd_box + (int64_t)leaf * 2 * D;
-        bool strict = true;
-#pragma unroll
-        for (int d = 0; d < D; d += 2) {
-          const u32x4 v = rng(gid, tlo, (uint32_t)(d >> 1), TAG_MH, thi);
-          y[d] = bx[d] + (bx[D + d] - bx[d]) * u53(v.x, v.y);
-          strict = strict && (y[d] > bx[d]) && (y[d] < bx[D + d]);
-          if (d + 1 < D) {
-            y[d + 1] = bx[d + 1] + (bx[D + d + 1] - bx[d + 1]) * u53(v.z, v.w);
-            strict = strict && (y[d + 1] > bx[d + 1]) && (y[d + 1] < bx[D + d + 1]);
-          }
-        }
-        // a point strictly inside a leaf box descends to that leaf (boxes nest and each split
-        // plane is a box face); only a draw rounded onto a face needs the descent
-        int ly = leaf;
-        if (!strict) ly = kd_find_leaf<D>(a.kd_nodes, a.kd_root, y);
-        lqy = a.kd_logq[ly];
         lf = lqy;   // log_jump_prob start proposed = log q(proposed)
         lb = lq;    // log_jump_prob proposed start = log q(start)
       }
@@ -1071,16 +926,15 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
         typedef const __attribute__((address_space(3))) double lconst;
         lly = eval_lik<D, P, LIK>(y, sub, a, (lconst*)s_kl);
         lpy = eval_prior<D, P>(y, sub, a, (lconst*)s_kp);
-      } else if constexpr (MCG_SCALAR_CONSTS) {
+      } else {
+        // likelihood / prior constants through scalar loads (the scalar cache and lgkmcnt, not
+        // a per-step vmcnt wait behind the proposal's loads)
         typedef const __attribute__((address_space(4))) double kconst;
         kconst* klik = (kconst*)a.lik;
         kconst* kpri = (kconst*)a.pri;
         asm volatile("" : "+s"(klik), "+s"(kpri));
         lly = eval_lik<D, P, LIK>(y, sub, a, klik);
         lpy = eval_prior<D, P>(y, sub, a, kpri);
-      } else {
-        lly = eval_lik<D, P, LIK>(y, sub, a, qlik);
-        lpy = eval_prior<D, P>(y, sub, a, qpri);
       }
     }
     // ---- Hastings ratio and accept test (mcmc.ml:42-56) ----
@@ -1100,10 +954,10 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
         const u32x4 wa = rng(gid, (uint32_t)Tj, CALL_ACCEPT, TAG_MH, (uint32_t)(Tj >> 32));
         lu_own = plog(u53(wa.x, wa.y), s_lt);
       }
-      if constexpr (P == 4 && MCG_DPP_XLANE) {    // quad broadcast of lane q (DPP)
+      if constexpr (P == 4) {                      // quad broadcast of lane q (DPP)
         lu = q == 0 ? quad_bcast_f64<0>(lu_own) : q == 1 ? quad_bcast_f64<1>(lu_own)
            : q == 2 ? quad_bcast_f64<2>(lu_own) : quad_bcast_f64<3>(lu_own);
-      } else if constexpr (P == 2 && MCG_DPP_XLANE) {   // pair broadcast of lane q (DPP)
+      } else if constexpr (P == 2) {               // pair broadcast of lane q (DPP)
         lu = q == 0 ? pair_bcast_f64<0>(lu_own) : pair_bcast_f64<1>(lu_own);
       } else {
         lu = __shfl(lu_own, (lane & ~(P - 1)) | q, 64);

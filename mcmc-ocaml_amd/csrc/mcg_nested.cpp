@@ -49,11 +49,6 @@ struct KeyBuf {
 struct NestedBufs {
   DevBuf x, ll, lp, nx, nll, nlp, tv, prefix, qadd, st, dead_x, dead_ll, dead_lp, rank, sync, trace, chk, rt_ix, rt_sc;
   KeyBuf keys[2], newk, newk_tmp;
-  // pipelined merges (a.pipe): the k lowest keys the walk reads, the second sorted-new-keys
-  // buffer, the merge stream and the per-generation hand-off events between the two streams
-  KeyBuf head, newk_tmp2;
-  hipStream_t s2 = nullptr;
-  hipEvent_t ev_sorted[2] = {nullptr, nullptr}, ev_full[2] = {nullptr, nullptr};
   int64_t dead_cap = 0;
   // pinned staging of two in-flight batches' dead (ll, lp) and their completion events
   double* h_stage[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -75,14 +70,6 @@ struct NestedBufs {
     if (h_st) (void)hipHostFree(h_st);
     for (auto e : done)
       if (e) (void)hipEventDestroy(e);
-    for (auto e : ev_sorted)
-      if (e) (void)hipEventDestroy(e);
-    for (auto e : ev_full)
-      if (e) (void)hipEventDestroy(e);
-    if (s2) {
-      (void)hipStreamSynchronize(s2);
-      (void)hipStreamDestroy(s2);
-    }
   }
 };
 
@@ -348,7 +335,7 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   }
   HC(hipMemcpyAsync(B.prefix.p, prefix.data(), (k + 1) * 8, hipMemcpyHostToDevice, s), "copy prefix");
   HC(hipMemcpyAsync(B.qadd.p, qadd.data(), k * 8, hipMemcpyHostToDevice, s), "copy qadd");
-  NestDevState st0{0.0, -HUGE_VAL, 0, 0, 0, -HUGE_VAL, INT64_MAX};
+  NestDevState st0{0.0, -HUGE_VAL, 0, 0, 0, -HUGE_VAL};
   HC(hipMemcpyAsync(B.st.p, &st0, sizeof st0, hipMemcpyHostToDevice, s), "copy state");
 
   NestArgs a{};
@@ -380,27 +367,9 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   if (const char* e = std::getenv("MCG_NEST_LANES"))
     a.lanes_hint = !std::strcmp(e, "wide") ? -1 : !std::strcmp(e, "narrow") ? -2 : std::atoi(e);
   a.fuse_retire = a.est_in_rank && std::getenv("MCG_NESTED_RETIRE_KERNEL") == nullptr;
-  // walker steps resolved in pairs across lane quads (nest_walk_pair_kernel) where the target
-  // allows it (box-folded register targets at 4 lanes, e.g. the shell at D = 16)
-  {
-    const char* e = std::getenv("MCG_NESTED_PAIR");
-    a.walk_pair = e ? std::atoi(e) : 0;
-  }
-  // pipelined merges (MCG_NESTED_PIPE=1): the full n-key merge of generation g
-  // runs on a second stream beside rank count g + 1 and the next walk reads only the k lowest
-  // keys (a 2k-key head merge).  Measured slower than the serial merge (the cross-stream event
-  // waits cost more per generation than the merge they hide), so it is not the default.
-  a.pipe = a.fuse_retire && std::getenv("MCG_NESTED_PIPE") != nullptr ? 1 : 0;
   // k <= 4096 (retire in the walk): sort + merge in one launch; MCG_NESTED_MERGE2=1 keeps the
   // counted-rank sort and the merge as two launches
-  const bool fused_merge = a.fuse_retire && !a.pipe && std::getenv("MCG_NESTED_MERGE2") == nullptr;
-  if (a.pipe) {
-    HC(B.head.ensure(k), "alloc head keys");
-    HC(B.newk_tmp2.ensure(k), "alloc new keys");
-    if (!B.s2) HC(hipStreamCreateWithFlags(&B.s2, hipStreamNonBlocking), "merge stream");
-    for (auto* e : {&B.ev_sorted[0], &B.ev_sorted[1], &B.ev_full[0], &B.ev_full[1]})
-      if (!*e) HC(hipEventCreateWithFlags(e, hipEventDisableTiming), "create event");
-  }
+  const bool fused_merge = a.fuse_retire && std::getenv("MCG_NESTED_MERGE2") == nullptr;
   // the walkers' draws of a generation in a table the previous merge fills (when it fits)
   a.rt_ix = nullptr;
   a.rt_sc = nullptr;
@@ -447,11 +416,6 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   const int base = in_tmp ? 1 : 0;                   // generation g reads keys[(base + g) % 2]
   HC(launch_key_sample(B.keys[base].l(), B.keys[base].t(), n, B.keys[base].sl(), B.keys[base].st(), s, a.st),
      "sample live keys");
-  if (a.pipe) {                                      // the first walk's head keys: keys[0, k)
-    HC(hipMemcpyAsync(B.head.l(), B.keys[base].l(), k * 8, hipMemcpyDeviceToDevice, s), "head keys");
-    HC(hipMemcpyAsync(B.head.t(), B.keys[base].t(), k * 8, hipMemcpyDeviceToDevice, s), "head keys");
-    HC(hipMemcpyAsync(B.head.s(), B.keys[base].s(), k * 4, hipMemcpyDeviceToDevice, s), "head keys");
-  }
   HC(launch_walk_draws(a, 0, s), "first draws");
 
   // Batches of generations, pipelined: while the GPU runs batch b + 1, the host appends batch b's
@@ -492,27 +456,6 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
     HC(hipMemsetAsync(B.trace.p, 0, 4 * 1024 * 8 * 8, s), "clear trace");
   }
 #endif
-  // pipelined merges: full merge of generation gm on the merge stream after event `after`:
-  // keys gm-1 (all n) with the sorted new keys of gm into keys gm; event ev_full[gm & 1]
-  auto full_merge = [&](int64_t gm, hipEvent_t after) -> hipError_t {
-    hipError_t e;
-    KeyBuf& c = B.keys[(base + gm) % 2];
-    KeyBuf& x = B.keys[(base + gm + 1) % 2];
-    KeyBuf& nk = (gm & 1) ? B.newk_tmp2 : B.newk_tmp;
-    NestArgs am = a;
-    am.key_ll = c.l();
-    am.key_tie = c.t();
-    am.key_slot = c.s();
-    am.key_samp_ll = c.sl();
-    am.key_samp_tie = c.st();
-    am.out_samp_ll = x.sl();
-    am.out_samp_tie = x.st();
-    am.mrep = gm * k;
-    if ((e = hipStreamWaitEvent(B.s2, after, 0)) != hipSuccess) return e;
-    if ((e = launch_merge_new(am, x.l(), x.t(), x.s(), nk.l(), nk.t(), nk.s(), B.s2)) != hipSuccess) return e;
-    if (check && (e = launch_check_sorted(x.l(), x.t(), n, gm, (long long*)B.chk.p + 1, B.s2)) != hipSuccess) return e;
-    return hipEventRecord(B.ev_full[gm & 1], B.s2);
-  };
   // Dead buffers replaced while batches were in flight, tagged with the sequence number of the
   // batch whose launch replaced them.  Once that batch is done, every kernel and grow copy that
   // touched the old buffer has finished (stream order), and so has the earlier batch whose
@@ -592,33 +535,6 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
 #ifdef MCG_NEST_TRACE
       a.trace = (g == trace_gen) ? (unsigned long long*)B.trace.p : nullptr;
 #endif
-      if (a.pipe) {
-        // generation g: walk g (reads the head keys) -> rank count g (sorts the new keys) ->
-        // head merge g (keys g-1 [k, 2k) with them).  The full merge of generation g - 1 runs on
-        // the merge stream beside rank count g (both are latency-bound; beside the walk it slowed
-        // the walkers), after walk g, and head merge g waits for it.  The batch's last full merge
-        // is enqueued at the batch's end (launch_batch below).
-        NestArgs aw = a;
-        aw.key_ll = B.head.l();
-        aw.key_tie = B.head.t();
-        aw.key_slot = B.head.s();
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        if (ctx->timing) timing_begin(ctx, &e0, &e1);
-        HC(walk(aw, s), "nested walk");
-        if (ctx->timing) timing_end(ctx, e0, e1, 1);
-        if (g > gen) {                                 // full merge g - 1 (its walk's batch)
-          HC(hipEventRecord(B.ev_sorted[g & 1], s), "record walk");
-          HC(full_merge(g - 1, B.ev_sorted[g & 1]), "full merge");
-        }
-        KeyBuf& nk = (g & 1) ? B.newk_tmp2 : B.newk_tmp;
-        HC(launch_sort_new_small(a, nk.l(), nk.t(), nk.s(), s), "sort new keys");
-        if (check) HC(launch_check_sorted(nk.l(), nk.t(), k, g, (long long*)B.chk.p, s), "check");
-        if (g > 0) HC(hipStreamWaitEvent(s, B.ev_full[(g - 1) & 1], 0), "head wait");
-        const int64_t ns = std::min<int64_t>(k, n - k);
-        HC(launch_head_merge(a, cur.l() + k, cur.t() + k, cur.s() + k, ns, nk.l(), nk.t(), nk.s(), B.head.l(),
-                             B.head.t(), B.head.s(), s), "head merge");
-        continue;
-      }
       hipEvent_t e0 = nullptr, e1 = nullptr;
       if (ctx->timing) timing_begin(ctx, &e0, &e1);
       HC(walk(a, s), "nested walk");
@@ -642,13 +558,6 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
       if (check) HC(launch_check_sorted(nk.l(), nk.t(), k, g, (long long*)B.chk.p, s), "check");
       HC(launch_merge_new(a, nxt.l(), nxt.t(), nxt.s(), nk.l(), nk.t(), nk.s(), s), "merge keys");
       if (check) HC(launch_check_sorted(nxt.l(), nxt.t(), n, g, (long long*)B.chk.p + 1, s), "check");
-    }
-    // the batch's last full merge (merge stream), then the state is read after it
-    if (a.pipe && G > 0) {
-      const int64_t gl = gen + G - 1;
-      HC(hipEventRecord(B.ev_sorted[(gl + 1) & 1], s), "record sorted");
-      HC(full_merge(gl, B.ev_sorted[(gl + 1) & 1]), "full merge");
-      HC(hipStreamWaitEvent(s, B.ev_full[gl & 1], 0), "batch merge wait");
     }
     HC(hipMemcpyAsync(&hst[q], B.st.p, sizeof(NestDevState), hipMemcpyDeviceToHost, s), "read state");
     HC(hipMemcpyAsync(B.h_stage[2 * q], (double*)B.dead_ll.p + gen * k, G * k * 8, hipMemcpyDeviceToHost, s),

@@ -24,7 +24,6 @@ struct NestDevState {
   int32_t error;
   long long gen_done;
   double max_ll;            // the largest live ll (the sorted keys' last): the stop test's L_max
-  long long stop_gen;       // the last generation of a stopped run (pipelined merges; else max)
 };
 
 // The stop / error flags and the generation count are read and written with agent-scope atomics
@@ -79,10 +78,6 @@ struct NestArgs {
                             // put the new points into the freed slots
   int32_t sym_box;          // box prior with lo[d] == -hi[d] for every d: tested as |y| <= hi
   int32_t lanes_hint;       // lanes per walker requested by MCG_NEST_LANES (0: the default)
-  int32_t walk_pair;        // nest_walk_pair_kernel where it applies (MCG_NESTED_PAIR)
-  int32_t pipe;             // pipelined key merges: the walk reads the head keys
-                            // (the k lowest), the full merge runs on a second stream beside the
-                            // next walk and skips generations past st->stop_gen only
   uint32_t row_bytes;       // D * 8: the draw table holds DE pairs as row byte offsets
   double* tv;               // ll + log dv of this generation's dead points (padded pow2)
   const double* prefix;     // [k+1] sum_{j'<j} log1p(-1/(n-j'))
@@ -106,43 +101,18 @@ struct NestArgs {
 #define NT_STAMP(kid, slot) do {} while (0)
 #endif
 
-#ifndef MCG_MERGE_WT
-#define MCG_MERGE_WT 1   // the fused merge's outputs as sc1 (write-through) stores
-#endif
-#ifndef MCG_TAB_WT
-#define MCG_TAB_WT 0     // experiment: the draw table (9.8 MB a generation at C3) as sc1 stores
-#endif
-#ifndef MCG_WALK_WT
-#define MCG_WALK_WT 0    // experiment: the walk's outputs and retired rows as sc1 stores
-#endif
-// an output store read by a later kernel: plain, or sc1 (a relaxed agent-scope atomic store:
-// written through and dropped from the XCD's L2, so less is left to write back when the kernel
-// ends)
-template <int WT, class T>
+// an output store read by a later kernel as sc1 (a relaxed agent-scope atomic store: written
+// through and dropped from the XCD's L2, so less is left to write back when the kernel ends);
+// the fused merge's outputs
+template <class T>
 __device__ __forceinline__ void wt_store(T* p, T v) {
-  if constexpr (WT != 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else *p = v;
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-#ifndef MCG_NEST_BOX_SKIP
-#define MCG_NEST_BOX_SKIP 1   // the walker skips its box test once the constraint implies it
-#endif
-#ifndef MCG_NEST_PREFETCH
-#define MCG_NEST_PREFETCH 4
-#endif
-#ifndef MCG_NEST_PFOLD
-#define MCG_NEST_PFOLD 1     // the walker's box prior folded into its constraint reduction
-#endif
-#ifndef MCG_NEST_SPEC
-#define MCG_NEST_SPEC 0      // experiment: walker steps in speculated pairs (slower: 28.3 -> 35.0 us at C3)
-#endif
-constexpr int kNestPrefetch = MCG_NEST_PREFETCH;    // DE steps whose partner rows are in flight
+constexpr int kNestPrefetch = 4;                   // DE steps whose partner rows are in flight
 // pad rows per draw-table half: the walker loads entries up to 3 prefetch groups past its step
 constexpr int kWalkTabPad = 3 * kNestPrefetch;
-#ifndef MCG_NEST_WALK_BLOCK
-#define MCG_NEST_WALK_BLOCK 64
-#endif
-constexpr int kNestWalkBlock = MCG_NEST_WALK_BLOCK;
+constexpr int kNestWalkBlock = 64;
 
 // The random numbers of walker step s (draw_new_live_point, nested.ml:50-74): the DE pair i != j
 // (pick_samples, mcmc.ml:199-203), the DE scale (1 with probability mode_hop, else
@@ -183,15 +153,8 @@ __device__ __forceinline__ void walk_draws_fill(const NestArgs& a, int64_t mrep,
     // byte offsets of the two rows: the walker adds them to the live set's base with no 64-bit
     // address arithmetic
     ix = (unsigned long long)((uint32_t)ix * a.row_bytes) | ((unsigned long long)((uint32_t)(ix >> 32) * a.row_bytes) << 32);
-    if constexpr (MCG_TAB_WT) {
-      wt_store<1>(&a.rt_ix[base + e], ix);
-      double* p = (double*)(a.rt_sc + base + e);
-      wt_store<1>(p, sc.x);
-      wt_store<1>(p + 1, sc.y);
-    } else {
-      a.rt_ix[base + e] = ix;
-      a.rt_sc[base + e] = sc;
-    }
+    a.rt_ix[base + e] = ix;
+    a.rt_sc[base + e] = sc;
   }
 }
 
@@ -350,7 +313,7 @@ struct WalkTarget {
       // the sum's rounding (< 1e-14 relative at D <= 64).  Once the box holds that whole ball
       // (late generations: the shell well inside the prior box), no such point is outside the
       // box and the box test cannot change a decision: the walk skips it (wave-uniform).
-      if constexpr (MCG_NEST_BOX_SKIP) {
+      {
         const double R = sqrt(s_out_hi) * (1.0 + 1e-9) + 1e-300;
         bool ok = s_out_hi >= 0.0 && R < inf;
 #pragma unroll
@@ -398,13 +361,13 @@ struct WalkTarget {
     }
   }
 
-  // The step's constraint and box prior as ONE cross-lane reduction (MCG_NEST_PFOLD): a lane
+  // The step's constraint and box prior as ONE cross-lane reduction: a lane
   // outside the box adds NaN to one of its canonical accumulators, inside it adds 0.0.  Every
   // accumulator is a sum of squares started from +0.0, so x + 0.0 = x and S keeps its bits; a
   // NaN makes S NaN, which the band test below counts as outside (!(S >= lo) is true for NaN),
   // so the step rejects for any threshold -- as prior() = -inf would.  Inside the box the
   // decision is constraint() && prior() > -inf exactly.  W = 4 register targets (the shell).
-  static constexpr bool kFold = kReg && LIK == MCG_LIK_GAUSS_SHELL && W == 4 && MCG_NEST_PFOLD;
+  static constexpr bool kFold = kReg && LIK == MCG_LIK_GAUSS_SHELL && W == 4;
   __device__ __forceinline__ double lp_box() const { return (SYM || box) ? lp_in : 0.0; }
   template <bool BOXT = true>   // BOXT = false: the box test is implied (box_test false)
   __device__ __forceinline__ bool constraint_box(const double* y, int sub, double thr) const {
@@ -551,9 +514,6 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
     const bool err = st_err;
     if (live - plse(st_est, live, lt) <= a.log_epsrel || err) {
       if (blockIdx.x == 0 && threadIdx.x == 0) {
-        // the previous generation was the last: its pipelined full merge (still running on the
-        // merge stream) completes; the ones after it skip
-        __hip_atomic_store(&a.st->stop_gen, (long long)(a.mrep / a.k) - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         nest_set(&a.st->stopped);
       }
       return;
@@ -574,11 +534,11 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
           if (wj >= a.k) break;
           const int rs = a.key_slot[wj];
           const int64_t m = a.mrep + wj;
-          wt_store<MCG_WALK_WT>(&a.dead_x[m * D + d], a.x[(int64_t)rs * D + d]);
+          a.dead_x[m * D + d] = a.x[(int64_t)rs * D + d];
           if (d == 0) {
             const double lls = a.ll[rs];
-            wt_store<MCG_WALK_WT>(&a.dead_ll[m], lls);
-            wt_store<MCG_WALK_WT>(&a.dead_lp[m], a.lp[rs]);
+            a.dead_ll[m] = lls;
+            a.dead_lp[m] = a.lp[rs];
             const double lv = a.st->log_vol + a.prefix[wj];
             __hip_atomic_store(a.tv + wj, lls + (lv + a.qadd[wj]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             a.rank[wj] = 0;
@@ -810,48 +770,6 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
       }
     }
     // the serial constrained steps
-#if MCG_NEST_SPEC
-    // two steps at a time, the second one speculated both ways: step u's proposal y0 and the two
-    // candidates of step u + 1 -- from y0 if step u accepts (ya), from the current point if it
-    // rejects (yr), the same arithmetic as computing it after the decision -- are judged
-    // together, three independent dependency chains on the walker's one wave instead of one,
-    // then the two accept decisions resolve in order.  The same states bit for bit.
-    static_assert(PD % 2 == 0, "speculated walker steps come in pairs");
-#pragma unroll
-    for (int u = 0; u < PD; u += 2) {
-      const bool live0 = s0 + u < nm, live1 = s0 + u + 1 < nm;
-      double y0[NL], ya[NL], yr[NL];
-#pragma unroll
-      for (int d = 0; d < NL; ++d) {
-        const double e1 = dsc_g[u + 1] * (bj[u + 1][d] - bi[u + 1][d]);
-        y0[d] = cur[d] + dsc_g[u] * (bj[u][d] - bi[u][d]);
-        ya[d] = y0[d] + e1;
-        yr[d] = cur[d] + e1;
-      }
-      refill(bi[u], ip_g[u]);                          // refill slots u, u + 1 with the rows of
-      refill(bj[u], jp_g[u]);                          // steps s + PD, s + PD + 1
-      refill(bi[u + 1], ip_g[u + 1]);
-      refill(bj[u + 1], jp_g[u + 1]);
-      const bool ok0 = tgt.constraint(y0, sub, a.m, thr);
-      const bool oka = tgt.constraint(ya, sub, a.m, thr);
-      const bool okr = tgt.constraint(yr, sub, a.m, thr);
-      const double lp0 = tgt.prior(y0, sub, a.m);
-      const double lpa = tgt.prior(ya, sub, a.m);
-      const double lpr = tgt.prior(yr, sub, a.m);
-      const double ninf = -__builtin_inf();
-      const double ml0 = ok0 ? lp0 : ninf, mla = oka ? lpa : ninf, mlr = okr ? lpr : ninf;
-      const bool acc0 = live0 && lu_g[u] < ml0 - cur_l;
-      const double cl1 = acc0 ? ml0 : cur_l;           // step u + 1 from the state u leaves
-      const double ml1 = acc0 ? mla : mlr;
-      const bool acc1 = live1 && lu_g[u + 1] < ml1 - cl1;
-#pragma unroll
-      for (int d = 0; d < NL; ++d) {
-        const double c1 = acc0 ? y0[d] : cur[d];
-        cur[d] = acc1 ? (acc0 ? ya[d] : yr[d]) : c1;
-      }
-      cur_l = acc1 ? ml1 : cl1;
-    }
-#else
 #pragma unroll
     for (int u = 0; u < PD; ++u) {
       const bool live = s0 + u < nm;
@@ -884,7 +802,6 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
         }
       }
     }
-#endif
     if constexpr (TAB) {
 #pragma unroll
       for (int u = 0; u < PD; ++u) {
@@ -906,248 +823,16 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   for (int i = 0; i < Lay::NCL; ++i)
 #pragma unroll
     for (int q = 0; q < W; ++q)
-      if (Lay::valid(sub, i, q)) wt_store<MCG_WALK_WT>(&a.nx[w * D + Lay::dim(sub, i, q)], cur[W * i + q]);
-  if (sub == 0) {
-    wt_store<MCG_WALK_WT>(&a.nll[w], nl);
-    wt_store<MCG_WALK_WT>(&a.nlp[w], np);
-    if (a.fuse_retire) {                               // the new point's key
-      wt_store<MCG_WALK_WT>(&a.newk_ll[w], nl);
-      wt_store<MCG_WALK_WT>(&a.newk_tie[w], -(long long)(a.mrep + w + 1));
-      wt_store<MCG_WALK_WT>(&a.newk_slot[w], ret_slot);
-    }
-    if (!(nl >= thr)) nest_set(&a.st->error);        // nested.ml:70-72 -> Failure
-  }
-}
-
-// ---- walker steps in resolved pairs across lanes (MCG_NEST_PAIR) ----
-// The same constrained DE walk as nest_walk_kernel (TAB, box-folded register target, 4 lanes per
-// walker), two steps at a time: step u's proposal y0 = cur + d_u and the two candidates of step
-// u + 1 -- ya = y0 + d_{u+1} if step u accepts, yr = cur + d_{u+1} if it rejects -- are judged
-// at once by three lane quads of the walker's 16-lane row (role 0: y0, 1: ya, 2: yr; role 3
-// repeats y0), and the two decisions resolve in order from one ballot of the three verdicts.
-// Every candidate is the arithmetic the serial walk would do, so the states are the same bit
-// for bit; a lane evaluates one candidate per PAIR of steps, so the serial chain per step is
-// halved.  A wave holds 4 walkers (16 per 512-thread workgroup: waves 0-3); waves 4-7 fill the
-// next generation's draw table and retire the workgroup's dead rows, at priority 0 on the SIMDs
-// the walkers hold at priority 3.
-template <int D, int LIK, bool SYM>
-__global__ void __launch_bounds__(512) nest_walk_pair_kernel(const NestArgs a) {
-  constexpr int P = 4;
-  using Lay = WalkLayout<D, P>;
-  using Tgt = WalkTarget<D, P, LIK, SYM>;
-  static_assert(Tgt::kFold && Lay::W == 4, "pair walker: box-folded 4-dim-block register targets");
-  constexpr int NL = Lay::NL;
-  constexpr int W = Lay::W;
-  constexpr int PD = kNestPrefetch;
-  static_assert(PD % 2 == 0, "pairs of steps");
-  NT_STAMP(0, 0);
-  const bool walker = threadIdx.x < 256;                  // waves 0-3; wave-uniform
-  const int lane = threadIdx.x & 63;
-  const int sub = lane & 3, role = (lane >> 2) & 3;
-  const int rowb = lane & ~15;                            // first lane of the walker's row
-  const int64_t w = (int64_t)blockIdx.x * 16 + ((threadIdx.x & 255) >> 4);
-  const bool active = w < a.k;
-  const int64_t wc = active ? w : 0;
-  const Rng rng{a.k0, a.k1};
-  const uint32_t wid = (uint32_t)(a.mrep + wc);
-  const uint32_t n = (uint32_t)a.n;
-  // first loads before the table staging and the stop test (as nest_walk_kernel)
-  const bool stopped0 = nest_stopped(a.st);
-  const double st_lv = a.st->log_vol, st_mx = a.st->max_ll, st_est = a.st->est;
-  const bool st_err = __hip_atomic_load(&a.st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-  const int64_t tbase = walk_tab_base(a, a.mrep);
-  const double2* const tsc_lane = a.rt_sc + tbase + wc;
-  const unsigned long long* const tix_lane = a.rt_ix + tbase + wc;
-  const uint32_t tk = (uint32_t)a.k;
-  auto tab_off = [&](int64_t st) -> uint32_t { return (uint32_t)st * tk; };
-  double thr = 0.0, ll_first = -__builtin_inf(), lp_first = 0.0;
-  int ret_slot = 0;
-  uint32_t s_first = 0;
-  double row_first[NL];
-  unsigned long long tix_cur[PD], tix_ring[PD];
-  double2 tsc_cur[PD];
-  Tgt tgt;
-  if (walker) {
-    tgt.load(a.m, sub);
-    thr = a.key_ll[a.k - 1];
-    ret_slot = a.key_slot[wc];
-    const u32x4 r = rng(wid, 0u, CALL_START, TAG_NEST_WALK, 0u);
-    s_first = randint(r.x, r.y, n);
-    ll_first = a.ll[s_first];
-    lp_first = a.lp[s_first];
-    const double* __restrict__ src = a.x + (int64_t)s_first * D;
-#pragma unroll
-    for (int i = 0; i < Lay::NCL; ++i)
-#pragma unroll
-      for (int q = 0; q < W; ++q) row_first[W * i + q] = src[Lay::dim(sub, i, q)];
-#pragma unroll
-    for (int u = 0; u < PD; ++u) {
-      tix_ring[u] = tix_lane[tab_off(u)];
-      tsc_cur[u] = tsc_lane[tab_off(u)];
-      tix_cur[u] = tix_lane[tab_off(PD + u)];
-    }
-  }
-  NT_STAMP(0, 1);
-  if (stopped0) return;
-  if (a.mrep > 0) {
-    // the previous generation's stop test, as nest_walk_kernel (global log table: no staging)
-    const double live = st_lv + st_mx;
-    if (live - plse(st_est, live, kLogTab) <= a.log_epsrel || st_err) {
-      if (blockIdx.x == 0 && threadIdx.x == 0) {
-        __hip_atomic_store(&a.st->stop_gen, (long long)(a.mrep / a.k) - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        nest_set(&a.st->stopped);
-      }
-      return;
-    }
-  }
-  if (!walker) {
-    // waves 4-7: retire this workgroup's 16 walkers' points, then the next generation's table
-    if (a.fuse_retire) {
-      const int64_t w0 = (int64_t)blockIdx.x * 16;
-      for (int64_t e = threadIdx.x - 256; e < 16 * D; e += 256) {
-        const int64_t wj = w0 + e / D;
-        const int d = (int)(e % D);
-        if (wj >= a.k) break;
-        const int rs = a.key_slot[wj];
-        const int64_t m = a.mrep + wj;
-        a.dead_x[m * D + d] = a.x[(int64_t)rs * D + d];
-        if (d == 0) {
-          const double lls = a.ll[rs];
-          a.dead_ll[m] = lls;
-          a.dead_lp[m] = a.lp[rs];
-          const double lv = a.st->log_vol + a.prefix[wj];
-          __hip_atomic_store(a.tv + wj, lls + (lv + a.qadd[wj]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          a.rank[wj] = 0;
-        }
-      }
-    }
-    walk_draws_fill(a, a.mrep + a.k, (int64_t)blockIdx.x * 256 + (threadIdx.x - 256), (int64_t)gridDim.x * 256, kLogTab);
-    return;
-  }
-  __builtin_amdgcn_s_setprio(3);
-  const bool first_ok = ll_first >= thr;
-  int64_t start = first_ok ? (int64_t)s_first : -1;
-  if (!first_ok) {
-    for (uint32_t att = 1; att < 4096; ++att) {
-      const u32x4 r = rng(wid, att, CALL_START, TAG_NEST_WALK, 0u);
-      const uint32_t sx = randint(r.x, r.y, n);
-      if (a.ll[sx] >= thr) {
-        start = sx;
-        break;
-      }
-    }
-  }
-  if (start < 0) start = a.key_slot[a.k - 1];
-  NT_STAMP(0, 2);
-  const char* const xb = (const char*)a.x;
-  const uint32_t lane_b = 8u * W * (uint32_t)sub;
-  auto refill = [&](double* dst, uint32_t v) {
-    const char* src = xb + (v + lane_b);
-#pragma unroll
-    for (int i = 0; i < Lay::NCL; ++i)
-#pragma unroll
-      for (int q = 0; q < W; ++q) dst[W * i + q] = *(const double*)(src + 8 * (W * P * i + q));
-  };
-  tgt.setup_constraint(thr);
-  double cur[NL];
-  double cur_l;
-  if (first_ok) {
-#pragma unroll
-    for (int d = 0; d < NL; ++d) cur[d] = row_first[d];
-    cur_l = lp_first;
-  } else {
-    const double* __restrict__ src = a.x + start * D;
-#pragma unroll
-    for (int i = 0; i < Lay::NCL; ++i)
-#pragma unroll
-      for (int q = 0; q < W; ++q) cur[W * i + q] = src[Lay::dim(sub, i, q)];
-    cur_l = (a.ll[start] >= thr) ? a.lp[start] : -__builtin_inf();
-  }
-  unsigned long long tix_next[PD];
-  double2 tsc_next[PD];
-  double bi[PD][NL], bj[PD][NL];
-#pragma unroll
-  for (int u = 0; u < PD; ++u) {
-    refill(bi[u], (uint32_t)tix_ring[u]);
-    refill(bj[u], (uint32_t)(tix_ring[u] >> 32));
-  }
-  const double lpb = tgt.lp_box();
-  const int nm = (int)a.nmcmc;
-  NT_STAMP(0, 3);
-  for (int s0 = 0; s0 < nm; s0 += PD) {
-    double dsc_g[PD], lu_g[PD];
-    uint32_t ip_g[PD], jp_g[PD];
-#pragma unroll
-    for (int u = 0; u < PD; ++u) {
-      dsc_g[u] = tsc_cur[u].x;
-      lu_g[u] = tsc_cur[u].y;
-      ip_g[u] = (uint32_t)tix_cur[u];
-      jp_g[u] = (uint32_t)(tix_cur[u] >> 32);
-    }
-#pragma unroll
-    for (int u = 0; u < PD; ++u) {
-      tsc_next[u] = tsc_lane[tab_off(s0 + PD + u)];
-      tix_next[u] = tix_lane[tab_off(s0 + 2 * PD + u)];
-    }
-#pragma unroll
-    for (int u = 0; u < PD; u += 2) {
-      const bool live0 = s0 + u < nm, live1 = s0 + u + 1 < nm;
-      double y0[NL], ya[NL], yr[NL], yc[NL];
-#pragma unroll
-      for (int d = 0; d < NL; ++d) {
-        const double du = dsc_g[u] * (bj[u][d] - bi[u][d]);
-        const double dv = dsc_g[u + 1] * (bj[u + 1][d] - bi[u + 1][d]);
-        y0[d] = cur[d] + du;                          // step u from the current point
-        ya[d] = y0[d] + dv;                           // step u + 1 after an accept
-        yr[d] = cur[d] + dv;                          // step u + 1 after a reject
-        yc[d] = role == 1 ? ya[d] : role == 2 ? yr[d] : y0[d];
-      }
-      refill(bi[u], ip_g[u]);
-      refill(bj[u], jp_g[u]);
-      refill(bi[u + 1], ip_g[u + 1]);
-      refill(bj[u + 1], jp_g[u + 1]);
-      // mcmc.ml:47-48 as in nest_walk_kernel: ml is lp_box when the proposal passes, -inf when
-      // it fails; after an accept cur_l is lp_box, so step u + 1's test is lu < lp_box - lp_box
-      const bool pre0 = live0 && lu_g[u] < lpb - cur_l;
-      const bool pre1r = live1 && lu_g[u + 1] < lpb - cur_l;
-      const bool pre1a = live1 && lu_g[u + 1] < lpb - lpb;
-      const bool ok = tgt.constraint_box(yc, sub, thr);
-      const unsigned long long bm = __ballot(ok);
-      const bool okA = (bm >> (rowb + sub)) & 1ull;
-      const bool okB = (bm >> (rowb + 4 + sub)) & 1ull;
-      const bool okC = (bm >> (rowb + 8 + sub)) & 1ull;
-      const bool acc0 = okA && pre0;
-      const bool acc1 = acc0 ? (okB && pre1a) : (okC && pre1r);
-#pragma unroll
-      for (int d = 0; d < NL; ++d) {
-        const double c1 = acc0 ? y0[d] : cur[d];
-        cur[d] = acc1 ? (acc0 ? ya[d] : yr[d]) : c1;
-      }
-      cur_l = (acc0 || acc1) ? lpb : cur_l;
-    }
-#pragma unroll
-    for (int u = 0; u < PD; ++u) {
-      tsc_cur[u] = tsc_next[u];
-      tix_cur[u] = tix_next[u];
-    }
-  }
-  NT_STAMP(0, 4);
-  const double nl = tgt.lik(cur, sub, a.m);
-  const double np = tgt.prior(cur, sub, a.m);
-  if (!active || role != 0) return;
-#pragma unroll
-  for (int i = 0; i < Lay::NCL; ++i)
-#pragma unroll
-    for (int q = 0; q < W; ++q) a.nx[w * D + Lay::dim(sub, i, q)] = cur[W * i + q];
+      if (Lay::valid(sub, i, q)) a.nx[w * D + Lay::dim(sub, i, q)] = cur[W * i + q];
   if (sub == 0) {
     a.nll[w] = nl;
     a.nlp[w] = np;
-    if (a.fuse_retire) {
+    if (a.fuse_retire) {                               // the new point's key
       a.newk_ll[w] = nl;
       a.newk_tie[w] = -(long long)(a.mrep + w + 1);
       a.newk_slot[w] = ret_slot;
     }
-    if (!(nl >= thr)) nest_set(&a.st->error);
+    if (!(nl >= thr)) nest_set(&a.st->error);        // nested.ml:70-72 -> Failure
   }
 }
 
@@ -1177,14 +862,6 @@ __global__ void __launch_bounds__(256) nest_init_kernel(const NestArgs a, double
   keys_slot[s] = (int)s;
 }
 
-// the pair walker applies to box-folded 4-dim-block register targets on 4 lanes (the layout is
-// checked before WalkTarget is instantiated: it static_asserts on invalid splits)
-template <int D, int LIK, int P>
-constexpr bool pair_walk_ok() {
-  if constexpr (P == 4 && D % 16 == 0 && LIK == MCG_LIK_GAUSS_SHELL) return WalkTarget<D, 4, LIK, true>::kFold;
-  else return false;
-}
-
 template <int D, int LIK, int P>
 hipError_t launch_nest_walk_p(const NestArgs& a, hipStream_t st) {
   // small workgroups: a generation has only k * P lanes, so one wave per workgroup spreads them
@@ -1194,12 +871,6 @@ hipError_t launch_nest_walk_p(const NestArgs& a, hipStream_t st) {
   // with the draw table: the same walker waves, each with three table-filling waves beside it
   const dim3 gt((unsigned)((a.k * P + 63) / 64)), bt(256);
   constexpr bool kSym = WalkTarget<D, P, LIK>::kReg;   // the |y| <= h form needs the register target
-  if constexpr (pair_walk_ok<D, LIK, P>()) {
-    if (a.rt_ix && a.sym_box && a.walk_pair) {
-      hipLaunchKernelGGL((nest_walk_pair_kernel<D, LIK, true>), dim3((unsigned)((a.k + 15) / 16)), dim3(512), 0, st, a);
-      return hipGetLastError();
-    }
-  }
   if (a.rt_ix && kSym && a.sym_box) hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, kSym>), gt, bt, 0, st, a);
   else if (a.rt_ix) hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, false>), gt, bt, 0, st, a);
   else hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, false, false>), dim3((unsigned)grid), dim3(block), 0, st, a);
@@ -1254,10 +925,6 @@ hipError_t launch_key_sample(const double* ll, const long long* tie, int64_t n, 
 // k <= 4096: the generation's unsorted new keys merged into the survivors in one launch (plus the
 // estimate and the slot writes): keys -> o*
 hipError_t launch_merge_fused(const NestArgs& a, double* oll, long long* otie, int* oslot, hipStream_t s);
-// pipelined merges: the k lowest of survivors[0, ns) (ns <= k) and the k sorted new keys into h*
-hipError_t launch_head_merge(const NestArgs& a, const double* sl, const long long* st, const int* ss, int64_t ns,
-                             const double* nl, const long long* nt, const int* nsl, double* hl, long long* ht,
-                             int* hs, hipStream_t s);
 // k <= 4096: new keys sorted into o* by counting ranks (a.rank zeroed by the retire kernel)
 hipError_t launch_sort_new_small(const NestArgs& a, double* oll, long long* otie, int* oslot,
                                  hipStream_t st);

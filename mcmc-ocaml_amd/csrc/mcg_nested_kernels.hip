@@ -356,9 +356,6 @@ __global__ void __launch_bounds__(256) rank_count_kernel(const NestArgs a, int n
       oslot[r] = sl_[e];
     }
   }
-  // pipelined merges: the next walk's L_max is the largest live ll = max(the survivors' largest,
-  // which is the previous L_max, and the largest new key) -- the merged keys' last entry
-  if (a.pipe && t == 0) a.st->max_ll = fmax(a.st->max_ll, s_ll[k - 1]);
   NT_STAMP(2, 5);
   slot_writes();
 }
@@ -487,12 +484,7 @@ __global__ void __launch_bounds__(256) merge_new_kernel(const NestArgs a, double
     kv_use = ku;
   }
   __syncthreads();
-  // pipelined (a.pipe): this merge runs beside the next generation's walk, which may find the
-  // run finished and set the stop flag; the merge of the last generation must still complete,
-  // so it tests the generation against st->stop_gen instead
-  if (a.pipe ? (a.mrep / a.k > __hip_atomic_load(&a.st->stop_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-             : nest_stopped(a.st))
-    return;
+  if (nest_stopped(a.st)) return;
   NT_STAMP(3, 1);
   if (e >= n) return;
   int64_t pos;
@@ -507,7 +499,7 @@ __global__ void __launch_bounds__(256) merge_new_kernel(const NestArgs a, double
     a.out_samp_tie[pos / kKeySample] = kt;
   }
   if (pos == n - 1) {
-    if (!a.pipe) a.st->max_ll = kl;                  // (pipelined: the rank count keeps it)
+    a.st->max_ll = kl;
     __hip_atomic_fetch_add(&a.st->gen_done, 1LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   NT_STAMP(3, 3);
@@ -601,20 +593,20 @@ __global__ void __launch_bounds__(BS) merge_fused_kernel(const NestArgs a, doubl
     nv[r] = a.newk_ll[j < k ? j : k - 1];
   }
   if (g0 < kD) {
-    wt_store<MCG_MERGE_WT>(&a.x[(int64_t)sj0 * D + d0], cx0);
+    wt_store(&a.x[(int64_t)sj0 * D + d0], cx0);
     if (d0 == 0) {
-      wt_store<MCG_MERGE_WT>(&a.ll[sj0], cl0);
-      wt_store<MCG_MERGE_WT>(&a.lp[sj0], cp0);
+      wt_store(&a.ll[sj0], cl0);
+      wt_store(&a.lp[sj0], cp0);
     }
   }
   for (int64_t g = g0 + gstride; g < kD; g += gstride) {   // k * D beyond one element a thread
     const int64_t j = g / D;
     const int64_t d = g - j * D;
     const int sj = a.newk_slot[j];
-    wt_store<MCG_MERGE_WT>(&a.x[(int64_t)sj * D + d], a.nx[g]);
+    wt_store(&a.x[(int64_t)sj * D + d], a.nx[g]);
     if (d == 0) {
-      wt_store<MCG_MERGE_WT>(&a.ll[sj], a.nll[j]);
-      wt_store<MCG_MERGE_WT>(&a.lp[sj], a.nlp[j]);
+      wt_store(&a.ll[sj], a.nll[j]);
+      wt_store(&a.lp[sj], a.nlp[j]);
     }
   }
   // the new ll stay in registers: classified as they land, and only the block's subset goes to
@@ -688,15 +680,15 @@ __global__ void __launch_bounds__(BS) merge_fused_kernel(const NestArgs a, doubl
       else hi = md;
     }
     const int64_t pos = i0 + lo + c_lo + lr;
-    wt_store<MCG_MERGE_WT>(&oll[pos], x);
-    wt_store<MCG_MERGE_WT>(&otie[pos], xt);
-    wt_store<MCG_MERGE_WT>(&oslot[pos], a.newk_slot[j]);
+    wt_store(&oll[pos], x);
+    wt_store(&otie[pos], xt);
+    wt_store(&oslot[pos], a.newk_slot[j]);
     if (pos % kKeySample == kKeySample - 1) {
       a.out_samp_ll[pos / kKeySample] = x;
       a.out_samp_tie[pos / kKeySample] = xt;
     }
     if (pos == n - 1) {
-      if (!a.pipe) a.st->max_ll = x;
+      a.st->max_ll = x;
       __hip_atomic_fetch_add(&a.st->gen_done, 1LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -711,15 +703,15 @@ __global__ void __launch_bounds__(BS) merge_fused_kernel(const NestArgs a, doubl
       else hi = md;
     }
     const int64_t pos = i0 + t + c_lo + lo;
-    wt_store<MCG_MERGE_WT>(&oll[pos], kl);
-    wt_store<MCG_MERGE_WT>(&otie[pos], kt);
-    wt_store<MCG_MERGE_WT>(&oslot[pos], ks);
+    wt_store(&oll[pos], kl);
+    wt_store(&otie[pos], kt);
+    wt_store(&oslot[pos], ks);
     if (pos % kKeySample == kKeySample - 1) {
       a.out_samp_ll[pos / kKeySample] = kl;
       a.out_samp_tie[pos / kKeySample] = kt;
     }
     if (pos == n - 1) {
-      if (!a.pipe) a.st->max_ll = kl;
+      a.st->max_ll = kl;
       __hip_atomic_fetch_add(&a.st->gen_done, 1LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -759,81 +751,6 @@ hipError_t launch_key_sample(const double* ll, const long long* tie, int64_t n, 
                              long long* stie, hipStream_t s, NestDevState* st) {
   const int64_t ns = n / kKeySample;
   hipLaunchKernelGGL(key_sample_kernel, dim3((unsigned)(ns / 256 + 1)), dim3(256), 0, s, ll, tie, n, sll, stie, st);
-  return hipGetLastError();
-}
-
-// Pipelined merges: generation g + 1 needs only the k lowest live keys (its
-// threshold, its retirees and their order), which are the k lowest of survivors[k, 2k) of the
-// previous full key array and the k sorted new keys.  Workgroup b takes 256 keys of one of the two
-// arrays, stages the other whole array (<= 4096 keys, 64 KB) in LDS and places each key at
-// own index + (keys of the other array below it), when that is below k.  Keys are unique, so the
-// two counts never collide.
-__global__ void __launch_bounds__(256) head_merge_kernel(const NestArgs a, const double* sl_, const long long* st_,
-                                                         const int* ss_, int64_t ns, const double* nl,
-                                                         const long long* nt, const int* nsl, double* hl,
-                                                         long long* ht, int* hs) {
-  __shared__ double o_l[kSmallSort];
-  __shared__ long long o_t[kSmallSort];
-  if (nest_stopped(a.st)) return;
-  const int64_t k = a.k;
-  const int nbs = (int)((ns + 255) / 256);
-  const bool from_surv = (int)blockIdx.x < nbs;       // block-uniform
-  const int64_t i = (int64_t)(from_surv ? blockIdx.x : blockIdx.x - nbs) * 256 + threadIdx.x;
-  const int64_t len_own = from_surv ? ns : k, len_oth = from_surv ? k : ns;
-  const double* ol = from_surv ? nl : sl_;
-  const long long* ot = from_surv ? nt : st_;
-  {
-    // every staging load in flight together (a loop of unknown trip count issued them one
-    // memory round trip at a time), then the LDS stores
-    constexpr int kPer = kSmallSort / 256;
-    double vl[kPer];
-    long long vt[kPer];
-#pragma unroll
-    for (int r = 0; r < kPer; ++r) {
-      const int64_t q = (int64_t)r * 256 + threadIdx.x;
-      const int64_t qc = q < len_oth ? q : len_oth - 1;
-      vl[r] = ol[qc];
-      vt[r] = ot[qc];
-    }
-#pragma unroll
-    for (int r = 0; r < kPer; ++r) {
-      const int64_t q = (int64_t)r * 256 + threadIdx.x;
-      if (q < len_oth) {
-        o_l[q] = vl[r];
-        o_t[q] = vt[r];
-      }
-    }
-  }
-  double kl = 0.0;
-  long long kt = 0;
-  int ks = 0;
-  if (i < len_own) {
-    kl = from_surv ? sl_[i] : nl[i];
-    kt = from_surv ? st_[i] : nt[i];
-    ks = from_surv ? ss_[i] : nsl[i];
-  }
-  __syncthreads();
-  if (i >= len_own) return;
-  int lo = 0, hi = (int)len_oth;
-  while (lo < hi) {
-    const int m = (lo + hi) >> 1;
-    if (key_less(o_l[m], o_t[m], kl, kt)) lo = m + 1;
-    else hi = m;
-  }
-  const int64_t pos = i + lo;
-  if (pos < k) {
-    hl[pos] = kl;
-    ht[pos] = kt;
-    hs[pos] = ks;
-  }
-}
-
-hipError_t launch_head_merge(const NestArgs& a, const double* sl, const long long* st, const int* ss, int64_t ns,
-                             const double* nl, const long long* nt, const int* nsl, double* hl, long long* ht,
-                             int* hs, hipStream_t s) {
-  if (a.k > kSmallSort || a.k < 1 || ns > kSmallSort) return hipErrorInvalidValue;
-  const unsigned grid = (unsigned)((ns + 255) / 256 + (a.k + 255) / 256);
-  hipLaunchKernelGGL(head_merge_kernel, dim3(grid), dim3(256), 0, s, a, sl, st, ss, ns, nl, nt, nsl, hl, ht, hs);
   return hipGetLastError();
 }
 

@@ -989,6 +989,24 @@ int mcg_tile_stats_device(mcg_ctx* ctx, void** dev_ptr, int64_t* ntiles) {
   return MCG_OK;
 }
 
+int mcg_tile_stats_into(mcg_ctx* ctx, double* dev_tiles) {
+  if (!ctx || !dev_tiles) return MCG_EINVAL;
+  if (ctx->nrec_total < 1) return set_error(ctx, MCG_ESTATE, "no accumulated records");
+  (void)hipSetDevice(ctx->opts.device);
+  TileArgs t{};
+  t.mean = (const double*)ctx->d_mean.p;
+  t.m2 = (const double*)ctx->d_m2.p;
+  t.hm_m = (const double*)ctx->d_hm_m.p;
+  t.hm_s = (const double*)ctx->d_hm_s.p;
+  t.tiles = dev_tiles;
+  t.N = ctx->N;
+  t.nrec = ctx->nrec_total;
+  t.D = ctx->D;
+  int rc;
+  if ((rc = hip_check(ctx, launch_tile_stats(t, ctx->stream), "tile launch"))) return rc;
+  return hip_check(ctx, hipStreamSynchronize(ctx->stream), "tile sync");
+}
+
 int mcg_tile_stats(mcg_ctx* ctx, double* tiles) {
   if (!ctx || !tiles) return MCG_EINVAL;
   int64_t nt = 0;

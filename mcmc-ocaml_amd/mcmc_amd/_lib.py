@@ -87,6 +87,7 @@ SIGNATURES = {
     "mcg_num_tiles": ([C.c_void_p], C.c_int64),
     "mcg_tile_stats": ([C.c_void_p, _dp], C.c_int),
     "mcg_tile_stats_device": ([C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)], C.c_int),
+    "mcg_tile_stats_into": ([C.c_void_p, C.c_void_p], C.c_int),
     "mcg_combine_tiles": ([C.c_int32, C.c_int64, _dp, _dp, _dp, _dp], C.c_int),
     "mcg_stats": ([C.c_void_p, _dp, _dp, _dp], C.c_int),
     "mcg_nested": ([C.c_void_p, C.POINTER(McgNestedOpts), C.POINTER(McgNestedResult), OBSERVER,

@@ -139,6 +139,14 @@ class Context:
         self._check(L.lib().mcg_tile_stats_device(self._p, C.byref(p), C.byref(nt)))
         return p.value, nt.value
 
+    def num_tiles(self):
+        return int(L.lib().mcg_num_tiles(self._p))
+
+    def tile_stats_into(self, dev_ptr):
+        """Tile partials written into a caller-owned device buffer (an int device address of
+        num_tiles() x (2D+3) doubles on this context's device), complete on return."""
+        self._check(L.lib().mcg_tile_stats_into(self._p, C.c_void_p(int(dev_ptr))))
+
     def stats(self):
         D = self.ndim
         mean = np.zeros(D); sd = np.zeros(D); lz = np.zeros(1)

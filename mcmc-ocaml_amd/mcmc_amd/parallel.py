@@ -26,7 +26,7 @@ def allgather_tiles(tiles, device=None, group=None):
     """All-gather every rank's tile partials (same tile count per rank), in rank order."""
     import torch
     import torch.distributed as dist
-    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if not dist.is_available() or not dist.is_initialized():
         return np.asarray(tiles)
     t = torch.from_numpy(np.ascontiguousarray(tiles, dtype=np.float64))
     if device is not None:
@@ -39,6 +39,33 @@ def allgather_tiles(tiles, device=None, group=None):
 def reduce_stats(ndim, tiles, device=None, group=None):
     """Global Stats.multi_mean / multi_std and log Z_HM from this rank's tile partials."""
     return combine_tiles(ndim, allgather_tiles(tiles, device, group))
+
+
+def allgather_tiles_device(ctx, device, group=None):
+    """The device path of the end-of-run exchange (RCCL over xGMI): the tile kernel writes this
+    rank's partials straight into a torch device buffer (mcg_tile_stats_into), which is the send
+    buffer of one all_gather_into_tensor; only the gathered tiles come back to the host for the
+    combine.  The collective runs whenever a process group is up -- a one-rank group too, so the
+    RCCL leg is exercised on one GPU -- and is skipped only without torch.distributed."""
+    import torch
+    import torch.distributed as dist
+    nt, w = ctx.num_tiles(), 2 * ctx.ndim + 3
+    send = torch.empty((nt, w), dtype=torch.float64, device=device)
+    # the buffer comes from torch's caching allocator: let torch's own stream finish with the
+    # memory before the context's stream writes it
+    torch.cuda.synchronize(device)
+    ctx.tile_stats_into(send.data_ptr())
+    if not dist.is_available() or not dist.is_initialized():
+        return send.cpu().numpy()
+    recv = torch.empty((dist.get_world_size(group) * nt, w), dtype=torch.float64, device=device)
+    dist.all_gather_into_tensor(recv, send, group=group)
+    return recv.cpu().numpy()
+
+
+def reduce_stats_device(ctx, device, group=None):
+    """reduce_stats over the device path (allgather_tiles_device): the same bits as the host
+    path, every rank folding the gathered tiles in global order."""
+    return combine_tiles(ctx.ndim, allgather_tiles_device(ctx, device, group))
 
 
 def replica_seed(seed, rank):
@@ -58,11 +85,11 @@ def allgather_runs(output, nlive, k, device=None, group=None, points=True):
     """All-gather every rank's nested run: the point counts first, then the (pts | ll | lp) rows
     padded to the longest run (points=False: ll | lp only, enough for log Z).  Returns
     [(output, nlive, k)] in rank order."""
-    rank, world = _world(group)
-    if world == 1:
+    import torch.distributed as dist
+    if not dist.is_available() or not dist.is_initialized():
         return [(output, nlive, k)]
     import torch
-    import torch.distributed as dist
+    rank, world = _world(group)
     pts = np.asarray(output[2], np.float64) if points else np.zeros((len(output.ll), 0))
     D = pts.shape[1]
     rows = np.concatenate([pts, output.ll[:, None], output.lp[:, None]], axis=1)

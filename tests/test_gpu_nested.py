@@ -276,16 +276,13 @@ def test_nested_walker_box_skip_near_the_box_bit_exact(oracle, T, sym):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", ["MCG_NESTED_NO_TABLE", "MCG_NESTED_RETIRE_KERNEL", "both", "MCG_NESTED_PIPE",
-                                 "MCG_NESTED_MERGE2", "MCG_NESTED_PAIR"])
+@pytest.mark.parametrize("env", ["MCG_NESTED_NO_TABLE", "MCG_NESTED_RETIRE_KERNEL", "both", "MCG_NESTED_MERGE2"])
 @pytest.mark.parametrize("D", [3, 16])
 def test_nested_alternate_paths_bit_exact(oracle, T, monkeypatch, env, D):
     """The paths the default run does not take: walkers drawing their own random numbers (no
     draw table: what a generation too big for the table uses), the separate retire kernel
-    (k > 4096 uses it), the pipelined head + full merges, the two-launch counted-rank sort +
-    merge instead of the one-launch fused merge, and the walker with its steps resolved in pairs
-    across lane quads (D = 16: nest_walk_pair_kernel) -- the same dead points as the oracle, bit
-    for bit."""
+    (k > 4096 uses it) and the two-launch counted-rank sort + merge instead of the one-launch
+    fused merge -- the same dead points as the oracle, bit for bit."""
     for var in (["MCG_NESTED_NO_TABLE", "MCG_NESTED_RETIRE_KERNEL"] if env == "both" else [env]):
         monkeypatch.setenv(var, "1")
     lik = T.gauss_shell(np.zeros(D), 1.0, 0.2)
@@ -296,13 +293,11 @@ def test_nested_alternate_paths_bit_exact(oracle, T, monkeypatch, env, D):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nlive,k", [(300, 200), (257, 256), (5000, 4096)])
-def test_nested_pipelined_head_merge_edges_bit_exact(oracle, T, monkeypatch, nlive, k):
-    """Pipelined merges (MCG_NESTED_PIPE) where the head merge sees fewer
-    survivors than new keys (k > nlive / 2), a single survivor (k = nlive - 1), and the largest
-    counted-rank k, run to convergence: dead points, stop generation, log Z and weights equal the
-    oracle's."""
-    monkeypatch.setenv("MCG_NESTED_PIPE", "1")
+@pytest.mark.parametrize("nlive,k", [(300, 200), (257, 256)])
+def test_nested_large_fraction_generations_bit_exact(oracle, T, nlive, k):
+    """Generations retiring most of the live set (k > nlive / 2) and all but one point
+    (k = nlive - 1), run to convergence: dead points, stop generation, log Z and weights equal
+    the oracle's."""
     D = 4
     lik = T.gauss_shell(np.zeros(D), 1.0, 0.2)
     pri = T.box(-2 * np.ones(D), 2 * np.ones(D))
