@@ -132,12 +132,29 @@ class Failure(McgError):
 _lib = None
 
 
+def _one_hip_runtime():
+    """Keep ONE HIP runtime in the process.  The ROCm torch wheel bundles its own libamdhip64.so
+    (SONAME libamdhip64.so.7) and HSA runtime; libmcg.so needs libamdhip64.so.7.  With torch
+    loaded first the dynamic loader serves libmcg's dependency from torch's copy (same SONAME), so
+    torch's collectives (RCCL) and libmcg share one runtime and one device address space.  With
+    libmcg loaded first it maps /opt/rocm's runtime, and a later `import torch` (its libraries name
+    the unversioned libamdhip64.so) maps a second HIP + HSA runtime, which then finds no GPU.  So
+    torch, when installed, is imported before libmcg.so is loaded (MCG_NO_TORCH_PRELOAD=1 skips)."""
+    if os.environ.get("MCG_NO_TORCH_PRELOAD"):
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def lib():
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError("libmcg.so not built (%s): run `python -c 'import __graft_entry__ as g; "
                                "g.build()'` -- there is no CPU fallback" % LIB_PATH)
+        _one_hip_runtime()
         L = C.CDLL(LIB_PATH)
         for name, (args, res) in SIGNATURES.items():
             fn = getattr(L, name)

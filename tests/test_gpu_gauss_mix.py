@@ -56,7 +56,9 @@ def test_gauss_mix_mh_bit_exact(oracle, T, case):
     if case == "one":
         d = run_gpu(T.diag_gauss(lik.params[1:1 + D], lik.params[1 + D:]), pri, T.gauss(s), x0, 17,
                     nbin=10, nskip=2, n_rec=60)
-        assert_same(g, d)
+        for key in ("ll0", "bits", "rec_x", "rec_ll", "x", "ll", "tiles"):
+            np.testing.assert_array_equal(g[key], d[key])
+        assert g["nacc"] == d["nacc"]
 
 
 def test_gauss_mix_de_proposal_bit_exact(oracle, T):
