@@ -18,19 +18,58 @@
 
 namespace mcg {
 
-template <int D, int P>
+// Lane layout of a chain on P lanes: lane `sub` owns the W-dim blocks c = sub, sub + P, ... (dims
+// W c .. W c + W - 1).  W = 4: the blocks are the Philox calls of the Gaussian proposal's normals
+// (dims 4c .. 4c+3 from call c).  W = 2 (D = 2P, the kD independence proposal only): a lane owns
+// two dims, whose box-draw uniforms are exactly one Philox call (dims 2c, 2c + 1 from call c), and
+// the two lanes of a canonical accumulator chain their fmas in dim order (reduce_canon_w2).
+template <int D, int P, int W = 4>
 struct Layout {
   static_assert(P == 1 || P == 2 || P == 4 || P == 8, "P must divide 8");
-  static constexpr int NC = (D + 3) / 4;                 // Philox calls per step
-  static constexpr int NCL = (NC + P - 1) / P;           // calls owned by one lane
-  static constexpr int NL = NCL * 4;                     // local dims
-  static constexpr int NA = 8 / P;                       // local accumulators
-  static_assert(P == 1 || D % (4 * P) == 0, "P > 1 needs D % 4P == 0");
-  __device__ static __forceinline__ int dim(int sub, int i, int q) { return 4 * (sub + P * i) + q; }
+  static_assert(W == 4 || (W == 2 && P >= 2 && D == 2 * P), "W = 2: two dims per lane, D = 2P");
+  static constexpr int NC = (D + W - 1) / W;             // blocks per chain
+  static constexpr int NCL = (NC + P - 1) / P;           // blocks owned by one lane
+  static constexpr int NL = NCL * W;                     // local dims
+  static constexpr int NA = W == 2 ? 1 : 8 / P;          // local accumulators
+  static_assert(P == 1 || D % (W * P) == 0, "P > 1 needs D % WP == 0");
+  __device__ static __forceinline__ int dim(int sub, int i, int q) { return W * (sub + P * i) + q; }
   __device__ static __forceinline__ bool valid(int sub, int i, int q) {
-    return P > 1 || (4 * i + q) < D;
+    return q < W && (P > 1 || (W * i + q) < D);
   }
 };
+
+// the width of a chain's lane blocks: two dims per lane where the kD proposal runs on D = 2P lanes
+template <int D, int P, int PROP>
+constexpr int lane_width() {
+  return (PROP == MCG_PROP_KD_INTERP && P >= 2 && D == 2 * P) ? 2 : 4;
+}
+
+// The canonical sum for W = 2 (D = 2P): lane sub holds the terms of dims 2 sub, 2 sub + 1, which
+// belong to accumulator A_j, j = sub / 2.  The even lane of the pair folds dims 4j, 4j + 1 from
+// zero, the odd lane continues from that partial with dims 4j + 2, 4j + 3 (the sequential fma
+// chain of A_j), and the odd lanes (A_0 .. A_{P/2-1}) meet in the canonical tree
+// ((A0 + A4) + (A2 + A6)) + ((A1 + A5) + (A3 + A7)), whose A_{P/2} .. A_7 are zero here (x + 0 = x
+// for the sums of squares): (A0 + A2) + (A1 + A3) at P = 8, A0 + A1 at P = 4, A0 at P = 2.  Even
+// lanes take their odd neighbour's value.  Additions are commutative, so every lane of the tree
+// holds the same bits.
+template <int P>
+__device__ __forceinline__ double reduce_canon_w2(double e0, double e1, int sub) {
+  static_assert(P == 2 || P == 4 || P == 8, "W = 2 chains run on 2, 4 or 8 lanes");
+  const double t = fma(e1, e1, fma(e0, e0, 0.0));
+  const double tp = xor_lane_d<1>(t);
+  const double a = fma(e1, e1, fma(e0, e0, tp));
+  double c;
+  if constexpr (P == 8) {
+    const double b = a + xor_lane_d<4>(a);
+    c = b + xor_lane_d<2>(b);
+  } else if constexpr (P == 4) {
+    c = a + xor_lane_d<2>(a);
+  } else {
+    c = a;
+  }
+  const double o = xor_lane_d<1>(c);
+  return (sub & 1) ? c : o;
+}
 
 // reduce the lane-local accumulators of the canonical tree across the P lanes of a chain
 template <int P>
@@ -198,11 +237,27 @@ __device__ __forceinline__ bool mix_has_kd(const double* __restrict__ q, int str
 // Q: a generic pointer, or (the MH kernel's per-step evaluation) a constant-address-space one,
 // whose uniform loads become scalar loads (the scalar cache and lgkmcnt, not vmcnt: a per-step
 // vector load of the constants waited with vmcnt(0) and drained every load issued ahead)
-template <int D, int P, int LIK, typename Q = const double* __restrict__>
+template <int D, int P, int LIK, typename Q = const double* __restrict__, int W = 4>
 __device__ __forceinline__ double eval_lik(const double* y, int sub, const MhArgs& a, Q q) {
-  using L = Layout<D, P>;
+  using L = Layout<D, P, W>;
   if constexpr (LIK == MCG_LIK_FLAT) {
     return 0.0;
+  } else if constexpr ((LIK == MCG_LIK_DIAG_GAUSS || LIK == MCG_LIK_GAUSS_SHELL) && W == 2) {
+    // two dims per lane (dims 2 sub, 2 sub + 1): the pair-chained canonical accumulator
+    double e[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int d = L::dim(sub, 0, k);
+      e[k] = LIK == MCG_LIK_DIAG_GAUSS ? fma(y[k], q[D + d], -q[d]) : y[k] - q[d];
+    }
+    const double S = reduce_canon_w2<P>(e[0], e[1], sub);
+    if constexpr (LIK == MCG_LIK_DIAG_GAUSS) {
+      return q[2 * D] - 0.5 * S;
+    } else {
+      const double r = psqrt(S);
+      const double qq = (r - q[D]) * q[D + 1];
+      return q[D + 2] - 0.5 * qq * qq;
+    }
   } else if constexpr (LIK == MCG_LIK_DIAG_GAUSS || LIK == MCG_LIK_GAUSS_SHELL) {
     // DIAG: q = mu/sigma[D], 1/sigma[D], C        SHELL: q = c[D], R, iw, C
     double A[L::NA];
@@ -228,7 +283,7 @@ __device__ __forceinline__ double eval_lik(const double* y, int sub, const MhArg
       return q[D + 2] - 0.5 * qq * qq;
     }
   } else if constexpr (LIK == MCG_LIK_FULLCOV_GAUSS) {
-    static_assert(P == 1, "FULLCOV: one lane per chain");
+    static_assert(P == 1 && W == 4, "FULLCOV: one lane per chain");
     // q = mu[D], C, U[D*D]
     double r[D];
 #pragma unroll
@@ -247,6 +302,7 @@ __device__ __forceinline__ double eval_lik(const double* y, int sub, const MhArg
     }
     return q[D] - 0.5 * canon8(A);
   } else if constexpr (LIK == MCG_LIK_GAUSS_MIX) {
+    static_assert(W == 4, "GAUSS_MIX: four-dim lane blocks");
     // log (sum_i exp g_i) over a.data_n components (test/nested_test.ml:52-57), g_i the DIAG
     // canonical form of component i (q + i (2D + 1): mu/sigma[D], 1/sigma[D], C_i), folded by a
     // one-pass max-shifted log-sum-exp in component order: s = sum_i exp(g_i - M) with the
@@ -278,7 +334,7 @@ __device__ __forceinline__ double eval_lik(const double* y, int sub, const MhArg
     return M == -__builtin_inf() ? M : M + plog(s);
   } else {
     // GAUSS_DATA / CAUCHY_DATA (bin/gaussian_cauchy.ml:149-164), D = 2 nd, y = (mu, sigma)
-    static_assert(P == 1, "DATA: one lane per chain");
+    static_assert(P == 1 && W == 4, "DATA: one lane per chain");
     constexpr int ND = D / 2;
     const double PI = 3.14159265358979323846;
     double lterm[ND];
@@ -299,9 +355,9 @@ __device__ __forceinline__ double eval_lik(const double* y, int sub, const MhArg
   }
 }
 
-template <int D, int P, typename Q = const double* __restrict__>
+template <int D, int P, typename Q = const double* __restrict__, int W = 4>
 __device__ __forceinline__ double eval_prior(const double* y, int sub, const MhArgs& a, Q q) {
-  using L = Layout<D, P>;
+  using L = Layout<D, P, W>;
   if (a.prior_kind == MCG_PRIOR_FLAT) return 0.0;
   int inb = 1;
   if (a.ubox) {
@@ -311,9 +367,9 @@ __device__ __forceinline__ double eval_prior(const double* y, int sub, const MhA
 #pragma unroll
     for (int i = 0; i < L::NCL; ++i)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < W; ++k) {
         if (!L::valid(sub, i, k)) continue;
-        const double v = y[4 * i + k];
+        const double v = y[W * i + k];
         inb &= (int)(v >= a.box_lo) & (int)(v <= a.box_hi);
       }
   } else {
@@ -322,18 +378,18 @@ __device__ __forceinline__ double eval_prior(const double* y, int sub, const MhA
 #pragma unroll
     for (int i = 0; i < L::NCL; ++i)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < W; ++k) {
         const int d = L::valid(sub, i, k) ? L::dim(sub, i, k) : 0;
-        lo[4 * i + k] = q[d];
-        hi[4 * i + k] = q[D + d];
+        lo[W * i + k] = q[d];
+        hi[W * i + k] = q[D + d];
       }
 #pragma unroll
     for (int i = 0; i < L::NCL; ++i)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < W; ++k) {
         if (!L::valid(sub, i, k)) continue;
-        const double v = y[4 * i + k];
-        inb &= (int)(v >= lo[4 * i + k]) & (int)(v <= hi[4 * i + k]);   // closed form of the box (see above)
+        const double v = y[W * i + k];
+        inb &= (int)(v >= lo[W * i + k]) & (int)(v <= hi[W * i + k]);   // closed form of the box (see above)
       }
   }
   inb = and_lanes<P>(inb);
@@ -348,14 +404,14 @@ constexpr bool separable() {
          PROP == MCG_PROP_GAUSS;
 }
 
-template <int D, int P>
+template <int D, int P, int W = 4>
 struct AccumCfg {
   // Welford accumulators of the lane's NL dims: in VGPRs when NL <= 8, else in LDS ([NL][256]
   // doubles each, conflict-free) when they fit in 64 KiB per block, else read-modified-written in
   // HBM at each record.
-  static constexpr bool kReg = Layout<D, P>::NL <= 8;
-  static constexpr bool kLds = !kReg && Layout<D, P>::NL <= 16;
-  static constexpr int kLdsBytes = kLds ? 2 * Layout<D, P>::NL * 256 * 8 : 0;
+  static constexpr bool kReg = Layout<D, P, W>::NL <= 8;
+  static constexpr bool kLds = !kReg && Layout<D, P, W>::NL <= 16;
+  static constexpr int kLdsBytes = kLds ? 2 * Layout<D, P, W>::NL * 256 * 8 : 0;
 };
 
 // Waves per SIMD the kernel is built for.  The fused Gaussian step with at most 8 dims per lane
@@ -366,7 +422,7 @@ struct AccumCfg {
 // four normals of a Philox call gathered together (one LDS wait).
 template <int D, int P, int LIK, int PROP>
 struct MhShape {
-  static constexpr bool kThree = separable<LIK, PROP>() && Layout<D, P>::NL <= 8;
+  static constexpr bool kThree = separable<LIK, PROP>() && Layout<D, P, lane_width<D, P, PROP>()>::NL <= 8;
   static constexpr bool kPipe = kThree;
   static constexpr int kWaves = kThree ? 3 : 1;
   static constexpr int kBlock = 256;
@@ -383,9 +439,12 @@ struct MhShape {
 template <int D, int P, int LIK, int PROP, int UNI>
 __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D, P, LIK, PROP>::kWaves)) mh_kernel(const MhArgs a) {
   constexpr int kBlk = MhShape<D, P, LIK, PROP>::kBlock;
-  using L = Layout<D, P>;
+  constexpr int kW = lane_width<D, P, PROP>();
+  using L = Layout<D, P, kW>;
+  using ACfg = AccumCfg<D, P, kW>;
   constexpr bool kSeparable = separable<LIK, PROP>();
   static_assert(kSeparable || !UNI, "UNI applies to the fused separable step");
+  static_assert(!kSeparable || kW == 4, "the fused Gaussian step takes four-dim lane blocks");
   extern __shared__ double lds_acc[];
   __shared__ double2 s_lt[kLogTabN];                 // math tables staged in LDS (gathers)
   __shared__ double2 s_nt[kNrmTabN];
@@ -406,8 +465,8 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
 #pragma unroll
   for (int i = 0; i < L::NCL; ++i)
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      x[4 * i + k] = L::valid(sub, i, k) ? a.x[(int64_t)L::dim(sub, i, k) * N + c] : 0.0;
+    for (int k = 0; k < kW; ++k)
+      x[kW * i + k] = L::valid(sub, i, k) ? a.x[(int64_t)L::dim(sub, i, k) * N + c] : 0.0;
   double ll = a.ll[c], lp = a.lp[c];
   double lq = 0.0;
   if constexpr (PROP == MCG_PROP_KD_INTERP) {
@@ -449,24 +508,24 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
   double hm_pv = 0.0;
   bool hm_pok = false;
   // accumulator slot j of this lane: VGPR, LDS [j][threadIdx] or HBM [dim][chain]
-  constexpr int NR = AccumCfg<D, P>::kReg ? L::NL : 1;
+  constexpr int NR = ACfg::kReg ? L::NL : 1;
   double rmean[NR], rm2[NR];
   auto acc_mean = [&](int i, int k) -> double& {
-    if constexpr (AccumCfg<D, P>::kReg) return rmean[4 * i + k];
-    else if constexpr (AccumCfg<D, P>::kLds) return lds_acc[(4 * i + k) * 256 + threadIdx.x];
+    if constexpr (ACfg::kReg) return rmean[kW * i + k];
+    else if constexpr (ACfg::kLds) return lds_acc[(kW * i + k) * 256 + threadIdx.x];
     else return a.mean[(int64_t)L::dim(sub, i, k) * N + c];
   };
   auto acc_m2 = [&](int i, int k) -> double& {
-    if constexpr (AccumCfg<D, P>::kReg) return rm2[4 * i + k];
-    else if constexpr (AccumCfg<D, P>::kLds) return lds_acc[(L::NL + 4 * i + k) * 256 + threadIdx.x];
+    if constexpr (ACfg::kReg) return rm2[kW * i + k];
+    else if constexpr (ACfg::kLds) return lds_acc[(L::NL + kW * i + k) * 256 + threadIdx.x];
     else return a.m2[(int64_t)L::dim(sub, i, k) * N + c];
   };
   if (accum) {
-    if constexpr (AccumCfg<D, P>::kReg || AccumCfg<D, P>::kLds) {
+    if constexpr (ACfg::kReg || ACfg::kLds) {
 #pragma unroll
       for (int i = 0; i < L::NCL; ++i)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < kW; ++k) {
           int64_t o = (int64_t)L::dim(sub, i, k) * N + c;
           acc_mean(i, k) = L::valid(sub, i, k) ? a.mean[o] : 0.0;
           acc_m2(i, k) = L::valid(sub, i, k) ? a.m2[o] : 0.0;
@@ -509,8 +568,8 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
 #pragma unroll
       for (int i = 0; i < L::NCL; ++i)
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (L::valid(sub, i, k)) px[L::dim(sub, i, k) * n] = x[4 * i + k];
+        for (int k = 0; k < kW; ++k)
+          if (L::valid(sub, i, k)) px[L::dim(sub, i, k) * n] = x[kW * i + k];
     }
     if ((a.flags & RUNF_RECORD_LLP) && active && sub == 0) {
       a.rec_ll[s * N + c] = ll;
@@ -522,12 +581,12 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
 #pragma unroll
       for (int i = 0; i < L::NCL; ++i)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < kW; ++k) {
           if (!L::valid(sub, i, k)) continue;
-          if constexpr (!AccumCfg<D, P>::kLds && !AccumCfg<D, P>::kReg) { if (!active) continue; }
+          if constexpr (!ACfg::kLds && !ACfg::kReg) { if (!active) continue; }
           double& mu = acc_mean(i, k);
           double& m2 = acc_m2(i, k);
-          const double xv = x[4 * i + k];
+          const double xv = x[kW * i + k];
           const double delta = xv - mu;
           const double mnew = fma(delta, inv, mu);
           m2 = fma(delta, xv - mnew, m2);
@@ -561,10 +620,10 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
 #pragma unroll
     for (int i = 0; i < L::NCL; ++i)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < kW; ++k) {
         const int d = L::valid(sub, i, k) ? L::dim(sub, i, k) : 0;
-        rc_m[4 * i + k] = LIK == MCG_LIK_FLAT ? 0.0 : a.lik[d];
-        rc_i[4 * i + k] = LIK == MCG_LIK_DIAG_GAUSS ? a.lik[D + d] : 0.0;
+        rc_m[kW * i + k] = LIK == MCG_LIK_FLAT ? 0.0 : a.lik[d];
+        rc_i[kW * i + k] = LIK == MCG_LIK_DIAG_GAUSS ? a.lik[D + d] : 0.0;
       }
   }
   // kD independence proposal: a step's draw depends on the RNG only (the picked training point's
@@ -576,19 +635,33 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
   int kd_leaf = 0, kd_leaf_n = 0;
   double kd_lo[KDN], kd_hi[KDN];
   double kd_lqp = 0.0;
-  auto kd_pick_leaf = [&](uint64_t Tp) -> int {
+  auto kd_pick = [&](uint64_t Tp) -> uint32_t {
     const u32x4 w = rng(gid, (uint32_t)Tp, CALL_KD_PICK, TAG_MH, (uint32_t)(Tp >> 32));
-    return a.kd_pt_leaf[randint(w.x, w.y, (uint32_t)a.kd_M)];
+    return randint(w.x, w.y, (uint32_t)a.kd_M);
+  };
+  auto kd_pick_leaf = [&](uint64_t Tp) -> int { return a.kd_pt_leaf[kd_pick(Tp)]; };
+  // P > 1: the picks are staggered over the chain's lanes like the accept uniforms: at the first
+  // step t of each group of P steps, lane `sub` draws the pick of step t + 2 + sub, and step
+  // t + q (which prefetches the leaf of step t + q + 2) takes it from lane q -- one pick per P
+  // lane-steps instead of one per lane-step
+  uint32_t pick_own = 0;
+  auto bcast_u32 = [&](uint32_t v, int q) -> uint32_t {
+    if constexpr (P == 4) {
+      return q == 0 ? quad_bcast_u32<0>(v) : q == 1 ? quad_bcast_u32<1>(v) : q == 2 ? quad_bcast_u32<2>(v)
+                                                                                  : quad_bcast_u32<3>(v);
+    } else {
+      return (uint32_t)__shfl((int)v, (lane & ~(P - 1)) | q, 64);
+    }
   };
   auto kd_load_box = [&](int leaf) {
     const double* __restrict__ bx = a.kd_box + (int64_t)leaf * 2 * D;
 #pragma unroll
     for (int i = 0; i < (PROP == MCG_PROP_KD_INTERP ? L::NCL : 0); ++i)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < kW; ++k) {
         const int d = L::valid(sub, i, k) ? L::dim(sub, i, k) : 0;
-        kd_lo[4 * i + k] = bx[d];
-        kd_hi[4 * i + k] = bx[D + d];
+        kd_lo[kW * i + k] = bx[d];
+        kd_hi[kW * i + k] = bx[D + d];
       }
     kd_lqp = a.kd_logq[leaf];
   };
@@ -612,8 +685,8 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
 #pragma unroll
     for (int i = 0; i < (PROP == MCG_PROP_KD_INTERP ? L::NCL : 0); ++i)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int j = 4 * i + 2 * h;
+      for (int h = 0; h < kW / 2; ++h) {
+        const int j = kW * i + 2 * h;
         if (!L::valid(sub, i, 2 * h)) continue;
         const u32x4 v = rng(gid, (uint32_t)Tu, (uint32_t)(L::dim(sub, i, 2 * h) >> 1), TAG_MH, (uint32_t)(Tu >> 32));
         kd_u[j] = u53(v.x, v.y);
@@ -672,12 +745,12 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
         const int cc = sub + P * i;
         if (!L::valid(sub, i, k)) return;
         const int d = 4 * cc + k;
-        const double yv = fma(UNI ? a.uni_s : qprop[d], zk, x[4 * i + k]);
-        y[4 * i + k] = yv;
+        const double yv = fma(UNI ? a.uni_s : qprop[d], zk, x[kW * i + k]);
+        y[kW * i + k] = yv;
         double rcm = 0.0, rci = 0.0;
         if constexpr (UNI) {
-          rcm = rc_m[4 * i + k];
-          rci = rc_i[4 * i + k];
+          rcm = rc_m[kW * i + k];
+          rci = rc_i[kW * i + k];
         }
         if constexpr (LIK == MCG_LIK_DIAG_GAUSS) {
           const double e = UNI ? fma(yv, rci, -rcm) : fma(yv, qlik[D + d], -qlik[d]);
@@ -696,15 +769,15 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
       auto dims = [&](const int i, const double* z) {
         const int cc = sub + P * i;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < kW; ++k) {
           if (!L::valid(sub, i, k)) continue;
           const int d = 4 * cc + k;
-          const double yv = fma(UNI ? a.uni_s : qprop[d], z[k], x[4 * i + k]);
-          y[4 * i + k] = yv;
+          const double yv = fma(UNI ? a.uni_s : qprop[d], z[k], x[kW * i + k]);
+          y[kW * i + k] = yv;
           double rcm = 0.0, rci = 0.0;
           if constexpr (UNI) {
-            rcm = rc_m[4 * i + k];
-            rci = rc_i[4 * i + k];
+            rcm = rc_m[kW * i + k];
+            rci = rc_i[kW * i + k];
           }
           if constexpr (LIK == MCG_LIK_DIAG_GAUSS) {
             const double e = UNI ? fma(yv, rci, -rcm)
@@ -783,8 +856,8 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
           z[2] = pnormal(w.z, s_nt);
           z[3] = pnormal(w.w, s_nt);
 #pragma unroll
-          for (int k = 0; k < 4; ++k)
-            if (L::valid(sub, i, k)) y[4 * i + k] = fma(qprop[L::dim(sub, i, k)], z[k], x[4 * i + k]);
+          for (int k = 0; k < kW; ++k)
+            if (L::valid(sub, i, k)) y[kW * i + k] = fma(qprop[L::dim(sub, i, k)], z[k], x[kW * i + k]);
         }
       } else if constexpr (PROP == MCG_PROP_WRAP_UNIFORM) {
         static_assert(P == 1, "WRAP: one lane per chain");
@@ -797,7 +870,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
                                     u53(w.z, w.w));
         }
       } else if constexpr (PROP == MCG_PROP_KD_INTERP) {
-        static_assert(P == 1 || D % (4 * P) == 0, "KD: P lanes need D % 4P == 0");
+        static_assert(P == 1 || D % (kW * P) == 0, "KD: P lanes need D % WP == 0");
         // Interpolate_pdf.draw (interpolate_pdf.ml:114-119) from the leaf and box loaded ahead;
         // dims 2c and 2c + 1 from call c (lane `sub`: the calls of its 4-dim blocks)
         kd_uniforms(T);
@@ -822,8 +895,8 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
 #pragma unroll
               for (int i = 0; i < L::NCL; ++i)
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
-                  if (L::valid(o, i, k)) yf[L::dim(o, i, k)] = __shfl(y[4 * i + k], (lane & ~(P - 1)) | o, 64);
+                for (int k = 0; k < kW; ++k)
+                  if (L::valid(o, i, k)) yf[L::dim(o, i, k)] = __shfl(y[kW * i + k], (lane & ~(P - 1)) | o, 64);
             lqy = a.kd_logq[kd_find_leaf<D>(a.kd_nodes, a.kd_root, yf)];
           }
         }
@@ -832,7 +905,13 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
         // accept and records and the next step's uniforms
         kd_leaf = kd_leaf_n;
         kd_load_box(kd_leaf);
-        kd_leaf_n = kd_pick_leaf(T + 2);
+        if constexpr (P == 1) {
+          kd_leaf_n = kd_pick_leaf(T + 2);
+        } else {
+          const int qk = (int)(t & (P - 1));
+          if (qk == 0) pick_own = kd_pick(T + 2 + (uint64_t)sub);
+          kd_leaf_n = a.kd_pt_leaf[bcast_u32(pick_own, qk)];
+        }
         lf = lqy;   // log_jump_prob start proposed = log q(proposed)
         lb = lq;    // log_jump_prob proposed start = log q(start)
       }
@@ -884,8 +963,8 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
             z[2] = pnormal(w.z, s_nt);
             z[3] = pnormal(w.w, s_nt);
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-              if (4 * i + k < D) y[4 * i + k] = fma(m[5 + 4 * i + k], z[k], x[4 * i + k]);
+            for (int k = 0; k < kW; ++k)
+              if (kW * i + k < D) y[kW * i + k] = fma(m[5 + kW * i + k], z[k], x[kW * i + k]);
           }
         } else if (kind == MCG_MIX_KD_INTERP) {
           const u32x4 w = rng(gid, tlo, CALL_KD_PICK, TAG_MH, thi);
@@ -924,8 +1003,8 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
       }
       if constexpr (kKdLds) {
         typedef const __attribute__((address_space(3))) double lconst;
-        lly = eval_lik<D, P, LIK>(y, sub, a, (lconst*)s_kl);
-        lpy = eval_prior<D, P>(y, sub, a, (lconst*)s_kp);
+        lly = eval_lik<D, P, LIK, lconst*, kW>(y, sub, a, (lconst*)s_kl);
+        lpy = eval_prior<D, P, lconst*, kW>(y, sub, a, (lconst*)s_kp);
       } else {
         // likelihood / prior constants through scalar loads (the scalar cache and lgkmcnt, not
         // a per-step vmcnt wait behind the proposal's loads)
@@ -933,8 +1012,8 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
         kconst* klik = (kconst*)a.lik;
         kconst* kpri = (kconst*)a.pri;
         asm volatile("" : "+s"(klik), "+s"(kpri));
-        lly = eval_lik<D, P, LIK>(y, sub, a, klik);
-        lpy = eval_prior<D, P>(y, sub, a, kpri);
+        lly = eval_lik<D, P, LIK, kconst*, kW>(y, sub, a, klik);
+        lpy = eval_prior<D, P, kconst*, kW>(y, sub, a, kpri);
       }
     }
     // ---- Hastings ratio and accept test (mcmc.ml:42-56) ----
@@ -1000,19 +1079,19 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
 #pragma unroll
   for (int i = 0; i < L::NCL; ++i)
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (L::valid(sub, i, k)) a.x[(int64_t)L::dim(sub, i, k) * n + c] = x[4 * i + k];
+    for (int k = 0; k < kW; ++k)
+      if (L::valid(sub, i, k)) a.x[(int64_t)L::dim(sub, i, k) * n + c] = x[kW * i + k];
   if (sub == 0) {
     a.ll[c] = ll;
     a.lp[c] = lp;
     a.nacc[c] += na;
   }
   if (accum) {
-    if constexpr (AccumCfg<D, P>::kReg || AccumCfg<D, P>::kLds) {
+    if constexpr (ACfg::kReg || ACfg::kLds) {
 #pragma unroll
       for (int i = 0; i < L::NCL; ++i)
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
+        for (int k = 0; k < kW; ++k)
           if (L::valid(sub, i, k)) {
             int64_t o = (int64_t)L::dim(sub, i, k) * n + c;
             a.mean[o] = acc_mean(i, k);
@@ -1052,7 +1131,7 @@ template <int D, int P, int LIK, int PROP>
 hipError_t launch_mh(const MhArgs& a, int64_t nthreads, hipStream_t s) {
   const int block = MhShape<D, P, LIK, PROP>::kBlock;
   const int64_t grid = (nthreads + block - 1) / block;
-  constexpr int lds = AccumCfg<D, P>::kLdsBytes;
+  constexpr int lds = AccumCfg<D, P, lane_width<D, P, PROP>()>::kLdsBytes;
   if constexpr (separable<LIK, PROP>()) {
     if (a.uni && a.uni_lo == -a.uni_hi) {
       hipLaunchKernelGGL((mh_kernel<D, P, LIK, PROP, 2>), dim3((unsigned)grid), dim3(block), lds, s, a);

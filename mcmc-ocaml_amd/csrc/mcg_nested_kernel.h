@@ -179,30 +179,7 @@ struct WalkLayout {
   }
 };
 
-// the canonical sum for W = 2 (D = 2P): lane sub holds the terms of dims 2 sub, 2 sub + 1, which
-// belong to accumulator A_j, j = sub / 2.  The even lane of the pair folds dims 4j, 4j + 1 from
-// zero, the odd lane continues from that partial with dims 4j + 2, 4j + 3 (the sequential fma
-// chain of A_j), and the odd lanes (A_0 .. A_{P/2-1}) meet in the canonical tree
-// ((A0 + A4) + (A2 + A6)) + ((A1 + A5) + (A3 + A7)), whose A_4 .. A_7 are zero here (x + 0 = x
-// for the sums of squares): (A0 + A2) + (A1 + A3) at P = 8, A0 + A1 at P = 4.  Even lanes take
-// their odd neighbour's value.  Additions are commutative, so every lane of the tree holds the
-// same bits.
-template <int P>
-__device__ __forceinline__ double reduce_canon_w2(double e0, double e1, int sub) {
-  static_assert(P == 4 || P == 8, "W = 2 walkers run on 4 or 8 lanes");
-  const double t = fma(e1, e1, fma(e0, e0, 0.0));
-  const double tp = xor_lane_d<1>(t);
-  const double a = fma(e1, e1, fma(e0, e0, tp));
-  double c;
-  if constexpr (P == 8) {
-    const double b = a + xor_lane_d<4>(a);
-    c = b + xor_lane_d<2>(b);
-  } else {
-    c = a + xor_lane_d<2>(a);
-  }
-  const double o = xor_lane_d<1>(c);
-  return (sub & 1) ? c : o;
-}
+// (the canonical sum for W = 2 is reduce_canon_w2, mcg_mh_kernel.h)
 
 // The log-target constants of one walker lane (its dims of mu/sigma or the shell centre, the box
 // bounds), loaded into registers once per launch.  Loaded per step through the parameter

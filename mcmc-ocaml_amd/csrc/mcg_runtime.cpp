@@ -751,18 +751,22 @@ int choose_lanes(mcg_ctx* ctx) {
   const bool kd_split = ctx->prop_kind == MCG_PROP_KD_INTERP &&
                         (ctx->lik_kind == MCG_LIK_DIAG_GAUSS || ctx->lik_kind == MCG_LIK_GAUSS_SHELL ||
                          ctx->lik_kind == MCG_LIK_FLAT);
+  // (the kD draw also splits two dims per lane when D = 2P: mcg_mh_kernel.h Layout W = 2)
+  auto splits = [&](int P) {
+    return (D % (4 * P) == 0 || (kd_split && D == 2 * P)) && find_mh_kernel(D, P, ctx->lik_kind, ctx->prop_kind);
+  };
   if (want > 0) {
     if (want == 1) return 1;
-    if ((separable || fullcov_mfma || kd_split) && D % (4 * want) == 0 && find_mh_kernel(D, want, ctx->lik_kind, ctx->prop_kind)) return want;
+    if ((separable || fullcov_mfma || kd_split) && splits(want)) return want;
     return 1;
   }
   if (fullcov_mfma) return 4;
   if (!separable && !kd_split) return 1;
   const int64_t lanes_target = (int64_t)std::max(ctx->num_cus, 1) * 4 * 4 * 64;  // 4 waves/SIMD
   int best = 1;
-  for (int P : {2, 4}) {
+  for (int P : {2, 4, 8}) {
     if (ctx->N * best >= lanes_target) break;
-    if (D % (4 * P) == 0 && find_mh_kernel(D, P, ctx->lik_kind, ctx->prop_kind)) best = P;
+    if ((P < 8 || kd_split) && splits(P)) best = P;
   }
   return best;
 }

@@ -200,10 +200,13 @@ def test_kd_interp_proposal_bit_exact(oracle, T):
 
 @pytest.mark.parametrize("D,lanes,uniform_box,nch", [(8, 1, True, 160), (8, 2, True, 160),
                                                       (8, 2, False, 100), (16, 2, False, 160),
-                                                      (16, 4, True, 100)])
+                                                      (16, 4, True, 100), (8, 4, True, 160),
+                                                      (8, 4, False, 100), (16, 8, True, 100),
+                                                      (4, 2, False, 160)])
 def test_kd_interp_lane_splits_bit_exact(oracle, T, D, lanes, uniform_box, nch):
-    """The kD draw split over 1, 2 or 4 lanes per chain (each lane its dims' box bounds and
-    uniforms, the likelihood / prior constants staged in LDS), with the box prior as kernel
+    """The kD draw split over 1, 2, 4 or 8 lanes per chain (each lane its dims' box bounds and
+    uniforms, the likelihood / prior constants staged in LDS) -- four-dim lane blocks, or two dims
+    per lane (D = 2 lanes: the pair-chained canonical accumulator) -- with the box prior as kernel
     arguments or as per-dim bounds: the oracle's chains bit for bit."""
     rng = np.random.default_rng(11 + D)
     mu = np.linspace(-0.2, 0.2, D); sg = np.linspace(0.8, 1.2, D)
@@ -217,6 +220,13 @@ def test_kd_interp_lane_splits_bit_exact(oracle, T, D, lanes, uniform_box, nch):
     g = run_gpu(lik, pri, kdp, x0, 9, nbin=3, nskip=2, n_rec=40, lanes=lanes)
     o = run_oracle(oracle, lik, pri, T.gauss(1.0), x0, 9, 3, 2, 40, kd=okd)
     assert_same(g, o)
+    from mcmc_amd import Context
+    ctx = Context(seed=9, lanes_per_chain=lanes)
+    ctx.set_model(lik, pri, kdp)
+    ctx.init(x0)
+    ctx.run(nbin=1, n_rec=0, record_x=False, record_llp=False)
+    assert ctx.lanes() == lanes
+    ctx.close()
 
 
 def test_kd_tree_export_matches_oracle(oracle, T):
