@@ -700,6 +700,30 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
       kd_leaf_n = kd_pick_leaf(a.step_base + 1);
     }
   }
+  // log u of step t (mcmc.ml:49).  P > 1: staggered accept uniforms -- at the first step of each
+  // group of P steps, lane `sub` of the chain draws log u for step t + sub; step t + q reads it
+  // from lane q (one DPP broadcast, or a shuffle at P = 8)
+  auto accept_lu = [&](int64_t t, uint64_t T) -> double {
+    if constexpr (P == 1) {
+      const u32x4 wa = rng(gid, (uint32_t)T, CALL_ACCEPT, TAG_MH, (uint32_t)(T >> 32));
+      return plog(u53(wa.x, wa.y), s_lt);
+    } else {
+      const int q = (int)(t & (P - 1));
+      if (q == 0) {
+        const uint64_t Tj = T + (uint64_t)sub;
+        const u32x4 wa = rng(gid, (uint32_t)Tj, CALL_ACCEPT, TAG_MH, (uint32_t)(Tj >> 32));
+        lu_own = plog(u53(wa.x, wa.y), s_lt);
+      }
+      if constexpr (P == 4) {
+        return q == 0 ? quad_bcast_f64<0>(lu_own) : q == 1 ? quad_bcast_f64<1>(lu_own)
+             : q == 2 ? quad_bcast_f64<2>(lu_own) : quad_bcast_f64<3>(lu_own);
+      } else if constexpr (P == 2) {
+        return q == 0 ? pair_bcast_f64<0>(lu_own) : pair_bcast_f64<1>(lu_own);
+      } else {
+        return __shfl(lu_own, (lane & ~(P - 1)) | q, 64);
+      }
+    }
+  };
   for (int64_t t = 0; t < a.nsteps; ++t) {
     const uint64_t T = a.step_base + (uint64_t)t;
     const uint32_t tlo = (uint32_t)T, thi = (uint32_t)(T >> 32);
@@ -1019,29 +1043,8 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
     // ---- Hastings ratio and accept test (mcmc.ml:42-56) ----
     const double post_y = lly + lpy;
     const double post_x = ll + lp;
+    const double lu = accept_lu(t, T);
     const double ratio = ((post_y - post_x) + lb) - lf;
-    double lu;
-    if constexpr (P == 1) {
-      const u32x4 wa = rng(gid, tlo, CALL_ACCEPT, TAG_MH, thi);
-      lu = plog(u53(wa.x, wa.y), s_lt);
-    } else {
-      // staggered accept uniforms: at the first step of each group of P steps, lane `sub` of the
-      // chain draws log u for step t + sub; step t + q reads it from lane q (one shuffle)
-      const int q = (int)(t & (P - 1));
-      if (q == 0) {
-        const uint64_t Tj = T + (uint64_t)sub;
-        const u32x4 wa = rng(gid, (uint32_t)Tj, CALL_ACCEPT, TAG_MH, (uint32_t)(Tj >> 32));
-        lu_own = plog(u53(wa.x, wa.y), s_lt);
-      }
-      if constexpr (P == 4) {                      // quad broadcast of lane q (DPP)
-        lu = q == 0 ? quad_bcast_f64<0>(lu_own) : q == 1 ? quad_bcast_f64<1>(lu_own)
-           : q == 2 ? quad_bcast_f64<2>(lu_own) : quad_bcast_f64<3>(lu_own);
-      } else if constexpr (P == 2) {               // pair broadcast of lane q (DPP)
-        lu = q == 0 ? pair_bcast_f64<0>(lu_own) : pair_bcast_f64<1>(lu_own);
-      } else {
-        lu = __shfl(lu_own, (lane & ~(P - 1)) | q, 64);
-      }
-    }
     const bool acc = lu < ratio;
     if (acc) {
 #pragma unroll

@@ -91,6 +91,9 @@ type likelihood =
   | Gauss_shell of float array * float * float
   | Gauss_data of float array array
   | Cauchy_data of float array array
+  | Gauss_mix of float array array * float array array
+      (* component means and sigmas: ll = log (sum_i exp (log_multi_gaussian mu_i sigma_i x)),
+         test/nested_test.ml:52-57 *)
 
 type prior =
   | Flat_prior
@@ -132,6 +135,11 @@ let destroy ctx = c_ctx_destroy ctx
 let carr a = CArray.start (CArray.of_list double (Array.to_list a))
 let flatten m = Array.concat (Array.to_list m)
 
+(* GAUSS_MIX parameters (include/mcg.h): m, then per component mu_i, sigma_i *)
+let mix_params mus sigmas =
+  let comps = Array.mapi (fun i mu -> Array.append mu sigmas.(i)) mus in
+  Array.concat ([| float (Array.length mus) |] :: Array.to_list comps)
+
 let set_model ctx lik pri prop =
   let kind, nd, params = match lik with
     | Flat d -> 0, d, [| 0.0 |]
@@ -139,7 +147,8 @@ let set_model ctx lik pri prop =
     | Fullcov_gauss (mu, u) -> 2, Array.length mu, Array.append mu (flatten u)
     | Gauss_shell (c, r, w) -> 3, Array.length c, Array.append c [| r; w |]
     | Gauss_data d -> 4, 2 * Array.length d.(0), Array.append [| float (Array.length d.(0)) |] (flatten d)
-    | Cauchy_data d -> 5, 2 * Array.length d.(0), Array.append [| float (Array.length d.(0)) |] (flatten d) in
+    | Cauchy_data d -> 5, 2 * Array.length d.(0), Array.append [| float (Array.length d.(0)) |] (flatten d)
+    | Gauss_mix (mus, sigmas) -> 6, Array.length mus.(0), mix_params mus sigmas in
   check ctx (c_set_likelihood ctx (Int32.of_int kind) (Int32.of_int nd) (carr params)
                (Unsigned.Size_t.of_int (Array.length params)));
   Hashtbl.replace dims ctx nd;
@@ -178,13 +187,20 @@ let set_model ctx lik pri prop =
 
 type state = mat * vec * vec
 
-(* Mcmc.make_mcmc_sampler (mcmc.ml:37-56) over a batch of chains: one MH step per call *)
+(* Mcmc.make_mcmc_sampler (mcmc.ml:37-56) over a batch of chains: one MH step per call.  The
+   chains stay on the device between calls: when the argument is the state this sampler returned
+   last, the step runs from the device copy (mcg_run + mcg_get_state, no mcg_init upload). *)
 let make_mcmc_sampler ctx lik pri prop =
   set_model ctx lik pri (Some prop);
+  let last = ref None in
   fun ((x : mat), (ll : vec), (lp : vec)) ->
     let d = Bigarray.Array2.dim1 x and nch = Bigarray.Array2.dim2 x in
-    check ctx (c_init ctx (Int64.of_int nch) (bigarray_start array2 x) (bigarray_start array1 ll)
-                 (bigarray_start array1 lp));
+    let resident = match !last with
+      | Some (x0, ll0, lp0) -> x == x0 && ll == ll0 && lp == lp0
+      | None -> false in
+    if not resident then
+      check ctx (c_init ctx (Int64.of_int nch) (bigarray_start array2 x) (bigarray_start array1 ll)
+                   (bigarray_start array1 lp));
     let o = make run_opts in
     setf o r_nbin 1L; setf o r_nskip 1L; setf o r_nrec 0L;
     setf o r_rx 0l; setf o r_rllp 0l; setf o r_racc 0l; setf o r_accum 0l; setf o r_append 0l;
@@ -193,6 +209,7 @@ let make_mcmc_sampler ctx lik pri prop =
     let x' = Array2.create float64 c_layout d nch in
     let ll' = Array1.create float64 c_layout nch and lp' = Array1.create float64 c_layout nch in
     check ctx (c_get_state ctx (bigarray_start array2 x') (bigarray_start array1 ll') (bigarray_start array1 lp'));
+    last := Some (x', ll', lp');
     (x', ll', lp')
 
 let reset_counters ctx = check ctx (c_reset_counters ctx)
@@ -312,7 +329,8 @@ let lik_params = function
   | Diag_gauss (mu, s) -> 1, Array.length mu, Array.append mu s
   | Fullcov_gauss (mu, u) -> 2, Array.length mu, Array.append mu (flatten u)
   | Gauss_shell (c, r, w) -> 3, Array.length c, Array.append c [| r; w |]
-  | Gauss_data _ | Cauchy_data _ -> raise (Invalid_argument "rjmcmc: data likelihoods are not supported")
+  | Gauss_data _ | Cauchy_data _ | Gauss_mix _ ->
+    raise (Invalid_argument "rjmcmc: data and mixture likelihoods are not supported")
 
 let rj_struct m =
   let s = make rj_model_s in

@@ -27,6 +27,9 @@ type likelihood =
   | Gauss_shell of float array * float * float   (** centre, radius, width *)
   | Gauss_data of float array array              (** bin/gaussian_cauchy.ml log_like_gaussian *)
   | Cauchy_data of float array array             (** bin/gaussian_cauchy.ml log_like_cauchy *)
+  | Gauss_mix of float array array * float array array
+      (** component means and sigmas: log of the sum of the components' log_multi_gaussian
+          densities, the multimodal target of test/nested_test.ml:41-64 *)
 
 type prior =
   | Flat_prior

@@ -163,6 +163,32 @@ def c3(args):
     return line
 
 
+def c2(args):
+    """The headline C2 MH workload (bench.py's timed part, for same-box A/B): D=32 diagonal
+    Gaussian, 65,536 chains, launches of 1,000 sweeps folded into the moments."""
+    D, N, S, K = 32, 65536, 1000, args.launches // 10
+    rng = np.random.default_rng(42)
+    mu, sg = rng.uniform(-1.0, 1.0, D), rng.uniform(0.5, 2.0, D)
+    s = 2.38 / math.sqrt(D) * float(np.median(sg))
+    ctx = Context(seed=args.seed)
+    ctx.set_model(T.diag_gauss(mu, sg), T.box(-10 * np.ones(D), 10 * np.ones(D)), T.gauss(s))
+    ctx.init(np.random.default_rng(1000).normal(mu[:, None], sg[:, None], size=(D, N)))
+    ctx.run(nbin=S, nskip=1, n_rec=1, record_x=False, record_llp=False, accumulate=True)
+    ctx.sync()
+    ctx.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(K):
+        ctx.run(nbin=0, nskip=1, n_rec=S, record_x=False, record_llp=False, accumulate=True, append=True)
+    ctx.sync()
+    dt = time.perf_counter() - t0
+    line = {"config": "C2 D=32 diagonal Gaussian, %d chains, %d sweeps" % (N, K * S), "unit": "MH steps/s",
+            "dtype": "f64", "value": N * S * K / dt, "lanes": ctx.lanes(),
+            "roofline": roofline("mcg::mh_kernel<32,P,DIAG_GAUSS,GAUSS>", N * S, 8.0 * (D + 2),
+                                 ctx.kernel_timing("mh"))}
+    ctx.close()
+    return line
+
+
 def c4(args):
     """Interpolate_pdf kD-tree independence proposal, D=8 N(0,1) target, M=32,768 exact draws,
     32,768 chains."""
@@ -254,7 +280,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3, help="C3: timed nested runs (median reported)")
     ap.add_argument("--c5-chains", type=int, default=131072)
     args = ap.parse_args()
-    fns = {"c1": c1, "c3": c3, "c4": c4, "c5": c5}
+    fns = {"c1": c1, "c2": c2, "c3": c3, "c4": c4, "c5": c5}
     for c in args.configs:
         line = fns[c](args)
         s = json.dumps(line)
