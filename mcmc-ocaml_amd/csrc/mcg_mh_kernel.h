@@ -608,12 +608,19 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
 
   double lu_own = 0.0;
   // UNI (isotropic proposal scale, one box for every dim): the scale and the box are kernel
-  // arguments (SGPRs), so the lane's likelihood constants fit in registers for the whole launch
-  double rc_m[UNI ? L::NL : 1], rc_i[UNI ? L::NL : 1];
+  // arguments (SGPRs), so the lane's likelihood constants fit in registers for the whole launch.
+  // kKdReg (kD proposal on P > 1 lanes, DIAG / SHELL / FLAT): the lane's likelihood constants,
+  // normaliser and prior box are registers too -- a handful per lane; staged in LDS they were a
+  // read and an lgkmcnt wait on every step's likelihood
+  constexpr bool kKdReg = PROP == MCG_PROP_KD_INTERP && P > 1;
+  static_assert(!kKdReg || LIK == MCG_LIK_FLAT || LIK == MCG_LIK_DIAG_GAUSS || LIK == MCG_LIK_GAUSS_SHELL,
+                "kD on P > 1 lanes: FLAT, DIAG_GAUSS or GAUSS_SHELL");
+  constexpr int kRc = (UNI || kKdReg) ? L::NL : 1;
+  double rc_m[kRc], rc_i[kRc];
   // UNI: the likelihood normaliser and the box's log density in VGPRs too (a per-step cached
   // load of each put a vector-memory wait on every step's critical path)
   double rc_c = 0.0, rc_lp = 0.0;
-  if constexpr (UNI) {
+  if constexpr (UNI || kKdReg) {
     rc_c = LIK == MCG_LIK_DIAG_GAUSS ? a.lik[2 * D] : LIK == MCG_LIK_GAUSS_SHELL ? a.lik[D + 2] : 0.0;
     rc_lp = a.prior_kind != MCG_PRIOR_FLAT ? a.pri[2 * D] : 0.0;
     asm volatile("" : "+v"(rc_c), "+v"(rc_lp));
@@ -624,6 +631,24 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
         const int d = L::valid(sub, i, k) ? L::dim(sub, i, k) : 0;
         rc_m[kW * i + k] = LIK == MCG_LIK_FLAT ? 0.0 : a.lik[d];
         rc_i[kW * i + k] = LIK == MCG_LIK_DIAG_GAUSS ? a.lik[D + d] : 0.0;
+      }
+  }
+  // kKdReg: the shell's radius and inverse width, and the prior box per lane dim
+  double rc_r = 0.0, rc_iw = 0.0;
+  double rc_lo[kKdReg ? L::NL : 1], rc_hi[kKdReg ? L::NL : 1];
+  if constexpr (kKdReg) {
+    if constexpr (LIK == MCG_LIK_GAUSS_SHELL) {
+      rc_r = a.lik[D];
+      rc_iw = a.lik[D + 1];
+    }
+    const bool pbox = a.prior_kind != MCG_PRIOR_FLAT;
+#pragma unroll
+    for (int i = 0; i < L::NCL; ++i)
+#pragma unroll
+      for (int k = 0; k < kW; ++k) {
+        const int d = L::valid(sub, i, k) ? L::dim(sub, i, k) : 0;
+        rc_lo[kW * i + k] = pbox ? (a.ubox ? a.box_lo : a.pri[d]) : 0.0;
+        rc_hi[kW * i + k] = pbox ? (a.ubox ? a.box_hi : a.pri[D + d]) : 0.0;
       }
   }
   // kD independence proposal: a step's draw depends on the RNG only (the picked training point's
@@ -665,19 +690,6 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
       }
     kd_lqp = a.kd_logq[leaf];
   };
-  // P > 1: the generic step's likelihood / prior constants staged in LDS (lane-dependent dims:
-  // scalar loads do not apply, and vector loads would be waited with vmcnt(0) every step)
-  constexpr bool kKdLds = PROP == MCG_PROP_KD_INTERP && P > 1;
-  constexpr int kKdLik = kKdLds ? 2 * D + 3 : 1, kKdPri = kKdLds ? 2 * D + 1 : 1;
-  __shared__ double s_kl[kKdLik], s_kp[kKdPri];
-  if constexpr (kKdLds) {
-    const int nl = LIK == MCG_LIK_DIAG_GAUSS ? 2 * D + 1 : LIK == MCG_LIK_GAUSS_SHELL ? D + 3 : 0;
-    __syncthreads();
-    for (int i = threadIdx.x; i < nl; i += blockDim.x) s_kl[i] = a.lik[i];
-    if (a.prior_kind != MCG_PRIOR_FLAT)
-      for (int i = threadIdx.x; i < 2 * D + 1; i += blockDim.x) s_kp[i] = a.pri[i];
-    __syncthreads();
-  }
   // the uniforms of a step's box draw (dims 2c and 2c + 1 from call c; the lane's own blocks),
   // drawn one step ahead
   double kd_u[KDN];
@@ -1025,10 +1037,56 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
         lf = mix_log_jp<D>(qprop, x, y, lqy, s_lt);   // log_jump_prob start proposed
         lb = mix_log_jp<D>(qprop, y, x, lq, s_lt);    // log_jump_prob proposed start
       }
-      if constexpr (kKdLds) {
-        typedef const __attribute__((address_space(3))) double lconst;
-        lly = eval_lik<D, P, LIK, lconst*, kW>(y, sub, a, (lconst*)s_kl);
-        lpy = eval_prior<D, P, lconst*, kW>(y, sub, a, (lconst*)s_kp);
+      if constexpr (kKdReg) {
+        // eval_lik / eval_prior of the lane's dims on the register constants (the same operations)
+        if constexpr (LIK == MCG_LIK_FLAT) {
+          lly = 0.0;
+        } else {
+          double S;
+          if constexpr (kW == 2) {
+            double e[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+              e[k] = LIK == MCG_LIK_DIAG_GAUSS ? fma(y[k], rc_i[k], -rc_m[k]) : y[k] - rc_m[k];
+            S = reduce_canon_w2<P>(e[0], e[1], sub);
+          } else {
+            double A[L::NA];
+#pragma unroll
+            for (int j = 0; j < L::NA; ++j) A[j] = 0.0;
+#pragma unroll
+            for (int i = 0; i < L::NCL; ++i)
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                if (!L::valid(sub, i, k)) continue;
+                const double e = LIK == MCG_LIK_DIAG_GAUSS ? fma(y[4 * i + k], rc_i[4 * i + k], -rc_m[4 * i + k])
+                                                           : y[4 * i + k] - rc_m[4 * i + k];
+                A[i % L::NA] = fma(e, e, A[i % L::NA]);
+              }
+            S = reduce_canon<P>(A);
+          }
+          if constexpr (LIK == MCG_LIK_DIAG_GAUSS) {
+            lly = rc_c - 0.5 * S;
+          } else {
+            const double rr = psqrt(S);
+            const double qq = (rr - rc_r) * rc_iw;
+            lly = rc_c - 0.5 * qq * qq;
+          }
+        }
+        if (a.prior_kind == MCG_PRIOR_FLAT) {
+          lpy = 0.0;
+        } else {
+          int inb = 1;
+#pragma unroll
+          for (int i = 0; i < L::NCL; ++i)
+#pragma unroll
+            for (int k = 0; k < kW; ++k) {
+              if (!L::valid(sub, i, k)) continue;
+              const double v = y[kW * i + k];
+              inb &= (int)(v >= rc_lo[kW * i + k]) & (int)(v <= rc_hi[kW * i + k]);
+            }
+          inb = and_lanes<P>(inb);
+          lpy = inb ? rc_lp : -__builtin_inf();
+        }
       } else {
         // likelihood / prior constants through scalar loads (the scalar cache and lgkmcnt, not
         // a per-step vmcnt wait behind the proposal's loads)

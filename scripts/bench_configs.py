@@ -30,6 +30,8 @@ HBM_PEAK_GBS = 8000.0
 
 def roofline(kernel, steps_per_launch, bytes_per_step, timing):
     per_launch = timing["total_ms"] / max(timing["launches"], 1)
+    if per_launch <= 0:            # no timed launch (e.g. under a profiler's kernel filter)
+        return {"bound": "hbm", "kernel": kernel, "avg_launch_ms": None, "launches": timing["launches"]}
     ach = steps_per_launch * bytes_per_step / (per_launch * 1e-3) / 1e9
     return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": ach / HBM_PEAK_GBS, "kernel": kernel, "bytes_per_step": bytes_per_step,
@@ -45,7 +47,7 @@ def valu_framing(name, D, N, S, avg_launch_ms):
             v = json.load(fh)
     except (OSError, ValueError):
         return None
-    if v.get("config") != {"ndim": D, "chains_per_gpu": N, "sweeps_per_step": S}:
+    if v.get("config") != {"ndim": D, "chains_per_gpu": N, "sweeps_per_step": S} or not avg_launch_ms:
         return None
     issue = 4.0 * v["valu_insts_per_launch"] / 1024.0
     return {"bound": "valu", "insts_per_launch": v["valu_insts_per_launch"],
