@@ -750,8 +750,8 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
     gconst* gprop = (gconst*)a.prop;
     // (the fused step with UNI constants reads none of them: no per-step copies there)
     if constexpr (!(kSeparable && UNI)) asm volatile("" : "+s"(glik), "+s"(gpri), "+s"(gprop));
-    const double* qlik = (const double*)glik;
-    const double* qpri = (const double*)gpri;
+    [[maybe_unused]] const double* qlik = (const double*)glik;
+    [[maybe_unused]] const double* qpri = (const double*)gpri;
     const double* qprop = (const double*)gprop;
     double lly, lpy;
     if constexpr (kSeparable) {

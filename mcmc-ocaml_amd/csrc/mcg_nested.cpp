@@ -281,6 +281,10 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   if (ctx->rj_active) return set_error(ctx, MCG_ESTATE, "nested sampling after mcg_set_rjmcmc: set a likelihood first");
   if (ctx->prior_kind != MCG_PRIOR_BOX && ctx->prior_kind != MCG_PRIOR_OPEN_BOX)
     return set_error(ctx, MCG_EINVAL, "nested sampling needs a box prior (draw_prior = uniform in the box)");
+  // the box's log density enters every walker step's MH ratio as lp_box - lp_box = +0: a finite
+  // value is what makes that test always pass (mcg_nested_kernel.h, the shell walker's step)
+  if (!std::isfinite(ctx->pri_host[2 * D]))
+    return set_error(ctx, MCG_EINVAL, "nested sampling needs a finite box log density");
   const int64_t n = opts->nlive > 0 ? opts->nlive : 1000;
   const int64_t k = opts->k > 0 ? opts->k : 1;
   const int64_t nmcmc = opts->nmcmc >= 0 ? opts->nmcmc : 1000;

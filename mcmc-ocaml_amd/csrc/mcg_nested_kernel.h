@@ -116,7 +116,9 @@ constexpr int kNestWalkBlock = 64;
 
 // The random numbers of walker step s (draw_new_live_point, nested.ml:50-74): the DE pair i != j
 // (pick_samples, mcmc.ml:199-203), the DE scale (1 with probability mode_hop, else
-// N(0, 2.38/sqrt(2D)), mcmc.ml:209-213) and log u of the accept test (mcmc.ml:49).
+// N(0, 2.38/sqrt(2D)), mcmc.ml:209-213) and log u of the accept test (mcmc.ml:49).  LU = false:
+// the walker's accept test never reads log u (the shell walker, see its step), left 0
+template <bool LU = true>
 __device__ __forceinline__ void walk_draw(const NestArgs& a, uint32_t wid, uint32_t s,
                                           const double2* nt, const double2* lt,
                                           unsigned long long& ix, double2& sc) {
@@ -124,13 +126,17 @@ __device__ __forceinline__ void walk_draw(const NestArgs& a, uint32_t wid, uint3
   const uint32_t n = (uint32_t)a.n;
   const u32x4 rI = rng(wid, s, CALL_DE_IDX, TAG_NEST_WALK, 0u);
   const u32x4 rS = rng(wid, s, CALL_DE_SCALE, TAG_NEST_WALK, 0u);
-  const u32x4 rA = rng(wid, s, CALL_ACCEPT, TAG_NEST_WALK, 0u);
   const uint32_t i = randint(rI.x, rI.y, n);
   const uint32_t jj = randint(rI.z, rI.w, n - 1);
   const uint32_t j = jj + (jj >= i ? 1u : 0u);
   ix = (unsigned long long)i | ((unsigned long long)j << 32);
   sc.x = (a.mode_hop != 0.0 && u53(rS.x, rS.y) < a.mode_hop) ? 1.0 : a.sigma_de * pnormal(rS.z, nt);
-  sc.y = plog(u53(rA.x, rA.y), lt);
+  if constexpr (LU) {
+    const u32x4 rA = rng(wid, s, CALL_ACCEPT, TAG_NEST_WALK, 0u);
+    sc.y = plog(u53(rA.x, rA.y), lt);
+  } else {
+    sc.y = 0.0;
+  }
 }
 
 // the draws of every walker step of the generation that starts at replacement mrep, entries
@@ -142,6 +148,7 @@ __device__ __forceinline__ void walk_draw(const NestArgs& a, uint32_t wid, uint3
 __device__ __forceinline__ int64_t walk_tab_base(const NestArgs& a, int64_t mrep) {
   return ((mrep / a.k) & 1) * a.k * (a.nmcmc + kWalkTabPad);
 }
+template <bool LU = true>
 __device__ __forceinline__ void walk_draws_fill(const NestArgs& a, int64_t mrep, int64_t e0, int64_t stride,
                                                 const double2* lt) {
   const int64_t tot = a.k * a.nmcmc, base = walk_tab_base(a, mrep);
@@ -149,7 +156,7 @@ __device__ __forceinline__ void walk_draws_fill(const NestArgs& a, int64_t mrep,
     const int64_t s = e / a.k, w = e - s * a.k;
     unsigned long long ix;
     double2 sc;
-    walk_draw(a, (uint32_t)(mrep + w), (uint32_t)s, kNrmTab, lt, ix, sc);
+    walk_draw<LU>(a, (uint32_t)(mrep + w), (uint32_t)s, kNrmTab, lt, ix, sc);
     // byte offsets of the two rows: the walker adds them to the live set's base with no 64-bit
     // address arithmetic
     ix = (unsigned long long)((uint32_t)ix * a.row_bytes) | ((unsigned long long)((uint32_t)(ix >> 32) * a.row_bytes) << 32);
@@ -522,7 +529,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
           }
         }
       }
-      walk_draws_fill(a, a.mrep + a.k, (int64_t)blockIdx.x * nf + (threadIdx.x - 64), (int64_t)gridDim.x * nf, lt);
+      walk_draws_fill<!WalkTarget<D, P, LIK, SYM>::kFold>(a, a.mrep + a.k, (int64_t)blockIdx.x * nf + (threadIdx.x - 64), (int64_t)gridDim.x * nf, lt);
 #ifdef MCG_NEST_TRACE
       if (a.trace && threadIdx.x == 64 && blockIdx.x < 1024)   // the table-filling waves' end
         a.trace[((size_t)0 * 1024 + blockIdx.x) * 8 + 5] = wall_clock64();
@@ -759,13 +766,15 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
       if constexpr (WalkTarget<D, P, LIK, SYM>::kFold) {
         // ml is lp_box when the proposal passes and -inf when it fails, and -inf - cur_l fails
         // `lu < ratio` for every cur_l (-inf or NaN), so the step accepts iff it passes and
-        // lu < lp_box - cur_l: that half is ready before the reduction, off the serial chain
-        const double lpb = tgt.lp_box();
-        const bool pre = live && lu_g[u] < lpb - cur_l;
-        if (tgt.template constraint_box<kBoxT>(y, sub, thr) && pre) {
+        // lu < lp_box - cur_l.  That half always holds: cur_l is lp_box (a live point inside the
+        // box, or the last accepted proposal) or -inf (a start outside the constraint or on an
+        // open box's face), so lp_box - cur_l is +0 or +inf, and log u < 0 for every u53 draw
+        // (the largest, 1 - 2^-53, gives -1.1e-16: tests/test_oracle.py).  The step accepts
+        // iff it passes: no accept uniform is loaded or compared (the oracle's test, kept
+        // literally, takes the same decisions)
+        if (tgt.template constraint_box<kBoxT>(y, sub, thr) && live) {
 #pragma unroll
           for (int d = 0; d < NL; ++d) cur[d] = y[d];
-          cur_l = lpb;
         }
       } else {
         const bool ok = tgt.constraint(y, sub, a.m, thr);

@@ -120,12 +120,16 @@ def c3(args):
     lik = T.gauss_shell(np.zeros(D), r, w)
     pri = T.box(-half * np.ones(D), half * np.ones(D))
     ctx = Context(seed=args.seed)
-    # args.reps timed runs in one context (the same seed: identical runs; the first also pays the
-    # buffer allocations), then one run with per-walk HIP events for the roofline
+    # args.reps timed runs in one context after a warm-up run (the same seed: identical runs),
+    # then one run with per-walk HIP events for the roofline
     # value: the run with its inputs and outputs in HBM (log Z, log dZ, weights and ll / lp come
     # back; the n x D dead points stay on the device); the full call that also copies the points
     # to the host (457 MB over PCIe at C3) is reported beside it
     walls, walls_pts = [], []
+    # one untimed run first: the first call in a context allocates the live set, keys, draw tables
+    # and dead buffers (~50 ms), which no later run pays
+    out = nested.nested_evidence(lik, pri, epsrel=0.01, nmcmc=nmcmc, nlive=nlive, mode_hopping_frac=0.1,
+                                 k=k, ctx=ctx, points=False)
     out = None
     for _ in range(max(1, args.reps)):
         out = None              # the previous run's arrays are freed outside the timed call (~25 ms)
@@ -279,7 +283,7 @@ def main():
     ap.add_argument("--nmcmc", type=int, default=100)
     ap.add_argument("--launches", type=int, default=100,
                     help="C4/C5: timed sweeps / 100 (C4: launches of 1,000 sweeps, C5: of 500 -- at or under\n                    the runtime's own launch length min(4096, 2^26/N))")
-    ap.add_argument("--reps", type=int, default=3, help="C3: timed nested runs (median reported)")
+    ap.add_argument("--reps", type=int, default=5, help="C3: timed nested runs after a warm-up run (median reported)")
     ap.add_argument("--c5-chains", type=int, default=131072)
     args = ap.parse_args()
     fns = {"c1": c1, "c2": c2, "c3": c3, "c4": c4, "c5": c5}

@@ -34,6 +34,21 @@ def test_uniform_and_randint_ranges(oracle):
     assert L.or_randint(0xffffffff, 0xffffffff, 10) == 9
 
 
+def test_log_of_every_uniform_is_negative(oracle):
+    """log u < 0 for every u53 value: the nested shell walker relies on it to skip its accept
+    test (lp_box - cur_l is +0 or +inf, csrc/mcg_nested_kernel.h).  The 2^17 largest u53 values
+    (u >= 1 - 2^-36) are checked one by one; below them |log u| > 1e-11 dwarfs the <= 1 ulp error
+    of the portable log, checked here on a sample."""
+    L = oracle.lib()
+    assert L.or_log(L.or_u53(0xffffffff, 0xffffffff)) < 0
+    for m in range(1 << 17):
+        u = 1.0 - (2 * m + 1) * 2.0 ** -53
+        assert L.or_log(u) < 0, (m, u)
+    rng = np.random.default_rng(5)
+    for u in 1.0 - np.exp(rng.uniform(np.log(2.0 ** -36), 0.0, 20000)):
+        assert L.or_log(u) < 0 and abs(L.or_log(u) - math.log(u)) <= 2 * math.ulp(math.log(u))
+
+
 def test_portable_math_accuracy(oracle):
     L = oracle.lib()
     rng = np.random.default_rng(1)
