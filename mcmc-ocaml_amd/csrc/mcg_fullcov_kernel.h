@@ -166,7 +166,7 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
 
   int64_t next_rec = a.next_rec, r = a.next_r;
   double inv_pf = 0.0;                                   // Welford weight, one record ahead
-  if (accum) inv_pf = a.inv_n[r - a.next_r0];
+  if (accum) inv_pf = welford_weight(a, r - a.next_r0);
   auto record = [&](int64_t R) {
     const int64_t s = R - a.rec_base;
     if ((a.flags & RUNF_RECORD_X) && active) {
@@ -184,7 +184,7 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
     }
     if (accum) {
       const double inv = inv_pf;
-      inv_pf = a.inv_n[R + 1 - a.next_r0];
+      inv_pf = welford_weight(a, R + 1 - a.next_r0);
 #pragma unroll
       for (int kb = 0; kb < NL; ++kb) {
         const double delta = x[kb] - rmean[kb];

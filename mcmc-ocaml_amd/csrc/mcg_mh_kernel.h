@@ -234,6 +234,15 @@ __device__ __forceinline__ bool mix_has_kd(const double* __restrict__ q, int str
   return kd;
 }
 
+// The Welford weight 1/(R+1) of record R (host IEEE division, MhArgs::inv_n): R is the same for
+// every lane, so this is a scalar load (lgkmcnt).  As a vector load, the step that copied it into
+// the next record's weight register waited with vmcnt(0), which also drained every load issued
+// ahead (the kD proposal's leaf and box prefetches: C4 stalled there once per step).
+__device__ __forceinline__ double welford_weight(const MhArgs& a, int64_t idx) {
+  typedef const __attribute__((address_space(4))) double kdouble;
+  return ((kdouble*)a.inv_n)[idx];
+}
+
 // Q: a generic pointer, or (the MH kernel's per-step evaluation) a constant-address-space one,
 // whose uniform loads become scalar loads (the scalar cache and lgkmcnt, not vmcnt: a per-step
 // vector load of the constants waited with vmcnt(0) and drained every load issued ahead)
@@ -424,7 +433,9 @@ template <int D, int P, int LIK, int PROP>
 struct MhShape {
   static constexpr bool kThree = separable<LIK, PROP>() && Layout<D, P, lane_width<D, P, PROP>()>::NL <= 8;
   static constexpr bool kPipe = kThree;
-  static constexpr int kWaves = kThree ? 3 : 1;
+  // (one lane per chain, D <= 8: the whole chain per lane does not fit 168 registers; those
+  // instances are built for the two waves per SIMD they reach)
+  static constexpr int kWaves = kThree ? (P > 1 ? 3 : 2) : 1;
   static constexpr int kBlock = 256;
   static constexpr bool kBatchNormals = !kThree;
   // harmonic-mean partials in LDS only where that was measured (C2: P = 4, three waves); a P = 1
@@ -556,7 +567,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
   // the Welford weight of the next record is loaded one record ahead: loaded where it is used,
   // its L2 latency sat exposed in every step (the table holds one entry past rec_end)
   double inv_pf = 0.0;
-  if (accum) inv_pf = a.inv_n[r - a.next_r0];
+  if (accum) inv_pf = welford_weight(a, r - a.next_r0);
   auto record = [&](int64_t R) {
     int64_t s = R - a.rec_base;
     if ((a.flags & RUNF_RECORD_X) && active) {
@@ -577,7 +588,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
     }
     if (accum) {
       const double inv = inv_pf;                      // 1/(R+1), host IEEE division
-      inv_pf = a.inv_n[R + 1 - a.next_r0];
+      inv_pf = welford_weight(a, R + 1 - a.next_r0);
 #pragma unroll
       for (int i = 0; i < L::NCL; ++i)
 #pragma unroll

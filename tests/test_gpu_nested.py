@@ -233,6 +233,21 @@ def test_nested_walker_lane_splits_bit_exact(oracle, T, monkeypatch, lanes, D, d
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("D,lanes,nmcmc", [(16, None, 45), (16, None, 100), (32, "narrow", 45)])
+def test_nested_walker_long_walks_bit_exact(oracle, T, monkeypatch, D, lanes, nmcmc):
+    """The shell walker on 4 lanes over long walks (the draw table's prefetch groups wrap many
+    times; a step count that is not a multiple of the walker's group of 4): the oracle's dead
+    points bit for bit."""
+    if lanes:
+        monkeypatch.setenv("MCG_NEST_LANES", lanes)
+    lik = T.gauss_shell(np.zeros(D), 1.0, 0.2)
+    pri = T.box(-2 * np.ones(D), 2 * np.ones(D))
+    g = gpu_nested(lik, pri, 21, nlive=500, nmcmc=nmcmc, mode_hopping_frac=0.1, k=64, max_dead=64 * 12)
+    o = oracle_nested(oracle, lik, pri, 21, nlive=500, nmcmc=nmcmc, mode_hop=0.1, k=64, max_iter=64 * 12)
+    assert_nested_same(g, o)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("D,sym,diag", [(16, False, False), (16, False, True), (16, True, True)])
 def test_nested_walker_box_forms_bit_exact(oracle, T, D, sym, diag):
     """The walker's two box tests: a box symmetric in every dim is tested as |y| <= h (one
