@@ -549,7 +549,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
     }
   }
   // fold the parked record of the group starting at record R0 (R0 % P == 0)
-  auto hm_flush = [&](int64_t R0) {
+  auto hm_flush = [&](int64_t R0) __attribute__((always_inline)) {
     const int li = (int)((R0 & 7) / P);
     if (hm_pok) {
       if constexpr (kHmLds) {
@@ -568,7 +568,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
   // its L2 latency sat exposed in every step (the table holds one entry past rec_end)
   double inv_pf = 0.0;
   if (accum) inv_pf = welford_weight(a, r - a.next_r0);
-  auto record = [&](int64_t R) {
+  auto record = [&](int64_t R) __attribute__((always_inline)) {
     int64_t s = R - a.rec_base;
     if ((a.flags & RUNF_RECORD_X) && active) {
       // opaque row pitch: left visible, the compiler hoists the per-dim record addresses out of
@@ -663,25 +663,27 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
       }
   }
   // kD independence proposal: a step's draw depends on the RNG only (the picked training point's
-  // leaf, its box, a uniform point in it), so the leaf of step t + 2 and the box and log q of
-  // step t + 1 are loaded while step t computes (a dependent leaf -> box load chain per step
-  // otherwise sits on every step's path).  The same values as loading them in the step.
+  // leaf, its box, a uniform point in it), so they are loaded ahead: KDA = 1, the leaf of step
+  // t + 2 and the box and log q of step t + 1 while step t computes; KDA = 2 (the step loop
+  // unrolled by two, one register slot per step parity), the leaf of step t + 4 and the box of
+  // step t + 2.  The same values as loading them in the step.
   // (P > 1: lane `sub` holds the box bounds of its own dims, local slot j at kd_lo[j], kd_hi[j])
   constexpr int KDN = PROP == MCG_PROP_KD_INTERP ? L::NL : 1;
-  int kd_leaf = 0, kd_leaf_n = 0;
-  double kd_lo[KDN], kd_hi[KDN];
-  double kd_lqp = 0.0;
-  auto kd_pick = [&](uint64_t Tp) -> uint32_t {
+  constexpr int KDA = PROP == MCG_PROP_KD_INTERP ? 2 : 1;
+  int kd_leaf_n[KDA];
+  double kd_lo[KDA][KDN], kd_hi[KDA][KDN];
+  double kd_lqp[KDA];
+  auto kd_pick = [&](uint64_t Tp) __attribute__((always_inline)) -> uint32_t {
     const u32x4 w = rng(gid, (uint32_t)Tp, CALL_KD_PICK, TAG_MH, (uint32_t)(Tp >> 32));
     return randint(w.x, w.y, (uint32_t)a.kd_M);
   };
-  auto kd_pick_leaf = [&](uint64_t Tp) -> int { return a.kd_pt_leaf[kd_pick(Tp)]; };
+  auto kd_pick_leaf = [&](uint64_t Tp) __attribute__((always_inline)) -> int { return a.kd_pt_leaf[kd_pick(Tp)]; };
   // P > 1: the picks are staggered over the chain's lanes like the accept uniforms: at the first
-  // step t of each group of P steps, lane `sub` draws the pick of step t + 2 + sub, and step
-  // t + q (which prefetches the leaf of step t + q + 2) takes it from lane q -- one pick per P
-  // lane-steps instead of one per lane-step
+  // step t of each group of P steps, lane `sub` draws the pick of step t + 2 KDA + sub, and step
+  // t + q (which prefetches the leaf of step t + q + 2 KDA) takes it from lane q -- one pick per
+  // P lane-steps instead of one per lane-step
   uint32_t pick_own = 0;
-  auto bcast_u32 = [&](uint32_t v, int q) -> uint32_t {
+  auto bcast_u32 = [&](uint32_t v, int q) __attribute__((always_inline)) -> uint32_t {
     if constexpr (P == 4) {
       return q == 0 ? quad_bcast_u32<0>(v) : q == 1 ? quad_bcast_u32<1>(v) : q == 2 ? quad_bcast_u32<2>(v)
                                                                                   : quad_bcast_u32<3>(v);
@@ -689,22 +691,23 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
       return (uint32_t)__shfl((int)v, (lane & ~(P - 1)) | q, 64);
     }
   };
-  auto kd_load_box = [&](int leaf) {
+  auto kd_load_box = [&](int leaf, auto slot_c) __attribute__((always_inline)) {
+    constexpr int sl = decltype(slot_c)::value;
     const double* __restrict__ bx = a.kd_box + (int64_t)leaf * 2 * D;
 #pragma unroll
     for (int i = 0; i < (PROP == MCG_PROP_KD_INTERP ? L::NCL : 0); ++i)
 #pragma unroll
       for (int k = 0; k < kW; ++k) {
         const int d = L::valid(sub, i, k) ? L::dim(sub, i, k) : 0;
-        kd_lo[kW * i + k] = bx[d];
-        kd_hi[kW * i + k] = bx[D + d];
+        kd_lo[sl][kW * i + k] = bx[d];
+        kd_hi[sl][kW * i + k] = bx[D + d];
       }
-    kd_lqp = a.kd_logq[leaf];
+    kd_lqp[sl] = a.kd_logq[leaf];
   };
   // the uniforms of a step's box draw (dims 2c and 2c + 1 from call c; the lane's own blocks),
   // drawn one step ahead
   double kd_u[KDN];
-  auto kd_uniforms = [&](uint64_t Tu) {
+  auto kd_uniforms = [&](uint64_t Tu) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < (PROP == MCG_PROP_KD_INTERP ? L::NCL : 0); ++i)
 #pragma unroll
@@ -718,15 +721,20 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
   };
   if constexpr (PROP == MCG_PROP_KD_INTERP) {
     if (a.nsteps > 0) {
-      kd_leaf = kd_pick_leaf(a.step_base);
-      kd_load_box(kd_leaf);
-      kd_leaf_n = kd_pick_leaf(a.step_base + 1);
+      kd_load_box(kd_pick_leaf(a.step_base), std::integral_constant<int, 0>{});
+      if constexpr (KDA == 2) {
+        kd_load_box(kd_pick_leaf(a.step_base + 1), std::integral_constant<int, 1>{});
+        kd_leaf_n[0] = kd_pick_leaf(a.step_base + 2);
+        kd_leaf_n[1] = kd_pick_leaf(a.step_base + 3);
+      } else {
+        kd_leaf_n[0] = kd_pick_leaf(a.step_base + 1);
+      }
     }
   }
   // log u of step t (mcmc.ml:49).  P > 1: staggered accept uniforms -- at the first step of each
   // group of P steps, lane `sub` of the chain draws log u for step t + sub; step t + q reads it
   // from lane q (one DPP broadcast, or a shuffle at P = 8)
-  auto accept_lu = [&](int64_t t, uint64_t T) -> double {
+  auto accept_lu = [&](int64_t t, uint64_t T) __attribute__((always_inline)) -> double {
     if constexpr (P == 1) {
       const u32x4 wa = rng(gid, (uint32_t)T, CALL_ACCEPT, TAG_MH, (uint32_t)(T >> 32));
       return plog(u53(wa.x, wa.y), s_lt);
@@ -747,7 +755,9 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
       }
     }
   };
-  for (int64_t t = 0; t < a.nsteps; ++t) {
+  // one MH step (mcmc.ml:37-56); par: the step's parity, a compile-time slot of the kD prefetch
+  auto mh_step = [&](int64_t t, auto par_c) __attribute__((always_inline)) {
+    constexpr int par = decltype(par_c)::value;
     const uint64_t T = a.step_base + (uint64_t)t;
     const uint32_t tlo = (uint32_t)T, thi = (uint32_t)(T >> 32);
     double lf = 0.0, lb = 0.0, lqy = 0.0;
@@ -788,7 +798,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
         philox_multi<L::NCL, true>(wl, gid, tlo, cidx, (TAG_MH << 16) | (thi & 0xFFFFu), rng.k0, rng.k1);
       }
       // the coordinates and terms of call i from its four normals
-      auto dims1 = [&](const int i, const int k, const double zk) {
+      auto dims1 = [&](const int i, const int k, const double zk) __attribute__((always_inline)) {
         const int cc = sub + P * i;
         if (!L::valid(sub, i, k)) return;
         const int d = 4 * cc + k;
@@ -813,7 +823,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
           ok = ok & (yv >= lo) & (yv <= hi);
         }
       };
-      auto dims = [&](const int i, const double* z) {
+      auto dims = [&](const int i, const double* z) __attribute__((always_inline)) {
         const int cc = sub + P * i;
 #pragma unroll
         for (int k = 0; k < kW; ++k) {
@@ -847,7 +857,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
       if constexpr (MhShape<D, P, LIK, PROP>::kPipe) {
         // one normal at a time with its table rows gathered one normal ahead: the gathers of
         // normal m + 1 are in flight while normal m is finished and its dim's terms computed
-        auto word = [&](int m) -> uint32_t {
+        auto word = [&](int m) __attribute__((always_inline)) -> uint32_t {
           const u32x4 w = wl[m >> 2];
           const int k = m & 3;
           return k == 0 ? w.x : k == 1 ? w.y : k == 2 ? w.z : w.w;
@@ -921,16 +931,18 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
         // Interpolate_pdf.draw (interpolate_pdf.ml:114-119) from the leaf and box loaded ahead;
         // dims 2c and 2c + 1 from call c (lane `sub`: the calls of its 4-dim blocks)
         kd_uniforms(T);
+        const double* klo = kd_lo[par];
+        const double* khi = kd_hi[par];
         bool strict = true;
 #pragma unroll
         for (int j = 0; j < L::NL; ++j) {
           if (!L::valid(sub, j >> 2, j & 3)) continue;
-          y[j] = kd_lo[j] + (kd_hi[j] - kd_lo[j]) * kd_u[j];
-          strict = strict && (y[j] > kd_lo[j]) && (y[j] < kd_hi[j]);
+          y[j] = klo[j] + (khi[j] - klo[j]) * kd_u[j];
+          strict = strict && (y[j] > klo[j]) && (y[j] < khi[j]);
         }
         if constexpr (P > 1) strict = and_lanes<P>(strict ? 1 : 0) != 0;
         // strictly inside its leaf box: that leaf (see below), whose log q came with the box
-        lqy = kd_lqp;
+        lqy = kd_lqp[par];
         if (!strict) {
           if constexpr (P == 1) {
             lqy = a.kd_logq[kd_find_leaf<D>(a.kd_nodes, a.kd_root, y)];
@@ -950,14 +962,13 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
         // the next step's box and log q go out now (its leaf arrived during this step), and
         // the leaf of the step after it: their latency hides behind this step's likelihood,
         // accept and records and the next step's uniforms
-        kd_leaf = kd_leaf_n;
-        kd_load_box(kd_leaf);
+        kd_load_box(kd_leaf_n[par], std::integral_constant<int, par>{});
         if constexpr (P == 1) {
-          kd_leaf_n = kd_pick_leaf(T + 2);
+          kd_leaf_n[par] = kd_pick_leaf(T + 2 * KDA);
         } else {
           const int qk = (int)(t & (P - 1));
-          if (qk == 0) pick_own = kd_pick(T + 2 + (uint64_t)sub);
-          kd_leaf_n = a.kd_pt_leaf[bcast_u32(pick_own, qk)];
+          if (qk == 0) pick_own = kd_pick(T + 2 * KDA + (uint64_t)sub);
+          kd_leaf_n[par] = a.kd_pt_leaf[bcast_u32(pick_own, qk)];
         }
         lf = lqy;   // log_jump_prob start proposed = log q(proposed)
         lb = lq;    // log_jump_prob proposed start = log q(start)
@@ -1141,6 +1152,16 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
       ++r;
       next_rec += a.nskip;
     }
+  };
+  if constexpr (KDA == 2) {
+    int64_t t = 0;
+    for (; t + 1 < a.nsteps; t += 2) {
+      mh_step(t, std::integral_constant<int, 0>{});
+      mh_step(t + 1, std::integral_constant<int, 1>{});
+    }
+    if (t < a.nsteps) mh_step(t, std::integral_constant<int, 0>{});
+  } else {
+    for (int64_t t = 0; t < a.nsteps; ++t) mh_step(t, std::integral_constant<int, 0>{});
   }
 
   if (!active) return;
