@@ -365,15 +365,18 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   a.newk_tie = B.newk.t();
   a.newk_slot = B.newk.s();
   a.rank = (int*)B.rank.p;
-  a.est_in_rank = k <= 4096 ? 1 : 0;                  // the counted-rank sort path
+  // k <= 8192: retirement in the walk and the sort + merge in one launch, whose extra workgroup
+  // folds the estimate; MCG_NESTED_MERGE2=1 keeps the counted-rank sort (k <= 4096, the estimate
+  // in its extra workgroup) and the merge as two launches; beyond, the retire kernel folds it
+  const bool merge2 = std::getenv("MCG_NESTED_MERGE2") != nullptr;
+  const bool retire_kernel = std::getenv("MCG_NESTED_RETIRE_KERNEL") != nullptr;
+  const bool fused_merge = !merge2 && !retire_kernel && k <= 8192;
+  a.est_in_rank = (fused_merge || k <= 4096) ? 1 : 0;
   // MCG_NEST_LANES: lanes per walker (8 for D % 32 == 0; 4 at D = 8, 8 at D = 16: two dims per
   // lane), "wide" for that wider split, "narrow" for the one-block-per-call split
   if (const char* e = std::getenv("MCG_NEST_LANES"))
     a.lanes_hint = !std::strcmp(e, "wide") ? -1 : !std::strcmp(e, "narrow") ? -2 : std::atoi(e);
-  a.fuse_retire = a.est_in_rank && std::getenv("MCG_NESTED_RETIRE_KERNEL") == nullptr;
-  // k <= 4096 (retire in the walk): sort + merge in one launch; MCG_NESTED_MERGE2=1 keeps the
-  // counted-rank sort and the merge as two launches
-  const bool fused_merge = a.fuse_retire && std::getenv("MCG_NESTED_MERGE2") == nullptr;
+  a.fuse_retire = a.est_in_rank && !retire_kernel;
   // the walkers' draws of a generation in a table the previous merge fills (when it fits)
   a.rt_ix = nullptr;
   a.rt_sc = nullptr;

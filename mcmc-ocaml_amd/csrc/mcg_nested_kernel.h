@@ -78,6 +78,7 @@ struct NestArgs {
                             // put the new points into the freed slots
   int32_t sym_box;          // box prior with lo[d] == -hi[d] for every d: tested as |y| <= hi
   int32_t lanes_hint;       // lanes per walker requested by MCG_NEST_LANES (0: the default)
+  int32_t walk_waves;       // walker waves per draw-table workgroup (1, or 2 beyond 256 waves)
   uint32_t row_bytes;       // D * 8: the draw table holds DE pairs as row byte offsets
   double* tv;               // ll + log dv of this generation's dead points (padded pow2)
   const double* prefix;     // [k+1] sum_{j'<j} log1p(-1/(n-j'))
@@ -429,8 +430,13 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   const bool stopped0 = nest_stopped(a.st);
   const double st_lv = a.st->log_vol, st_mx = a.st->max_ll, st_est = a.st->est;
   const bool st_err = __hip_atomic_load(&a.st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-  const bool walker = !TAB || threadIdx.x < 64;       // wave-uniform
-  const int64_t tid = (int64_t)blockIdx.x * (TAB ? 64 : blockDim.x) + threadIdx.x;
+  // with the draw table a 256-thread workgroup holds ww walker waves (waves 0 .. ww-1, one SIMD
+  // each) and 4 - ww table-filling waves: one walker wave per SIMD of the chip up to 1,024
+  // walker waves (k P <= 65,536 lanes; ww = 2 from 256 walker waves on)
+  const int ww = TAB ? a.walk_waves : 1;
+  const int wl = 64 * ww;                              // walker lanes per workgroup
+  const bool walker = !TAB || (int)threadIdx.x < wl;   // wave-uniform
+  const int64_t tid = (int64_t)blockIdx.x * (TAB ? wl : blockDim.x) + threadIdx.x;
   const int sub = (int)(tid & (P - 1));
   const int64_t w = tid / P;
   const bool active = w < a.k;
@@ -506,13 +512,13 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   if constexpr (TAB) {
     // waves 1-3 of the workgroup (one SIMD each; the walkers are wave 0) draw the next
     // generation's table and leave
-    if (threadIdx.x >= 64) {
-      const int64_t nf = blockDim.x - 64;
+    if ((int)threadIdx.x >= wl) {
+      const int64_t nf = blockDim.x - wl;
       if (a.fuse_retire) {
         // retire the dead points of this workgroup's walkers (see below): element e of the
-        // (64 / P) x D block, the scalars with d == 0
-        const int64_t w0 = (int64_t)blockIdx.x * (64 / P);
-        for (int64_t e = threadIdx.x - 64; e < (64 / P) * D; e += nf) {
+        // (wl / P) x D block, the scalars with d == 0
+        const int64_t w0 = (int64_t)blockIdx.x * (wl / P);
+        for (int64_t e = threadIdx.x - wl; e < (wl / P) * D; e += nf) {
           const int64_t wj = w0 + e / D;
           const int d = (int)(e % D);
           if (wj >= a.k) break;
@@ -529,9 +535,9 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
           }
         }
       }
-      walk_draws_fill<!WalkTarget<D, P, LIK, SYM>::kFold>(a, a.mrep + a.k, (int64_t)blockIdx.x * nf + (threadIdx.x - 64), (int64_t)gridDim.x * nf, lt);
+      walk_draws_fill<!WalkTarget<D, P, LIK, SYM>::kFold>(a, a.mrep + a.k, (int64_t)blockIdx.x * nf + (threadIdx.x - wl), (int64_t)gridDim.x * nf, lt);
 #ifdef MCG_NEST_TRACE
-      if (a.trace && threadIdx.x == 64 && blockIdx.x < 1024)   // the table-filling waves' end
+      if (a.trace && (int)threadIdx.x == wl && blockIdx.x < 1024)   // the table-filling waves' end
         a.trace[((size_t)0 * 1024 + blockIdx.x) * 8 + 5] = wall_clock64();
 #endif
       return;
@@ -855,10 +861,14 @@ hipError_t launch_nest_walk_p(const NestArgs& a, hipStream_t st) {
   const int block = kNestWalkBlock;
   const int64_t grid = (a.k * P + block - 1) / block;
   // with the draw table: the same walker waves, each with three table-filling waves beside it
-  const dim3 gt((unsigned)((a.k * P + 63) / 64)), bt(256);
+  // (two walker waves and two filling waves per workgroup beyond 256 walker waves)
+  NestArgs b = a;
+  const int64_t wwaves = (a.k * P + 63) / 64;
+  b.walk_waves = wwaves > 256 ? 2 : 1;
+  const dim3 gt((unsigned)((wwaves + b.walk_waves - 1) / b.walk_waves)), bt(256);
   constexpr bool kSym = WalkTarget<D, P, LIK>::kReg;   // the |y| <= h form needs the register target
-  if (a.rt_ix && kSym && a.sym_box) hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, kSym>), gt, bt, 0, st, a);
-  else if (a.rt_ix) hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, false>), gt, bt, 0, st, a);
+  if (b.rt_ix && kSym && b.sym_box) hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, kSym>), gt, bt, 0, st, b);
+  else if (b.rt_ix) hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, false>), gt, bt, 0, st, b);
   else hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, false, false>), dim3((unsigned)grid), dim3(block), 0, st, a);
   return hipGetLastError();
 }

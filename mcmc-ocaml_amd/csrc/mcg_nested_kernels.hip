@@ -518,18 +518,19 @@ __global__ void __launch_bounds__(256) merge_new_kernel(const NestArgs a, double
 // No sorted new-key array, no hand-off between workgroups: the old rank count -> merge pair
 // (two launches, 11.5 + 11.1 us at C3) becomes one launch.  An extra workgroup folds the running
 // estimate; every merge workgroup then takes a share of the new points' slot writes.
-constexpr int kSubCap = kSmallSort;
-#ifndef MCG_MERGE_BS
-#define MCG_MERGE_BS 256
-#endif
-constexpr int kMergeBS = MCG_MERGE_BS;
 #ifndef MCG_MERGE_UNROLL
 #define MCG_MERGE_UNROLL 16
 #endif
+constexpr int kFusedMax = 2 * kSmallSort;                // the largest k of the one-launch merge
 
-template <int BS>   // workgroup size = survivors per workgroup
+// BS: workgroup size = survivors per workgroup; KCAP: the largest k (new keys per thread
+// KCAP / BS, the block's subset staged in LDS up to KCAP keys).  k <= 4096: <256, 4096>; up to
+// 8192: <512, 8192> (98 KB of LDS, one workgroup per CU: 512 survivors a workgroup keep the
+// grid to one round on the 256 CUs)
+template <int BS, int KCAP>
 __global__ void __launch_bounds__(BS) merge_fused_kernel(const NestArgs a, double* oll, long long* otie,
                                                          int* oslot) {
+  constexpr int kSubCap = KCAP;
   NT_STAMP(3, 0);
   if (nest_stopped(a.st)) return;                         // grid-uniform: set by an earlier launch
   const int64_t n = a.n, k = a.k, ns = n - k;
@@ -585,7 +586,7 @@ __global__ void __launch_bounds__(BS) merge_fused_kernel(const NestArgs a, doubl
   const bool has_hi = i0 + BS < ns;
   const double hi_l = has_hi ? sll[i0 + BS] : 0.0;
   const long long hi_t = has_hi ? stie[i0 + BS] : 0;
-  constexpr int kPer = kSmallSort / BS;
+  constexpr int kPer = KCAP / BS;
   double nv[kPer];
 #pragma unroll
   for (int r = 0; r < kPer; ++r) {
@@ -719,21 +720,14 @@ __global__ void __launch_bounds__(BS) merge_fused_kernel(const NestArgs a, doubl
 }
 
 hipError_t launch_merge_fused(const NestArgs& a, double* oll, long long* otie, int* oslot, hipStream_t s) {
-  if (a.k > kSmallSort || a.k < 1 || !a.est_in_rank) return hipErrorInvalidValue;
-  // survivors per workgroup (MCG_NESTED_MERGE_BS): every workgroup stages and classifies all k
-  // new keys, so fewer, wider workgroups divide that work over more threads
-  static const int bs = [] {
-    const char* e = std::getenv("MCG_NESTED_MERGE_BS");
-    const int v = e ? std::atoi(e) : kMergeBS;
-    return (v == 256 || v == 512 || v == 1024) ? v : kMergeBS;
-  }();
-  const unsigned nblk = (unsigned)((a.n - a.k + bs - 1) / bs);
-  if (bs == 1024)
-    hipLaunchKernelGGL(merge_fused_kernel<1024>, dim3(nblk + 1), dim3(1024), 0, s, a, oll, otie, oslot);
-  else if (bs == 512)
-    hipLaunchKernelGGL(merge_fused_kernel<512>, dim3(nblk + 1), dim3(512), 0, s, a, oll, otie, oslot);
-  else
-    hipLaunchKernelGGL(merge_fused_kernel<256>, dim3(nblk + 1), dim3(256), 0, s, a, oll, otie, oslot);
+  if (a.k > kFusedMax || a.k < 1 || !a.est_in_rank) return hipErrorInvalidValue;
+  if (a.k <= kSmallSort) {
+    const unsigned nblk = (unsigned)((a.n - a.k + 255) / 256);
+    hipLaunchKernelGGL((merge_fused_kernel<256, kSmallSort>), dim3(nblk + 1), dim3(256), 0, s, a, oll, otie, oslot);
+  } else {
+    const unsigned nblk = (unsigned)((a.n - a.k + 511) / 512);
+    hipLaunchKernelGGL((merge_fused_kernel<512, kFusedMax>), dim3(nblk + 1), dim3(512), 0, s, a, oll, otie, oslot);
+  }
   return hipGetLastError();
 }
 
