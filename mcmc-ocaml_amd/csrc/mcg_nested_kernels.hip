@@ -399,10 +399,7 @@ __device__ __forceinline__ int64_t count_less_2l(const double* ll, const long lo
 
 // the new keys' sample: every 4th key (k <= 4096), so a survivor's search ends with two
 // dependent global probes instead of four
-#ifndef MCG_MERGE_NEW_SAMPLE
-#define MCG_MERGE_NEW_SAMPLE 1024
-#endif
-constexpr int kSampNew = MCG_MERGE_NEW_SAMPLE, kSampSurv = 2048;
+constexpr int kSampNew = 1024, kSampSurv = 2048;
 constexpr int64_t kSampNewMin = kSampNew >= 1024 ? 4 : 16;
 
 // survivors keys[k..n) + k sorted new keys -> out[0..n) by rank scatter; the thread placing the
@@ -518,9 +515,6 @@ __global__ void __launch_bounds__(256) merge_new_kernel(const NestArgs a, double
 // No sorted new-key array, no hand-off between workgroups: the old rank count -> merge pair
 // (two launches, 11.5 + 11.1 us at C3) becomes one launch.  An extra workgroup folds the running
 // estimate; every merge workgroup then takes a share of the new points' slot writes.
-#ifndef MCG_MERGE_UNROLL
-#define MCG_MERGE_UNROLL 16
-#endif
 constexpr int kFusedMax = 2 * kSmallSort;                // the largest k of the one-launch merge
 
 // BS: workgroup size = survivors per workgroup; KCAP: the largest k (new keys per thread
@@ -618,7 +612,7 @@ __global__ void __launch_bounds__(BS) merge_fused_kernel(const NestArgs a, doubl
   // order).  The subset order does not matter: it is ranked by counting below.
   uint32_t inmask = 0;
   int wsub = 0, wbelow = 0;                               // wave-uniform
-#pragma unroll MCG_MERGE_UNROLL
+#pragma unroll 16
   for (int r = 0; r < kPer; ++r) {
     const int64_t j = (int64_t)r * BS + t;
     const bool ok = j < k;
@@ -650,7 +644,7 @@ __global__ void __launch_bounds__(BS) merge_fused_kernel(const NestArgs a, doubl
     m += s_scan[w2];
     c_lo += s_scan[NW + w2];
   }
-#pragma unroll MCG_MERGE_UNROLL
+#pragma unroll 16
   for (int r = 0; r < kPer; ++r) {
     const bool in = (inmask >> r) & 1u;
     const unsigned long long bm = __ballot(in);
