@@ -275,7 +275,7 @@ def c5(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("configs", nargs="*", default=["c1", "c3", "c4", "c5"])
+    ap.add_argument("configs", nargs="*", default=["c1", "c3", "c3k8", "c4", "c5"])
     ap.add_argument("--out", default=None)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--nlive", type=int, default=131072)
@@ -286,7 +286,13 @@ def main():
     ap.add_argument("--reps", type=int, default=5, help="C3: timed nested runs after a warm-up run (median reported)")
     ap.add_argument("--c5-chains", type=int, default=131072)
     args = ap.parse_args()
-    fns = {"c1": c1, "c2": c2, "c3": c3, "c4": c4, "c5": c5}
+    def c3k8(a):
+        """C3 with 8,192 retirements a generation (two walker waves per draw-table workgroup)."""
+        b = argparse.Namespace(**vars(a))
+        b.k = 8192
+        return c3(b)
+
+    fns = {"c1": c1, "c2": c2, "c3": c3, "c3k8": c3k8, "c4": c4, "c5": c5}
     for c in args.configs:
         line = fns[c](args)
         s = json.dumps(line)
