@@ -204,6 +204,10 @@ def main():
     ctx.set_timing(True)
     if dist:      # the communicator is created by its first collective: not inside the timed region
         tdist.all_reduce(torch.zeros(1, dtype=torch.float64, device=comm))
+    if comm is not None:
+        # the first all_gather_into_tensor of a process sets RCCL's gather path up (~1 ms at N = 1):
+        # one untimed pass of the same end-of-run reduction, on the burn-in state
+        reduce_stats_device(ctx, comm)
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
