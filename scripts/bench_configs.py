@@ -275,7 +275,7 @@ def c5(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("configs", nargs="*", default=["c1", "c3", "c3k8", "c4", "c5"])
+    ap.add_argument("configs", nargs="*", default=["c1", "c3", "c3k8", "c3n1k", "c4", "c5"])
     ap.add_argument("--out", default=None)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--nlive", type=int, default=131072)
@@ -292,7 +292,13 @@ def main():
         b.k = 8192
         return c3(b)
 
-    fns = {"c1": c1, "c2": c2, "c3": c3, "c3k8": c3k8, "c4": c4, "c5": c5}
+    def c3n1k(a):
+        """C3 at nested_evidence's own default walk length, nmcmc 1,000 (nested.ml:122)."""
+        b = argparse.Namespace(**vars(a))
+        b.nmcmc = 1000
+        return c3(b)
+
+    fns = {"c1": c1, "c2": c2, "c3": c3, "c3k8": c3k8, "c3n1k": c3n1k, "c4": c4, "c5": c5}
     for c in args.configs:
         line = fns[c](args)
         s = json.dumps(line)
