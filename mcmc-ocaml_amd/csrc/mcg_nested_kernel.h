@@ -560,7 +560,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   if (start < 0) start = a.key_slot[a.k - 1];
   NT_STAMP(0, 2);
   double cur[NL], y[NL];
-  auto load_row_at = [&](double* dst, const double* __restrict__ src) {
+  auto load_row_at = [&](double* dst, const double* __restrict__ src) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < Lay::NCL; ++i)
 #pragma unroll
@@ -572,7 +572,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   // VGPR (global_load ... saddr) and one 32-bit add per row
   const char* const xb = (const char*)a.x;
   const uint32_t lane_b = 8u * W * (uint32_t)sub;
-  auto load_row_off = [&](double* dst, uint32_t v) {
+  auto load_row_off = [&](double* dst, uint32_t v) __attribute__((always_inline)) {
     const char* src = xb + (v + lane_b);
 #pragma unroll
     for (int i = 0; i < Lay::NCL; ++i)
@@ -580,11 +580,11 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
       for (int q = 0; q < W; ++q)
         dst[W * i + q] = Lay::valid(sub, i, q) ? *(const double*)(src + 8 * (W * P * i + q)) : 0.0;
   };
-  auto refill = [&](double* dst, uint32_t v) {
+  auto refill = [&](double* dst, uint32_t v) __attribute__((always_inline)) {
     if constexpr (TAB) load_row_off(dst, v);
     else load_row_at(dst, a.x + (int64_t)v * D);
   };
-  auto load_row = [&](double* dst, int64_t row) {
+  auto load_row = [&](double* dst, int64_t row) __attribute__((always_inline)) {
     const double* __restrict__ src = a.x + row * D;
 #pragma unroll
     for (int i = 0; i < Lay::NCL; ++i)
@@ -593,7 +593,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
         dst[W * i + q] = Lay::valid(sub, i, q) ? src[Lay::dim(sub, i, q)] : 0.0;
   };
   // differential_evolution_proposal's pick_samples (mcmc.ml:199-203): i, then j != i
-  auto pick = [&](int64_t s, uint32_t& i, uint32_t& j) {
+  auto pick = [&](int64_t s, uint32_t& i, uint32_t& j) __attribute__((always_inline)) {
     const u32x4 ri = rng(wid, (uint32_t)s, CALL_DE_IDX, TAG_NEST_WALK, 0u);
     i = randint(ri.x, ri.y, n);
     const uint32_t jj = randint(ri.z, ri.w, n - 1);
@@ -619,7 +619,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
     double hop[PD / 4 > 0 ? PD / 4 : 1], lu[PD / 4 > 0 ? PD / 4 : 1];
     NrmPending z[PD / 4 > 0 ? PD / 4 : 1];
   };
-  auto group_issue = [&](int64_t s0, GroupRng& G) {
+  auto group_issue = [&](int64_t s0, GroupRng& G) __attribute__((always_inline)) {
     if constexpr (P == 4 && PD % 4 == 0) {
 #pragma unroll
       for (int h = 0; h < PD / 4; ++h) {
@@ -688,7 +688,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   NT_STAMP(0, 3);
   // two copies of the loop: with the box test, and without it once the constraint implies it
   // (setup_constraint: box_test is wave-uniform)
-  auto walk_loop = [&](auto box_t) {
+  auto walk_loop = [&](auto box_t) __attribute__((always_inline)) {
   constexpr bool kBoxT = decltype(box_t)::value;
   for (int s0 = 0; s0 < nm; s0 += PD) {
     double dsc_g[PD], lu_g[PD];
