@@ -246,11 +246,12 @@ def test_nested_large_k_one_launch_merge_bit_exact(oracle, T, D, nlive, k):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("D,lanes,nmcmc", [(16, None, 45), (16, None, 100), (32, "narrow", 45)])
+@pytest.mark.parametrize("D,lanes,nmcmc", [(16, None, 45), (16, None, 100), (16, None, 1000), (32, "narrow", 45)])
 def test_nested_walker_long_walks_bit_exact(oracle, T, monkeypatch, D, lanes, nmcmc):
     """The shell walker on 4 lanes over long walks (the draw table's prefetch groups wrap many
-    times; a step count that is not a multiple of the walker's group of 4): the oracle's dead
-    points bit for bit."""
+    times; a step count that is not a multiple of the walker's group of 4; nested_evidence's
+    default nmcmc = 1,000, nested.ml:122, as in the c3n1k config line): the oracle's dead points
+    bit for bit."""
     if lanes:
         monkeypatch.setenv("MCG_NEST_LANES", lanes)
     lik = T.gauss_shell(np.zeros(D), 1.0, 0.2)
