@@ -617,13 +617,20 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
       if (inflight[q ^ 1]) (void)hipEventSynchronize(B.done[q ^ 1]);
       return set_error(ctx, MCG_EFAIL, "Error in draw_new_live_point: new log(L) below the threshold");
     }
-    // the fold worker must be done with R.ll / R.wts before they grow
-    const auto tf = now();
-    if (fw.joinable()) fw.join();
-    t_fold += ms(tf, now());
-    // this batch's dead points: generations [gstart[q], st.gen_done) of the ones it launched
+    auto join_fold = [&] {
+      const auto tf = now();
+      if (fw.joinable()) fw.join();
+      t_fold += ms(tf, now());
+    };
+    // this batch's dead points: generations [gstart[q], st.gen_done) of the ones it launched.
+    // The fold worker reads R.ll through a pointer taken when it started, so R.ll may grow under
+    // it only within its capacity (the worker is joined first when it must reallocate)
     const int64_t d0 = gstart[q] * k, d1 = st.gen_done * k;
     if (d1 > d0) {
+      if (R.ll.capacity() < R.ll.size() + (size_t)(d1 - d0)) {
+        join_fold();
+        R.ll.reserve(std::max(2 * R.ll.capacity(), R.ll.size() + (size_t)(d1 - d0) + (size_t)(kMaxBatch * k)));
+      }
       R.ll.insert(R.ll.end(), B.h_stage[2 * q], B.h_stage[2 * q] + (d1 - d0));
       R.lp.insert(R.lp.end(), B.h_stage[2 * q + 1], B.h_stage[2 * q + 1] + (d1 - d0));
     }
@@ -649,6 +656,9 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
       reported = ndead;
     }
     retired_dead.release_upto(done_seq);
+    // the refill above went out before this join: the fold of the last batch never holds up the
+    // GPU's next batch
+    join_fold();
     if (st.stopped) {
       // a batch enqueued past the stop retires nothing; let it drain before the final copies
       if (inflight[q ^ 1]) HC(hipEventSynchronize(B.done[q ^ 1]), "nested sync");
