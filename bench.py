@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Headline benchmark: batched Metropolis-Hastings on the C2 workload of BASELINE.json.
 
-  python bench.py [--gpus N --steps K --warmup W]     (N > 1: launched by torch.distributed.run)
+  python bench.py [--gpus N --steps K --warmup W]   (N > 1: starts N ranks via a child
+                                                   torch.distributed.run, or runs under one)
 
 Workload (BASELINE.json configs[1]): D=32 diagonal-Gaussian log-target, isotropic Gaussian
 proposal s = 2.38/sqrt(D) * median(sigma), flat box prior [-10, 10]^32, 65,536 independent chains
@@ -57,12 +58,21 @@ def cpu_baseline(args, mu, sg, s):
     GPU box grants 16 CPUs per GPU and exports OMP_NUM_THREADS=16, while its affinity mask shows
     the whole machine), built with -march=native on this host (oracle/Makefile `native`; the
     portable library otherwise), median of 3 timed repeats.  Baseline only."""
+    D = args.ndim
+    O, build = oracle_native()
+    m = O.Model(D, 1, np.concatenate([mu, sg]), 1,
+                np.concatenate([-10 * np.ones(D), 10 * np.ones(D), [-D * math.log(20.0)]]),
+                1, [s])
+    rng = np.random.default_rng(7)
+    return oracle_rate(O, m, lambda n: rng.normal(mu[:, None], sg[:, None], size=(D, n)),
+                       args.cpu_seconds, build, "C2")
+
+
+def oracle_native():
+    """The oracle library built with -march=native on this host (oracle/Makefile `native`), or the
+    portable build if that fails.  Returns (oracle module, build description)."""
     import subprocess
     import oracle as O
-    D = args.ndim
-    nproc = len(os.sched_getaffinity(0))
-    granted = int(os.environ.get("OMP_NUM_THREADS", nproc) or nproc)
-    threads = int(os.environ.get("MCG_CPU_THREADS", min(nproc, granted)))
     build = "-O3 -march=native (built on this host)"
     try:
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "native"], check=True,
@@ -70,13 +80,19 @@ def cpu_baseline(args, mu, sg, s):
         O.LIB_PATH = os.path.join(ROOT, "oracle", "_native", "liboracle.so")
     except (OSError, subprocess.SubprocessError) as e:
         build = "-O3 -march=x86-64-v3 (native build failed: %s)" % type(e).__name__
-    m = O.Model(D, 1, np.concatenate([mu, sg]), 1,
-                np.concatenate([-10 * np.ones(D), 10 * np.ones(D), [-D * math.log(20.0)]]),
-                1, [s])
-    rng = np.random.default_rng(7)
+    return O, build
+
+
+def oracle_rate(O, m, draw_x0, seconds, build, name):
+    """MH steps/s of the oracle's batched sampler on model `m`: pthreads over chain blocks on
+    cpu_threads() cores (64 x threads x 4 chains), a sample sized to ~`seconds` of wall time per
+    repeat, median of 3; plus the single-core rate (256 chains, ~1 s)."""
+    nproc = len(os.sched_getaffinity(0))
+    threads = cpu_threads()
+    D = m.ndim
 
     def run(nch, nsteps, nthreads):
-        x0 = rng.normal(mu[:, None], sg[:, None], size=(D, nch))
+        x0 = draw_x0(nch)
         ll = np.array([m.loglik(x0[:, i]) for i in range(nch)])
         lp = np.full(nch, m.logprior(x0[:, 0]))
         t = time.perf_counter()
@@ -91,14 +107,14 @@ def cpu_baseline(args, mu, sg, s):
         return rates[1], nsteps, rates
 
     nch = 64 * threads * 4
-    rate, nsteps, reps = median_rate(nch, threads, args.cpu_seconds)
+    rate, nsteps, reps = median_rate(nch, threads, seconds)
     # one core: the single-threaded ocamlopt-equivalent proxy
     n1 = 256
     rate1, s1, reps1 = median_rate(n1, 1, 1.0)
     return dict(value=rate, unit="MH steps/s", cores=threads, kind="port", nproc=nproc,
                 repeats=[float(r) for r in reps], statistic="median of 3",
-                sample="%d chains x %d steps of the C2 target per repeat (oracle/oracle.c, %s, %d threads "
-                       "of %d in the affinity mask)" % (nch, nsteps, build, threads, nproc),
+                sample="%d chains x %d steps of the %s target per repeat (oracle/oracle.c, %s, %d threads "
+                       "of %d in the affinity mask)" % (nch, nsteps, name, build, threads, nproc),
                 single_core_value=rate1, single_core_repeats=[float(r) for r in reps1],
                 single_core_sample="%d chains x %d steps, 1 thread, median of 3" % (n1, s1))
 
@@ -139,9 +155,69 @@ def pmc_valu(D, N, S, avg_launch_ms):
             "source": "profiles/pmc_valu.json (rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE)"}
 
 
+def launch_ranks(n, script, argv):
+    """`--gpus N` without a launcher around us: start N ranks (one process per GPU) as a CHILD
+    `python -m torch.distributed.run --nproc-per-node N ... script argv` and return its exit code.
+    Called before anything imports torch or touches the GPU (a process that has initialised the
+    GPU must not exec another program; here the parent never initialises it at all).  The ranks'
+    stdout is inherited, so rank 0's one JSON line is the line this command prints.
+    Returns None when no launch is needed (N = 1, or WORLD_SIZE already set by a launcher)."""
+    import socket
+    import subprocess
+    world = os.environ.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != n:
+            raise SystemExit("bench: --gpus %d but the launcher started WORLD_SIZE=%s ranks" % (n, world))
+        return None
+    if n <= 1:
+        return None
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), script] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    # torch.distributed.run sets OMP_NUM_THREADS=1 in ranks when it is unset; rank 0's CPU
+    # baseline keeps the thread count this process would have used at N = 1
+    env.setdefault("MCG_CPU_THREADS", str(cpu_threads()))
+    return subprocess.run(cmd, env=env).returncode
+
+
+def cpu_threads():
+    """CPUs this process may use: the affinity mask, capped at OMP_NUM_THREADS (the GPU box grants
+    16 CPUs per GPU and exports OMP_NUM_THREADS=16, while its affinity mask shows the machine)."""
+    nproc = len(os.sched_getaffinity(0))
+    granted = int(os.environ.get("OMP_NUM_THREADS", nproc) or nproc)
+    return int(os.environ.get("MCG_CPU_THREADS", min(nproc, granted)))
+
+
+def launch_check(args):
+    """--launch-check: the rank bring-up of the bench without the GPU work (CPU-testable).  Every
+    rank joins the process group on `gloo`, rank 0 gathers (rank, local rank, world) and prints
+    one JSON line with n_gpus = the world size."""
+    import torch.distributed as tdist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        tdist.init_process_group("gloo")
+        ranks = [None] * world
+        tdist.all_gather_object(ranks, (rank, local, world))
+    else:
+        ranks = [(rank, local, world)]
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "gpus_arg": args.gpus,
+                          "ranks": [list(r) for r in ranks], "cpu_threads": cpu_threads()}), flush=True)
+    if world > 1:
+        tdist.barrier()
+        tdist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs (ranks); without WORLD_SIZE in the environment N > 1 launches N ranks")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--sweeps", type=int, default=1000, help="MH sweeps per bench step (one launch, <= 1024)")
@@ -156,7 +232,15 @@ def main():
                     help="extra single-GPU nested runs per rank (own seeds) for the bias estimate")
     ap.add_argument("--cpu-seconds", type=float, default=1.5,
                     help="wall seconds of the CPU baseline sample (x threads = CPU work)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="bring the ranks up (gloo) and print the rank map; no GPU work")
     args = ap.parse_args()
+
+    rc = launch_ranks(args.gpus, os.path.abspath(__file__), sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
+    if args.launch_check:
+        return launch_check(args)
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -281,7 +365,8 @@ def main():
             tdist.barrier()
             tdist.destroy_process_group()
         return
-    cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(args, mu, sg, s)
+    # rank 0 only, at every N (the other ranks wait in the final barrier)
+    cpu = None if args.no_cpu_baseline else cpu_baseline(args, mu, sg, s)
     line = {
         "metric": METRIC,
         "value": value,
@@ -308,6 +393,8 @@ def main():
                      "kernel": "mcg::mh_kernel<32,P,DIAG_GAUSS,GAUSS>",
                      "bytes_per_step": bytes_per_step, "avg_launch_ms": per_launch,
                      "launches": timing["launches"],
+                     "timing_source": "HIP events recorded on the context's stream around each of the "
+                                      "K timed mh_kernel launches (mcg_kernel_timing), averaged",
                      "valu": pmc_valu(D, N, S, per_launch)},
         "cpu_baseline": cpu,
         "accept_frac": acc / max(acc + rej, 1),

@@ -3,8 +3,8 @@
 across GPUs (131,072 per GPU: 1,048,576 over 8), an RCCL all-gather of the tile partials for the
 evidence / posterior-moment reductions.
 
-  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
-      --master-port P scripts/bench_c5.py [--steps K --warmup W --sweeps S]
+  python scripts/bench_c5.py --gpus N [--steps K --warmup W --sweeps S]
+  (or under python -m torch.distributed.run --nnodes=1 --nproc-per-node N ... --gpus N)
 
 One process per GPU (RANK / LOCAL_RANK / WORLD_SIZE from the environment).  Rank r owns the
 global chains [r*N, (r+1)*N) (chain_offset = r*N), so every chain's Philox stream and start point
@@ -72,9 +72,25 @@ def digest(*arrays):
     return h.hexdigest()[:16]
 
 
+def cpu_baseline(mu, cov, s, seconds):
+    """The oracle's full-covariance MH step (oracle/oracle.c, the restatement of mcmc.ml:37-56 with
+    stats.ml's Gaussian in its precision-Cholesky form) on a bounded sample of the C5 target, on
+    rank 0 only: bench.oracle_rate (cpu_threads() cores, median of 3).  Baseline only."""
+    from bench import oracle_native, oracle_rate
+    from mcmc_amd import targets as T
+    O, build = oracle_native()
+    D = len(mu)
+    lik = T.fullcov_gauss(mu, cov)
+    m = O.Model(D, lik.kind, lik.params, 0, (), 1, [s])
+    Lc = np.linalg.cholesky(cov)
+    rng = np.random.default_rng(7)
+    return oracle_rate(O, m, lambda n: mu[:, None] + Lc @ rng.normal(size=(D, n)), seconds, build, "C5")
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=0, help="(informational; WORLD_SIZE decides)")
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs (ranks); without WORLD_SIZE in the environment N > 1 launches N ranks")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--sweeps", type=int, default=500, help="MH sweeps per bench step (one launch)")
@@ -83,7 +99,16 @@ def main():
                     help="global chain count split over the ranks (strong scaling; overrides --chains)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--out", default=None, help="append the JSON line to this file")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=1.5,
+                    help="wall seconds per repeat of the CPU baseline sample (rank 0)")
     args = ap.parse_args()
+
+    sys.path.insert(0, ROOT)
+    from bench import launch_ranks      # child torch.distributed.run before any GPU call
+    rc = launch_ranks(args.gpus, os.path.abspath(__file__), sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -155,6 +180,7 @@ def main():
     ach_tfs = step_chain_steps * flops_per_step / (kernel_ms_per_step * 1e-3) / 1e12
     total_chains = N * world
     if rank == 0:
+        cpu = None if args.no_cpu_baseline else cpu_baseline(mu, cov, s, args.cpu_seconds)
         sdt = np.sqrt(np.diag(cov))
         line = {
             "metric": "C5 MH steps/s (whole job), D=64 full-covariance Gaussian",
@@ -182,6 +208,7 @@ def main():
                          "fp64_matrix": {"achieved": ach_tfs, "peak": FP64_MATRIX_PEAK_TFS,
                                          "unit": "TFLOP/s", "frac": ach_tfs / FP64_MATRIX_PEAK_TFS,
                                          "flops_per_step": flops_per_step}},
+            "cpu_baseline": cpu,
             "accept_frac": acc / max(acc + rej, 1),
             "log_z_harmonic_mean": log_z_hm,
             "posterior_check": {"max_abs_mean_err_over_sd": float(np.max(np.abs(mean - mu) / sdt)),

@@ -6,7 +6,7 @@ mkdir -p gpurun_out/c5r gpurun_out/pmc_cfg
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 for w in 1 2 4; do
   MCG_BENCH_BACKEND=gloo MCG_BENCH_DEVICE=0 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $w \
-    --master-addr 127.0.0.1 --master-port $((29600 + w)) scripts/bench_c5.py --total-chains 524288 --steps 4 --warmup 1 \
+    --master-addr 127.0.0.1 --master-port $((29600 + w)) scripts/bench_c5.py --gpus $w --total-chains 524288 --steps 4 --warmup 1 \
     --out gpurun_out/c5r/rehearsal.jsonl > gpurun_out/c5r/w$w.log 2>&1 || { tail -20 gpurun_out/c5r/w$w.log; exit 1; }
   tail -1 gpurun_out/c5r/rehearsal.jsonl | cut -c1-200
 done

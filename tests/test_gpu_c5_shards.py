@@ -15,13 +15,19 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(world, tmp_path, port):
+def _run(world, tmp_path, port, self_launch=False):
+    """world ranks under an explicit torch.distributed.run, or (self_launch) the runner's own
+    `--gpus N` child launch -- the shape the driver uses for bench.py."""
     out = tmp_path / ("c5_w%d.jsonl" % world)
     env = dict(os.environ, MCG_BENCH_BACKEND="gloo", MCG_BENCH_DEVICE="0", PYTHONUNBUFFERED="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
-           "--master-addr", "127.0.0.1", "--master-port", str(port),
-           os.path.join(ROOT, "scripts", "bench_c5.py"), "--total-chains", "16384", "--sweeps", "40",
-           "--steps", "2", "--warmup", "1", "--out", str(out)]
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    launcher = [] if self_launch else [
+        "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+        "--master-addr", "127.0.0.1", "--master-port", str(port)]
+    cmd = [sys.executable] + launcher + [
+           os.path.join(ROOT, "scripts", "bench_c5.py"), "--gpus", str(world), "--total-chains", "16384",
+           "--sweeps", "40", "--steps", "2", "--warmup", "1", "--out", str(out), "--no-cpu-baseline"]
     subprocess.run(cmd, env=env, check=True, timeout=100, cwd=ROOT)
     return json.loads(out.read_text().strip().splitlines()[-1])
 
@@ -30,7 +36,7 @@ def test_c5_sharded_runner_is_rank_count_invariant(tmp_path):
     import random
     port = 29500 + random.randint(4001, 6000)
     one = _run(1, tmp_path, port)
-    two = _run(2, tmp_path, port + 1)
+    two = _run(2, tmp_path, port + 1, self_launch=True)
     assert one["config"]["chains_total"] == two["config"]["chains_total"] == 16384
     assert two["n_gpus"] == 2 and two["scaling"] == "strong"
     assert one["moments_digest"] == two["moments_digest"]
