@@ -72,8 +72,14 @@ enum {
    FLAT     : (none)              lp = 0
    BOX      : lo[D], hi[D], lp_in lp = lp_in if lo <= x <= hi for all d (inclusive) else -inf
    OPEN_BOX : lo[D], hi[D], lp_in same with strict inequalities (test/nested_test.ml:23-28)
-   For nested sampling the prior must be a box: draw_prior = uniform in [lo, hi]. */
-enum { MCG_PRIOR_FLAT = 0, MCG_PRIOR_BOX = 1, MCG_PRIOR_OPEN_BOX = 2 };
+   DIAG_GAUSS: mu[D], sigma[D]    lp = Stats.log_multi_gaussian mu sigma x (stats.ml:98-108), in
+                                  the canonical form of the DIAG_GAUSS likelihood (sigma > 0)
+   Nested sampling takes a BOX / OPEN_BOX prior (draw_prior = uniform in [lo, hi],
+   Stats.draw_uniform, stats.ml:126-128) or a DIAG_GAUSS prior (draw_prior = mu + sigma z per
+   dim, Stats.draw_gaussian, stats.ml:113-124); with the Gaussian prior the walkers' constrained
+   MH test log u < log_prior y - log_prior x (nested.ml:54-59) is a real test.  The reversible
+   jump sampler (mcg_set_rjmcmc) takes FLAT and box priors only. */
+enum { MCG_PRIOR_FLAT = 0, MCG_PRIOR_BOX = 1, MCG_PRIOR_OPEN_BOX = 2, MCG_PRIOR_DIAG_GAUSS = 3 };
 
 /* ---- proposal kinds (replace jump_proposal / log_jump_prob, mcmc.mli:58-60) ----
    GAUSS        : s[1] or s[D]        y = x + s*z, z ~ N(0,1) per dim (symmetric)

@@ -364,10 +364,19 @@ __device__ __forceinline__ double eval_lik(const double* y, int sub, const MhArg
   }
 }
 
+// MCG_PRIOR_DIAG_GAUSS: Stats.log_multi_gaussian mu sigma y (stats.ml:98-108) in the canonical
+// form of the DIAG_GAUSS likelihood -- its device constants [mu/sigma[D], 1/sigma[D], C] head the
+// prior descriptor (mcg_runtime.cpp pack_prior), so the same code evaluates it bit for bit
+template <int D, int P, typename Q = const double* __restrict__, int W = 4>
+__device__ __forceinline__ double eval_gauss_prior(const double* y, int sub, const MhArgs& a, Q q) {
+  return eval_lik<D, P, MCG_LIK_DIAG_GAUSS, Q, W>(y, sub, a, q);
+}
+
 template <int D, int P, typename Q = const double* __restrict__, int W = 4>
 __device__ __forceinline__ double eval_prior(const double* y, int sub, const MhArgs& a, Q q) {
   using L = Layout<D, P, W>;
   if (a.prior_kind == MCG_PRIOR_FLAT) return 0.0;
+  if (a.prior_kind == MCG_PRIOR_DIAG_GAUSS) return eval_gauss_prior<D, P, Q, W>(y, sub, a, q);
   int inb = 1;
   if (a.ubox) {
     // one box for every dim: the bounds are kernel arguments (SGPRs).  Per-dim loads of the
@@ -405,6 +414,8 @@ __device__ __forceinline__ double eval_prior(const double* y, int sub, const MhA
   return inb ? q[2 * D] : -__builtin_inf();
 }
 
+constexpr int kUniGaussPrior = 3;
+
 // the fused step (per Philox call: normals, coordinates, likelihood terms, box test) applies to
 // separable likelihoods with a Gaussian random-walk proposal
 template <int LIK, int PROP>
@@ -429,9 +440,10 @@ struct AccumCfg {
 // gathers' 32 in-flight registers would spill): C2 1.87e10 -> 1.96e10 MH steps/s against two
 // waves with batched gathers.  Everything else is left to the compiler's register budget, its
 // four normals of a Philox call gathered together (one LDS wait).
-template <int D, int P, int LIK, int PROP>
+template <int D, int P, int LIK, int PROP, int UNI = 0>
 struct MhShape {
-  static constexpr bool kThree = separable<LIK, PROP>() && Layout<D, P, lane_width<D, P, PROP>()>::NL <= 8;
+  static constexpr bool kThree = separable<LIK, PROP>() && UNI != kUniGaussPrior &&
+                                 Layout<D, P, lane_width<D, P, PROP>()>::NL <= 8;
   static constexpr bool kPipe = kThree;
   // (one lane per chain, D <= 8: the whole chain per lane does not fit 168 registers; those
   // instances are built for the two waves per SIMD they reach)
@@ -446,15 +458,20 @@ struct MhShape {
 
 // UNI: 0 = constants through pointers; 1 = isotropic proposal scale and one box [lo, hi] for
 // every dim as kernel arguments; 2 = the same with a symmetric box [-h, h], tested as |y| <= h
-// (one compare per dim; the same predicate as lo <= y <= hi for every double, NaN included)
+// (one compare per dim; the same predicate as lo <= y <= hi for every double, NaN included);
+// kUniGaussPrior = a separable likelihood under a DIAG_GAUSS prior: the step is not fused (the
+// fused step folds a box test, not a second canonical sum), it runs the generic proposal +
+// eval_lik + eval_prior path
 template <int D, int P, int LIK, int PROP, int UNI>
-__global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D, P, LIK, PROP>::kWaves)) mh_kernel(const MhArgs a) {
-  constexpr int kBlk = MhShape<D, P, LIK, PROP>::kBlock;
+__global__ void __launch_bounds__((MhShape<D, P, LIK, PROP, UNI>::kBlock), (MhShape<D, P, LIK, PROP, UNI>::kWaves)) mh_kernel(const MhArgs a) {
+  using Shape = MhShape<D, P, LIK, PROP, UNI>;
+  constexpr int kBlk = Shape::kBlock;
   constexpr int kW = lane_width<D, P, PROP>();
   using L = Layout<D, P, kW>;
   using ACfg = AccumCfg<D, P, kW>;
-  constexpr bool kSeparable = separable<LIK, PROP>();
-  static_assert(kSeparable || !UNI, "UNI applies to the fused separable step");
+  constexpr bool kSeparable = separable<LIK, PROP>() && UNI != kUniGaussPrior;
+  static_assert(kSeparable || UNI == 0 || (UNI == kUniGaussPrior && separable<LIK, PROP>()),
+                "UNI applies to the fused separable step");
   static_assert(!kSeparable || kW == 4, "the fused Gaussian step takes four-dim lane blocks");
   extern __shared__ double lds_acc[];
   __shared__ double2 s_lt[kLogTabN];                 // math tables staged in LDS (gathers)
@@ -505,7 +522,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
   constexpr int NH = P >= 8 ? 1 : 8 / P;
   // the partials live in LDS ([2 NH][256], conflict-free): touched once per P records, they
   // would otherwise hold 4 NH VGPRs through the whole step
-  constexpr bool kHmLds = MhShape<D, P, LIK, PROP>::kHmLds;
+  constexpr bool kHmLds = Shape::kHmLds;
   __shared__ double s_hm[kHmLds ? 2 * NH * kBlk : 1];
   double hcm_r[kHmLds ? 1 : NH], hcs_r[kHmLds ? 1 : NH];
   auto hcm = [&](int l) -> double& {
@@ -626,14 +643,15 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
   constexpr bool kKdReg = PROP == MCG_PROP_KD_INTERP && P > 1;
   static_assert(!kKdReg || LIK == MCG_LIK_FLAT || LIK == MCG_LIK_DIAG_GAUSS || LIK == MCG_LIK_GAUSS_SHELL,
                 "kD on P > 1 lanes: FLAT, DIAG_GAUSS or GAUSS_SHELL");
-  constexpr int kRc = (UNI || kKdReg) ? L::NL : 1;
+  constexpr bool kUniReg = UNI == 1 || UNI == 2;
+  constexpr int kRc = (kUniReg || kKdReg) ? L::NL : 1;
   double rc_m[kRc], rc_i[kRc];
   // UNI: the likelihood normaliser and the box's log density in VGPRs too (a per-step cached
   // load of each put a vector-memory wait on every step's critical path)
   double rc_c = 0.0, rc_lp = 0.0;
-  if constexpr (UNI || kKdReg) {
+  if constexpr (kUniReg || kKdReg) {
     rc_c = LIK == MCG_LIK_DIAG_GAUSS ? a.lik[2 * D] : LIK == MCG_LIK_GAUSS_SHELL ? a.lik[D + 2] : 0.0;
-    rc_lp = a.prior_kind != MCG_PRIOR_FLAT ? a.pri[2 * D] : 0.0;
+    rc_lp = a.prior_kind != MCG_PRIOR_FLAT && a.prior_kind != MCG_PRIOR_DIAG_GAUSS ? a.pri[2 * D] : 0.0;
     asm volatile("" : "+v"(rc_c), "+v"(rc_lp));
 #pragma unroll
     for (int i = 0; i < L::NCL; ++i)
@@ -652,7 +670,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
       rc_r = a.lik[D];
       rc_iw = a.lik[D + 1];
     }
-    const bool pbox = a.prior_kind != MCG_PRIOR_FLAT;
+    const bool pbox = a.prior_kind == MCG_PRIOR_BOX || a.prior_kind == MCG_PRIOR_OPEN_BOX;
 #pragma unroll
     for (int i = 0; i < L::NCL; ++i)
 #pragma unroll
@@ -770,7 +788,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
     gconst* gpri = (gconst*)a.pri;
     gconst* gprop = (gconst*)a.prop;
     // (the fused step with UNI constants reads none of them: no per-step copies there)
-    if constexpr (!(kSeparable && UNI)) asm volatile("" : "+s"(glik), "+s"(gpri), "+s"(gprop));
+    if constexpr (!(kSeparable && kUniReg)) asm volatile("" : "+s"(glik), "+s"(gpri), "+s"(gprop));
     [[maybe_unused]] const double* qlik = (const double*)glik;
     [[maybe_unused]] const double* qpri = (const double*)gpri;
     const double* qprop = (const double*)gprop;
@@ -854,7 +872,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
           }
         }
       };
-      if constexpr (MhShape<D, P, LIK, PROP>::kPipe) {
+      if constexpr (Shape::kPipe) {
         // one normal at a time with its table rows gathered one normal ahead: the gathers of
         // normal m + 1 are in flight while normal m is finished and its dim's terms computed
         auto word = [&](int m) __attribute__((always_inline)) -> uint32_t {
@@ -874,7 +892,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
 #pragma unroll
       for (int i = 0; i < L::NCL; ++i) {
         double z[4];
-        if constexpr (MhShape<D, P, LIK, PROP>::kBatchNormals) {
+        if constexpr (Shape::kBatchNormals) {
           pnormal4_lds(wl[i], s_nt, z);
         } else {
           const u32x4 w = wl[i];
@@ -1096,6 +1114,11 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP>::kBlock), (MhShape<D
         }
         if (a.prior_kind == MCG_PRIOR_FLAT) {
           lpy = 0.0;
+        } else if (a.prior_kind == MCG_PRIOR_DIAG_GAUSS) {
+          typedef const __attribute__((address_space(4))) double kconst;
+          kconst* kpri = (kconst*)a.pri;
+          asm volatile("" : "+s"(kpri));
+          lpy = eval_gauss_prior<D, P, kconst*, kW>(y, sub, a, kpri);
         } else {
           int inb = 1;
 #pragma unroll
@@ -1226,6 +1249,10 @@ hipError_t launch_mh(const MhArgs& a, int64_t nthreads, hipStream_t s) {
   const int64_t grid = (nthreads + block - 1) / block;
   constexpr int lds = AccumCfg<D, P, lane_width<D, P, PROP>()>::kLdsBytes;
   if constexpr (separable<LIK, PROP>()) {
+    if (a.prior_kind == MCG_PRIOR_DIAG_GAUSS) {
+      hipLaunchKernelGGL((mh_kernel<D, P, LIK, PROP, kUniGaussPrior>), dim3((unsigned)grid), dim3(block), lds, s, a);
+      return hipGetLastError();
+    }
     if (a.uni && a.uni_lo == -a.uni_hi) {
       hipLaunchKernelGGL((mh_kernel<D, P, LIK, PROP, 2>), dim3((unsigned)grid), dim3(block), lds, s, a);
       return hipGetLastError();

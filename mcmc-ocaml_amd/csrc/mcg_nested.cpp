@@ -279,11 +279,12 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   const int D = ctx->Dk, Dr = ctx->D;
   if (D < 1) return set_error(ctx, MCG_ESTATE, "set the likelihood first");
   if (ctx->rj_active) return set_error(ctx, MCG_ESTATE, "nested sampling after mcg_set_rjmcmc: set a likelihood first");
-  if (ctx->prior_kind != MCG_PRIOR_BOX && ctx->prior_kind != MCG_PRIOR_OPEN_BOX)
-    return set_error(ctx, MCG_EINVAL, "nested sampling needs a box prior (draw_prior = uniform in the box)");
+  const bool box_prior = ctx->prior_kind == MCG_PRIOR_BOX || ctx->prior_kind == MCG_PRIOR_OPEN_BOX;
+  if (!box_prior && ctx->prior_kind != MCG_PRIOR_DIAG_GAUSS)
+    return set_error(ctx, MCG_EINVAL, "nested sampling needs a box or DIAG_GAUSS prior (a draw_prior)");
   // the box's log density enters every walker step's MH ratio as lp_box - lp_box = +0: a finite
   // value is what makes that test always pass (mcg_nested_kernel.h, the shell walker's step)
-  if (!std::isfinite(ctx->pri_host[2 * D]))
+  if (box_prior && !std::isfinite(ctx->pri_host[2 * D]))
     return set_error(ctx, MCG_EINVAL, "nested sampling needs a finite box log density");
   const int64_t n = opts->nlive > 0 ? opts->nlive : 1000;
   const int64_t k = opts->k > 0 ? opts->k : 1;
@@ -348,7 +349,7 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
     // a box prior symmetric in every dim (closed form lo[d] == -hi[d], bitwise): the walkers
     // test it as |y| <= hi, one compare per dim
     const auto& bx = ctx->pri_host;
-    bool sym = ctx->prior_kind != MCG_PRIOR_FLAT && (int64_t)bx.size() >= 2 * D;
+    bool sym = box_prior && (int64_t)bx.size() >= 2 * D;
     for (int64_t d = 0; d < D && sym; ++d) {
       const double nhi = -bx[(size_t)(D + d)];
       sym = !std::memcmp(&bx[(size_t)d], &nhi, 8);

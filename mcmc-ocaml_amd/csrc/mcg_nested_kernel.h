@@ -193,7 +193,7 @@ struct WalkLayout {
 // bounds), loaded into registers once per launch.  Loaded per step through the parameter
 // pointers they would queue behind the prefetched DE rows in the in-order vector-memory counter
 // and expose the full load latency every step.  Same operations as eval_lik / eval_prior.
-template <int D, int P, int LIK, bool SYM = false>
+template <int D, int P, int LIK, bool SYM = false, bool GP = false>
 struct WalkTarget {
   using Lay = WalkLayout<D, P>;
   static constexpr int W = Lay::W;
@@ -209,7 +209,7 @@ struct WalkTarget {
     if constexpr (kReg) {
       const double* __restrict__ q = a.lik;
       const double* __restrict__ pr = a.pri;
-      box = a.prior_kind != MCG_PRIOR_FLAT;
+      box = !GP && a.prior_kind != MCG_PRIOR_FLAT;   // GP: no bounds (lo, hi = -+inf)
 #pragma unroll
       for (int i = 0; i < Lay::NCL; ++i)
 #pragma unroll
@@ -219,12 +219,12 @@ struct WalkTarget {
           const int d = v ? Lay::dim(sub, i, k) : 0;
           m0[j] = (v && LIK != MCG_LIK_FLAT) ? q[d] : 0.0;
           m1[j] = (v && LIK == MCG_LIK_DIAG_GAUSS) ? q[D + d] : 0.0;
-          lo[j] = v ? pr[d] : -__builtin_inf();
-          hi[j] = v ? pr[D + d] : __builtin_inf();
+          lo[j] = (v && !GP) ? pr[d] : -__builtin_inf();
+          hi[j] = (v && !GP) ? pr[D + d] : __builtin_inf();
         }
       if constexpr (LIK == MCG_LIK_DIAG_GAUSS) c0 = q[2 * D];
       if constexpr (LIK == MCG_LIK_GAUSS_SHELL) { c0 = q[D]; c1 = q[D + 1]; c2 = q[D + 2]; }
-      lp_in = pr[2 * D];
+      lp_in = GP ? 0.0 : pr[2 * D];
     }
   }
 
@@ -352,7 +352,7 @@ struct WalkTarget {
   // NaN makes S NaN, which the band test below counts as outside (!(S >= lo) is true for NaN),
   // so the step rejects for any threshold -- as prior() = -inf would.  Inside the box the
   // decision is constraint() && prior() > -inf exactly.  W = 4 register targets (the shell).
-  static constexpr bool kFold = kReg && LIK == MCG_LIK_GAUSS_SHELL && W == 4;
+  static constexpr bool kFold = kReg && LIK == MCG_LIK_GAUSS_SHELL && W == 4 && !GP;
   __device__ __forceinline__ double lp_box() const { return (SYM || box) ? lp_in : 0.0; }
   template <bool BOXT = true>   // BOXT = false: the box test is implied (box_test false)
   __device__ __forceinline__ bool constraint_box(const double* y, int sub, double thr) const {
@@ -390,7 +390,14 @@ struct WalkTarget {
   }
 
   __device__ __forceinline__ double prior(const double* y, int sub, const MhArgs& a) const {
-    if constexpr (!kReg) {
+    if constexpr (GP) {
+      // Stats.log_multi_gaussian of the prior (canonical DIAG form), its constants through
+      // scalar loads (kept out of the in-order vector-memory queue of the prefetched DE rows)
+      typedef const __attribute__((address_space(4))) double kconst;
+      kconst* kpri = (kconst*)a.pri;
+      asm volatile("" : "+s"(kpri));
+      return eval_gauss_prior<D, P, kconst*, W>(y, sub, a, kpri);
+    } else if constexpr (!kReg) {
       return eval_prior<D, P>(y, sub, a, a.pri);
     } else {
       if (!SYM && !box) return 0.0;                   // SYM implies a box prior
@@ -413,7 +420,9 @@ struct WalkTarget {
 // scale, accept decision and start point agree without communication; the log-target is the
 // canonical sum reduced across the P lanes (reduce_canon).  The DE partner rows of step s + 1
 // depend only on the RNG, so they are loaded while step s computes (one step of prefetch).
-template <int D, int LIK, int P, bool TAB, bool SYM>
+// GP: a DIAG_GAUSS prior, whose log density makes the walker's MH test log u < lp(y) - lp(cur)
+// (nested.ml:54-59) a real test (with box priors it holds for every passing proposal)
+template <int D, int LIK, int P, bool TAB, bool SYM, bool GP = false>
 __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   using Lay = WalkLayout<D, P>;
   constexpr int NL = Lay::NL;
@@ -461,7 +470,8 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   double row_first[NL];
   unsigned long long tix_cur[PD], tix_ring[PD];
   double2 tsc_cur[PD];
-  WalkTarget<D, P, LIK, SYM> tgt;                    // the log-target's constants (registers)
+  using Tgt = WalkTarget<D, P, LIK, SYM, GP>;
+  Tgt tgt;                                           // the log-target's constants (registers)
   if (walker) {
     tgt.load(a.m, sub);
     thr = a.key_ll[a.k - 1];
@@ -535,7 +545,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
           }
         }
       }
-      walk_draws_fill<!WalkTarget<D, P, LIK, SYM>::kFold>(a, a.mrep + a.k, (int64_t)blockIdx.x * nf + (threadIdx.x - wl), (int64_t)gridDim.x * nf, lt);
+      walk_draws_fill<!Tgt::kFold>(a, a.mrep + a.k, (int64_t)blockIdx.x * nf + (threadIdx.x - wl), (int64_t)gridDim.x * nf, lt);
 #ifdef MCG_NEST_TRACE
       if (a.trace && (int)threadIdx.x == wl && blockIdx.x < 1024)   // the table-filling waves' end
         a.trace[((size_t)0 * 1024 + blockIdx.x) * 8 + 5] = wall_clock64();
@@ -769,7 +779,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
       refill(bj[u], jp_g[u]);
       // mcmc.ml:47-48 computes (((ml + 0) - (cur_l + 0)) + 0) - 0 (flat proposal density); the
       // +0 / -0 terms change at most the sign of a zero, so `lu < ratio` is the same test
-      if constexpr (WalkTarget<D, P, LIK, SYM>::kFold) {
+      if constexpr (Tgt::kFold) {
         // ml is lp_box when the proposal passes and -inf when it fails, and -inf - cur_l fails
         // `lu < ratio` for every cur_l (-inf or NaN), so the step accepts iff it passes and
         // lu < lp_box - cur_l.  That half always holds: cur_l is lp_box (a live point inside the
@@ -836,13 +846,26 @@ __global__ void __launch_bounds__(256) nest_init_kernel(const NestArgs a, double
   if (s >= a.n) return;
   const Rng rng{a.k0, a.k1};
   const double* __restrict__ lo = a.m.pri + 2 * D + 1;     // caller's bounds (see mcg_set_prior)
-  const double* __restrict__ hi = a.m.pri + 3 * D + 1;
+  const double* __restrict__ hi = a.m.pri + 3 * D + 1;     // (DIAG_GAUSS prior: mu, sigma)
   double x[D];
+  if (a.m.prior_kind == MCG_PRIOR_DIAG_GAUSS) {
+    // Stats.draw_gaussian mu sigma per dim (stats.ml:113-124: mu + sigma z): the normals of dims
+    // 4c .. 4c+3 from call c
 #pragma unroll
-  for (int d = 0; d < D; d += 2) {
-    const u32x4 r = rng((uint32_t)s, 0u, (uint32_t)(d >> 1), TAG_NEST_PRIOR, 0u);
-    x[d] = lo[d] + (hi[d] - lo[d]) * u53(r.x, r.y);
-    if (d + 1 < D) x[d + 1] = lo[d + 1] + (hi[d + 1] - lo[d + 1]) * u53(r.z, r.w);
+    for (int d = 0; d < D; d += 4) {
+      const u32x4 r = rng((uint32_t)s, 0u, (uint32_t)(d >> 2), TAG_NEST_PRIOR, 0u);
+      const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (d + j < D) x[d + j] = lo[d + j] + hi[d + j] * pnormal(w[j], kNrmTab);
+    }
+  } else {
+#pragma unroll
+    for (int d = 0; d < D; d += 2) {
+      const u32x4 r = rng((uint32_t)s, 0u, (uint32_t)(d >> 1), TAG_NEST_PRIOR, 0u);
+      x[d] = lo[d] + (hi[d] - lo[d]) * u53(r.x, r.y);
+      if (d + 1 < D) x[d + 1] = lo[d + 1] + (hi[d + 1] - lo[d + 1]) * u53(r.z, r.w);
+    }
   }
 #pragma unroll
   for (int d = 0; d < D; ++d) a.x[s * D + d] = x[d];
@@ -867,6 +890,11 @@ hipError_t launch_nest_walk_p(const NestArgs& a, hipStream_t st) {
   b.walk_waves = wwaves > 256 ? 2 : 1;
   const dim3 gt((unsigned)((wwaves + b.walk_waves - 1) / b.walk_waves)), bt(256);
   constexpr bool kSym = WalkTarget<D, P, LIK>::kReg;   // the |y| <= h form needs the register target
+  if (a.m.prior_kind == MCG_PRIOR_DIAG_GAUSS) {
+    if (b.rt_ix) hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, false, true>), gt, bt, 0, st, b);
+    else hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, false, false, true>), dim3((unsigned)grid), dim3(block), 0, st, a);
+    return hipGetLastError();
+  }
   if (b.rt_ix && kSym && b.sym_box) hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, kSym>), gt, bt, 0, st, b);
   else if (b.rt_ix) hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, false>), gt, bt, 0, st, b);
   else hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, false, false>), dim3((unsigned)grid), dim3(block), 0, st, a);

@@ -80,6 +80,8 @@ int mcg_set_rjmcmc(mcg_ctx* ctx, const mcg_rj_model* a, const mcg_rj_model* b) {
     if (q->lik_kind != MCG_LIK_FLAT && q->lik_kind != MCG_LIK_DIAG_GAUSS && q->lik_kind != MCG_LIK_GAUSS_SHELL &&
         q->lik_kind != MCG_LIK_FULLCOV_GAUSS)
       return set_error(ctx, MCG_EINVAL, "RJ: likelihood kind %d not supported", q->lik_kind);
+    if (q->prior_kind == MCG_PRIOR_DIAG_GAUSS)
+      return set_error(ctx, MCG_EINVAL, "RJ: FLAT, BOX or OPEN_BOX priors only");
     std::vector<double> lik, pri, jmp, into;
     if ((rc = pack_likelihood(ctx, q->lik_kind, D, q->lik_params, q->n_lik, lik, nullptr, nullptr))) return rc;
     if ((rc = pack_prior(ctx, q->prior_kind, D, q->prior_params, q->n_prior, pri))) return rc;

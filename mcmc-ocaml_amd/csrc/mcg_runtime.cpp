@@ -430,6 +430,19 @@ std::vector<double> pad_prior(int D, int DM, const std::vector<double>& v, doubl
   return o;
 }
 
+std::vector<double> pad_gauss_prior(int D, int DM, const std::vector<double>& v) {
+  if (D == DM) return v;
+  std::vector<double> o(4 * (size_t)DM + 1, 0.0);
+  for (int d = 0; d < D; ++d) {
+    o[d] = v[d];
+    o[DM + d] = v[D + d];
+    o[2 * DM + 1 + d] = v[2 * D + 1 + d];
+    o[3 * DM + 1 + d] = v[3 * D + 1 + d];
+  }
+  o[2 * DM] = v[2 * D];
+  return o;
+}
+
 std::vector<double> pad_rows(const double* rows, int64_t n, int D, int DM) {
   std::vector<double> o((size_t)n * DM, 0.0);
   for (int64_t i = 0; i < n; ++i) std::copy(rows + i * D, rows + (i + 1) * D, o.begin() + i * DM);
@@ -507,6 +520,23 @@ int pack_prior(mcg_ctx* ctx, int32_t kind, int D, const double* params, size_t n
         dev[d] = std::nextafter(params[d], HUGE_VAL);
         dev[D + d] = std::nextafter(params[D + d], -HUGE_VAL);
       }
+  } else if (kind == MCG_PRIOR_DIAG_GAUSS) {
+    // [mu/sigma[D], 1/sigma[D], C, mu[D], sigma[D]]: the DIAG_GAUSS likelihood's canonical
+    // constants (the kernels evaluate lp with that same code), then the caller's mu and sigma
+    // for the prior draws of nested sampling (Stats.draw_gaussian, stats.ml:113-124)
+    if (!params || n != (size_t)(2 * D))
+      return set_error(ctx, MCG_EINVAL, "DIAG_GAUSS prior: params = mu[D], sigma[D]");
+    double C = 0.0;
+    for (int d = 0; d < D; ++d) {
+      if (!(params[D + d] > 0.0) || !std::isfinite(params[D + d]) || !std::isfinite(params[d]))
+        return set_error(ctx, MCG_EINVAL, "DIAG_GAUSS prior: finite mu, 0 < sigma < inf");
+      dev[D + d] = 1.0 / params[D + d];
+      dev[d] = params[d] * dev[D + d];
+      C = C + (kNegHalfLog2Pi - std::log(params[D + d]));
+      dev[2 * D + 1 + d] = params[d];
+      dev[3 * D + 1 + d] = params[D + d];
+    }
+    dev[2 * D] = C;
   } else {
     return set_error(ctx, MCG_EINVAL, "unknown prior kind %d", kind);
   }
@@ -525,8 +555,11 @@ int mcg_set_prior(mcg_ctx* ctx, int32_t kind, const double* params, size_t n) {
   std::vector<double> dev;
   int prc = pack_prior(ctx, kind, D, params, n, dev);
   if (prc) return prc;
-  // padded dims: unbounded in the box test, drawn at 0 by nested sampling's prior draws
-  dev = pad_prior(D, ctx->Dk, dev, 0.0, 0.0);
+  // padded dims: unbounded in the box test, drawn at 0 by nested sampling's prior draws; a
+  // Gaussian prior's pad dims have zero constants (each adds +0.0 to its canonical accumulator,
+  // as the DIAG_GAUSS likelihood's pad dims do) and are drawn as 0 + 0 z
+  if (kind == MCG_PRIOR_DIAG_GAUSS) dev = pad_gauss_prior(D, ctx->Dk, dev);
+  else dev = pad_prior(D, ctx->Dk, dev, 0.0, 0.0);
   ctx->prior_kind = kind;
   ctx->pri_host = dev;
   int rc = hip_check(ctx, ctx->d_pri.ensure(dev.size() * 8), "alloc prior");
@@ -710,7 +743,8 @@ MhArgs base_args(mcg_ctx* ctx) {
   const auto& bx = ctx->pri_host;
   // one box for every dim (bitwise), any proposal: eval_prior compares against kernel arguments
   // instead of loading 2D bounds per step
-  if (ctx->prior_kind != MCG_PRIOR_FLAT && D >= 1 && (int)bx.size() >= 2 * D && !ctx->rj_active) {
+  const bool box_desc = ctx->prior_kind != MCG_PRIOR_DIAG_GAUSS;   // bx holds bounds (FLAT: +-inf)
+  if (ctx->prior_kind != MCG_PRIOR_FLAT && box_desc && D >= 1 && (int)bx.size() >= 2 * D && !ctx->rj_active) {
     bool same = Dr == D || (bx[0] <= 0.0 && 0.0 <= bx[D]);
     for (int d = 1; d < Dr && same; ++d)
       same = !std::memcmp(&bx[d], &bx[0], 8) && !std::memcmp(&bx[D + d], &bx[D], 8);
@@ -720,7 +754,8 @@ MhArgs base_args(mcg_ctx* ctx) {
       a.box_hi = bx[D];
     }
   }
-  if (ctx->prop_kind == MCG_PROP_GAUSS && D >= 1 && Dr == D && (int)sp.size() >= D && (int)bx.size() >= 2 * D) {
+  if (ctx->prop_kind == MCG_PROP_GAUSS && box_desc && D >= 1 && Dr == D && (int)sp.size() >= D &&
+      (int)bx.size() >= 2 * D) {
     bool same = true;
     for (int d = 1; d < D && same; ++d)
       same = !std::memcmp(&sp[d], &sp[0], 8) && !std::memcmp(&bx[d], &bx[0], 8) &&
@@ -745,7 +780,9 @@ int choose_lanes(mcg_ctx* ctx) {
   int want = ctx->opts.lanes_per_chain;
   if (env && *env) want = std::atoi(env);
   // full covariance, Gaussian proposal, D in {16,32,48,64}: the matrix-core kernel (4 lanes/chain)
+  // (its step tests a box prior only: a Gaussian prior runs the one-lane kernel)
   const bool fullcov_mfma = ctx->lik_kind == MCG_LIK_FULLCOV_GAUSS && ctx->prop_kind == MCG_PROP_GAUSS &&
+                            ctx->prior_kind != MCG_PRIOR_DIAG_GAUSS &&
                             find_mh_kernel(D, 4, ctx->lik_kind, ctx->prop_kind) != nullptr;
   // the kD independence proposal with a separable likelihood: its draw splits over lanes too
   const bool kd_split = ctx->prop_kind == MCG_PROP_KD_INTERP &&

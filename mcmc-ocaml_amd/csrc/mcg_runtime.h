@@ -131,6 +131,8 @@ std::vector<double> pad_lik(int32_t kind, int D, int DM, const std::vector<doubl
 // unbounded in the check and drawn in [pad_draw, pad_draw] (0: nested sampling's prior draws
 // leave them at 0)
 std::vector<double> pad_prior(int D, int DM, const std::vector<double>& v, double pad_draw_lo, double pad_draw_hi);
+// a DIAG_GAUSS prior descriptor at width DM: zero constants (and mu = sigma = 0) in the pad dims
+std::vector<double> pad_gauss_prior(int D, int DM, const std::vector<double>& v);
 // rows [n][D] -> [n][DM] with zero pad columns
 std::vector<double> pad_rows(const double* rows, int64_t n, int D, int DM);
 typedef hipError_t (*rj_init_fn)(const MhArgs&, int draw_tags, const double* xa, const double* xb, hipStream_t);

@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("MCG_LIBRARY", os.path.join(PKG_ROOT, "lib", "libmcg.s
 MCG_OK, MCG_EINVAL, MCG_EFAIL, MCG_EDEVICE, MCG_ENOMEM, MCG_ESTATE = 0, -1, -2, -3, -4, -5
 LIK_FLAT, LIK_DIAG_GAUSS, LIK_FULLCOV_GAUSS, LIK_GAUSS_SHELL, LIK_GAUSS_DATA, LIK_CAUCHY_DATA, LIK_GAUSS_MIX = range(7)
 LIK_MIX_MAX = 64
-PRIOR_FLAT, PRIOR_BOX, PRIOR_OPEN_BOX = 0, 1, 2
+PRIOR_FLAT, PRIOR_BOX, PRIOR_OPEN_BOX, PRIOR_DIAG_GAUSS = 0, 1, 2, 3
 PROP_GAUSS, PROP_WRAP_UNIFORM, PROP_KD_INTERP, PROP_DE, PROP_MIXTURE = 1, 2, 3, 4, 5
 MIX_GAUSS, MIX_SHIFT_UNIFORM, MIX_WRAP_UNIFORM, MIX_KD_INTERP = 1, 2, 3, 4
 RJ_JUMP_GAUSS, RJ_JUMP_WRAP, RJ_JUMP_INDEP_GAUSS, RJ_JUMP_KD = 1, 2, 3, 4

@@ -92,6 +92,15 @@ def box(lo, hi, lp_in=None, open_=False):
     return Prior(L.PRIOR_OPEN_BOX if open_ else L.PRIOR_BOX, np.concatenate([lo, hi, [lp_in]]))
 
 
+def gauss_prior(mu, sigma):
+    """log_prior = Stats.log_multi_gaussian mu sigma (stats.ml:98-108); nested sampling's
+    draw_prior = Stats.draw_gaussian mu sigma per dim (stats.ml:113-124)."""
+    mu, sigma = _f64(mu), _f64(sigma)
+    if mu.shape != sigma.shape:
+        raise ValueError("gauss_prior: mu and sigma must have the same length")
+    return Prior(L.PRIOR_DIAG_GAUSS, np.concatenate([mu, sigma]))
+
+
 # ---- proposals ----
 def gauss(scale):
     """y = x + scale * N(0, 1) per dim (symmetric; log_jump_prob = 0)."""

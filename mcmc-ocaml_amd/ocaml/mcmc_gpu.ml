@@ -99,6 +99,9 @@ type prior =
   | Flat_prior
   | Box of float array * float array * float
   | Open_box of float array * float array * float
+  | Gauss_prior of float array * float array
+      (* mu, sigma: log_prior = Stats.log_multi_gaussian mu sigma, draw_prior =
+         Stats.draw_gaussian per dim (stats.ml:98-124) *)
 
 type mix_component =
   | Mix_gauss of float array
@@ -157,7 +160,10 @@ let set_model ctx lik pri prop =
    | Box (lo, hi, lp) | Open_box (lo, hi, lp) ->
      let k = match pri with Open_box _ -> 2l | _ -> 1l in
      let p = Array.concat [ lo; hi; [| lp |] ] in
-     check ctx (c_set_prior ctx k (carr p) (Unsigned.Size_t.of_int (Array.length p))));
+     check ctx (c_set_prior ctx k (carr p) (Unsigned.Size_t.of_int (Array.length p)))
+   | Gauss_prior (mu, sigma) ->
+     let p = Array.append mu sigma in
+     check ctx (c_set_prior ctx 3l (carr p) (Unsigned.Size_t.of_int (Array.length p))));
   match prop with
   | None -> ()
   | Some (Gauss s) -> check ctx (c_set_proposal ctx 1l (carr s) (Unsigned.Size_t.of_int (Array.length s)))
@@ -338,7 +344,8 @@ let rj_struct m =
   let pk, pp = match m.rj_prior with
     | Flat_prior -> 0, [||]
     | Box (lo, hi, l) -> 1, Array.concat [ lo; hi; [| l |] ]
-    | Open_box (lo, hi, l) -> 2, Array.concat [ lo; hi; [| l |] ] in
+    | Open_box (lo, hi, l) -> 2, Array.concat [ lo; hi; [| l |] ]
+    | Gauss_prior _ -> invalid_arg "Mcmc_gpu: reversible jump takes flat or box priors" in
   let jump = function
     | Rj_gauss sc -> 1, sc
     | Rj_wrap (lo, hi, dx) -> 2, Array.concat [ lo; hi; dx ]

@@ -35,6 +35,9 @@ type prior =
   | Flat_prior
   | Box of float array * float array * float     (** lo, hi, log density inside (inclusive) *)
   | Open_box of float array * float array * float
+  | Gauss_prior of float array * float array
+      (** mu, sigma: Stats.log_multi_gaussian mu sigma; nested sampling draws the live points
+          with Stats.draw_gaussian per dim *)
 
 (** components of Mcmc.combine_jump_proposals (mcmc.ml:165-185) *)
 type mix_component =
@@ -86,7 +89,7 @@ val mcmc_array :
     log of Evidence.evidence_harmonic_mean (evidence.ml:101-107). *)
 val stats : ctx -> float array * float array * float
 
-(** Nested.nested_evidence (nested.mli:50-61) with the context's likelihood and box prior;
+(** Nested.nested_evidence (nested.mli:50-61) with the context's likelihood and its box or Gauss_prior prior;
     [k] live points retired per generation (1 = the reference algorithm).  Returns the
     nested_output tuple: log Z, log dZ, points (n x D), log weights. *)
 val nested_evidence :

@@ -276,6 +276,7 @@ typedef struct {
   double de_mh, de_sigma; int64_t de_M; const double* de_pts;   /* DE: samples [M][D] */
   const double* raw_lik;                       /* the caller's likelihood parameters */
   int ngm; double* gm;                         /* GAUSS_MIX: per component mu/s[D], 1/s[D], C */
+  double* gp; const double* gp_mu; const double* gp_sig;   /* DIAG_GAUSS prior: mu/s[D], 1/s[D], C */
 } prep_t;
 
 /* one component of Mcmc.combine_jump_proposals (mcmc.ml:165-185): normalised weight p, log p,
@@ -289,7 +290,7 @@ struct mix_comp {
 };
 
 static void prep_free(prep_t* p) {
-  free(p->mu); free(p->isig); free(p->ctr); free(p->s); free(p->gm);
+  free(p->mu); free(p->isig); free(p->ctr); free(p->s); free(p->gm); free(p->gp);
   for (int c = 0; c < p->nmix; ++c) { free(p->mix[c].inv_s); free(p->mix[c].width); }
   free(p->mix);
 }
@@ -354,6 +355,21 @@ static int prep_model(const or_model* m, prep_t* p) {
   }
   if (p->prior == MCG_PRIOR_BOX || p->prior == MCG_PRIOR_OPEN_BOX) {
     p->lo = m->prior_params; p->hi = m->prior_params + D; p->lp_in = m->prior_params[2 * D];
+  } else if (p->prior == MCG_PRIOR_DIAG_GAUSS) {
+    /* Stats.log_multi_gaussian mu sigma as a log_prior (stats.ml:98-108): the DIAG_GAUSS
+       likelihood's canonical constants (above) of the prior's mu, sigma */
+    const double* pq = m->prior_params;
+    if (m->n_prior_params != 2 * (int64_t)D) return -1;
+    p->gp_mu = pq; p->gp_sig = pq + D;
+    p->gp = (double*)malloc(sizeof(double) * (size_t)(2 * D + 1));
+    double C = 0.0;
+    for (int d = 0; d < D; ++d) {
+      if (!(pq[D + d] > 0.0)) return -1;
+      p->gp[D + d] = 1.0 / pq[D + d];
+      p->gp[d] = pq[d] * p->gp[D + d];
+      C = C + (NEG_HALF_LOG_2PI - log(pq[D + d]));
+    }
+    p->gp[2 * D] = C;
   }
   if (p->prop == MCG_PROP_GAUSS) {
     p->s = (double*)malloc(sizeof(double) * D);
@@ -570,6 +586,15 @@ static double lik_eval(const prep_t* p, const double* x) {
 
 static double prior_eval(const prep_t* p, const double* x) {
   if (p->prior == MCG_PRIOR_FLAT) return 0.0;
+  if (p->prior == MCG_PRIOR_DIAG_GAUSS) {
+    if (g_literal) return or_log_multi_gaussian(p->gp_mu, p->gp_sig, x, p->D);   /* stats.ml:103-108 */
+    double A[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int d = 0; d < p->D; ++d) {
+      double e = fma(x[d], p->gp[p->D + d], -p->gp[d]);
+      A[(d >> 2) & 7] = fma(e, e, A[(d >> 2) & 7]);
+    }
+    return p->gp[2 * p->D] - 0.5 * canon8(A);
+  }
   int inb = 1;
   for (int d = 0; d < p->D; ++d) {
     if (p->prior == MCG_PRIOR_BOX) inb &= (x[d] >= p->lo[d]) & (x[d] <= p->hi[d]);
@@ -1289,7 +1314,8 @@ int or_nested(const or_model* m, uint64_t seed, const or_nested_opts* o, double*
   if (prep_model(m, &p) != 0) return -1;
   int D = p.D;
   int64_t n = o->nlive, k = o->k;
-  if (n < 2 || k < 1 || k >= n || D > 256 || !(p.prior == MCG_PRIOR_BOX || p.prior == MCG_PRIOR_OPEN_BOX)) {
+  if (n < 2 || k < 1 || k >= n || D > 256 ||
+      !(p.prior == MCG_PRIOR_BOX || p.prior == MCG_PRIOR_OPEN_BOX || p.prior == MCG_PRIOR_DIAG_GAUSS)) {
     prep_free(&p); return -1;
   }
   double* lx = (double*)malloc(sizeof(double) * (size_t)(n * D));   /* live AoS [slot][D] */
@@ -1306,8 +1332,18 @@ int or_nested(const or_model* m, uint64_t seed, const or_nested_opts* o, double*
   /* prefix[j] = sum_{j'<j} log1p(-1/(n-j')) -- volume after j retirements in a generation */
   prefix[0] = 0.0;
   for (int64_t j = 0; j < k; ++j) prefix[j + 1] = prefix[j] + log1p(-1.0 / (double)(n - j));
-  /* draw_prior: uniform in the box (Stats.draw_uniform, stats.ml:126-128) */
+  /* draw_prior: uniform in the box (Stats.draw_uniform, stats.ml:126-128), or for a DIAG_GAUSS
+     prior Stats.draw_gaussian mu sigma per dim (stats.ml:113-124: mu + sigma z) with the normals
+     of dims 4c .. 4c+3 from call c */
   for (int64_t s = 0; s < n; ++s) {
+    if (p.prior == MCG_PRIOR_DIAG_GAUSS) {
+      for (int c = 0; 4 * c < D; ++c) {
+        uint32_t w[4];
+        rng4(seed, (uint32_t)s, 0u, (uint32_t)c, TAG_NEST_PRIOR, 0u, w);
+        for (int j = 0; j < 4 && 4 * c + j < D; ++j)
+          lx[s * D + 4 * c + j] = p.gp_mu[4 * c + j] + p.gp_sig[4 * c + j] * or_normal(w[j]);
+      }
+    } else
     for (int d = 0; d < D; d += 2) {
       uint32_t w[4];
       rng4(seed, (uint32_t)s, 0u, (uint32_t)(d >> 1), TAG_NEST_PRIOR, 0u, w);

@@ -142,6 +142,7 @@ def test_kind_numbers_are_the_header_enums():
     assert "c_set_proposal ctx 5l" in body and _enum("MCG_PROP_MIXTURE") == 5
     assert "Open_box _ -> 2l" in body and _enum("MCG_PRIOR_OPEN_BOX") == 2
     assert _enum("MCG_PRIOR_BOX") == 1
+    assert "c_set_prior ctx 3l" in body and _enum("MCG_PRIOR_DIAG_GAUSS") == 3
 
 
 def _ml_run_opts(fun):
