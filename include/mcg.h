@@ -286,6 +286,13 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
 /* all points of the last nested run (dead in retirement order, then live ascending in ll):
    pts [n_total][D] row-major, ll, lp, log_wts [n_total] (nested_output, nested.ml:20) */
 int mcg_nested_get(mcg_ctx* ctx, double* pts, double* ll, double* lp, double* log_wts);
+/* The last nested run's points as rows in a caller-owned device buffer on the context's device
+   (the send buffer of a replica all-gather over RCCL), device to device: row i of
+   [n_total] = (pts[i][0..D) when with_points, ll[i], lp[i]), `row_stride` doubles apart
+   (>= D + 2 with points, >= 2 without), in nested_output order.  Complete when this returns.
+   Replaces nested_output's host copy for the exchange: only the gathered rows of every
+   replica come back to the host, for mcg_nested_merge. */
+int mcg_nested_rows_into(mcg_ctx* ctx, double* dev_rows, int64_t row_stride, int32_t with_points);
 /* Nested.log_total_error_estimate (nested.ml:148-150) */
 double mcg_log_total_error_estimate(double log_ev, double log_dev, int64_t nlive);
 /* Nested.posterior_samples n (nested.ml:167-178) as indices: the running sums of exp log_wts

@@ -892,6 +892,22 @@ int mcg_nested_get(mcg_ctx* ctx, double* pts, double* ll, double* lp, double* lo
   return MCG_OK;
 }
 
+int mcg_nested_rows_into(mcg_ctx* ctx, double* dev_rows, int64_t row_stride, int32_t with_points) {
+  if (!ctx || !dev_rows) return MCG_EINVAL;
+  const NestedState& R = ctx->nested;
+  if (R.n_total == 0 || !ctx->nested_bufs) return set_error(ctx, MCG_ESTATE, "no nested run");
+  if (row_stride < (with_points ? R.ndim : 0) + 2)
+    return set_error(ctx, MCG_EINVAL, "row_stride %lld < %d", (long long)row_stride, (with_points ? R.ndim : 0) + 2);
+  (void)hipSetDevice(ctx->opts.device);
+  NestedBufs& B = ctx->nested_bufs->b;
+  int rc;
+  if ((rc = hip_check(ctx, launch_nested_rows((const double*)B.dead_x.p, R.ndim_k, R.ndim, (const double*)B.dead_ll.p,
+                                              (const double*)B.dead_lp.p, R.n_total, dev_rows, row_stride,
+                                              with_points ? 1 : 0, ctx->stream), "rows launch")))
+    return rc;
+  return hip_check(ctx, hipStreamSynchronize(ctx->stream), "rows sync");
+}
+
 int mcg_evidence_weights(int64_t ntot, int64_t nlive, int64_t k, const double* ll, int64_t chunk,
                          double* log_ev, double* log_dev, double* log_wts) {
   if (!ll || !log_ev || !log_dev || !log_wts || k < 1 || nlive <= k || ntot < nlive) return MCG_EINVAL;

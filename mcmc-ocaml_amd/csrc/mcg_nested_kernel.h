@@ -937,6 +937,9 @@ hipError_t launch_merge_new(const NestArgs& a, double* out_ll, long long* out_ti
 // the final live rows in key order behind the dead rows
 hipError_t launch_gather_live(const double* x, const double* ll, const double* lp, const int* slot, int64_t n,
                               int D, double* ox, double* oll, double* olp, hipStream_t st);
+// the run's rows (x | ll | lp) into a device buffer of row stride `stride` (mcg_nested_rows_into)
+hipError_t launch_nested_rows(const double* x, int Dk, int D, const double* ll, const double* lp, int64_t n,
+                              double* out, int64_t stride, int pts, hipStream_t st);
 // the walkers' draws of the generation starting at replacement mrep (the first generation's table)
 hipError_t launch_walk_draws(const NestArgs& a, int64_t mrep, hipStream_t st);
 hipError_t launch_check_sorted(const double* ll, const long long* tie, int64_t n, long long gen,

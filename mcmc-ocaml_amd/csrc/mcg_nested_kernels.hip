@@ -843,6 +843,30 @@ hipError_t launch_gather_live(const double* x, const double* ll, const double* l
 }
 
 
+// the run's output rows for a device-side exchange (mcg_nested_rows_into): element e of the
+// [n][ncol] block, ncol = (D if points) + 2; row r = (x[r][0..D) | ll[r], lp[r])
+__global__ void __launch_bounds__(256) nested_rows_kernel(const double* __restrict__ x, int Dk, int D,
+                                                          const double* __restrict__ ll,
+                                                          const double* __restrict__ lp, int64_t n,
+                                                          double* __restrict__ out, int64_t stride, int pts) {
+  const int ncol = (pts ? D : 0) + 2;
+  const int64_t tot = n * ncol;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / ncol;
+    const int c = (int)(e - r * ncol);
+    const int cd = pts ? D : 0;
+    out[r * stride + c] = c < cd ? x[r * Dk + c] : c == cd ? ll[r] : lp[r];
+  }
+}
+
+hipError_t launch_nested_rows(const double* x, int Dk, int D, const double* ll, const double* lp, int64_t n,
+                              double* out, int64_t stride, int pts, hipStream_t s) {
+  const int64_t tot = n * ((pts ? D : 0) + 2);
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((tot + 255) / 256, 16384));
+  hipLaunchKernelGGL(nested_rows_kernel, dim3(grid), dim3(256), 0, s, x, Dk, D, ll, lp, n, out, stride, pts);
+  return hipGetLastError();
+}
+
 __global__ void __launch_bounds__(256) walk_draws_kernel(const NestArgs a, int64_t mrep) {
   walk_draws_fill(a, mrep, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x, kLogTab);
 }

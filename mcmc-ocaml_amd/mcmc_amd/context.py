@@ -147,6 +147,13 @@ class Context:
         num_tiles() x (2D+3) doubles on this context's device), complete on return."""
         self._check(L.lib().mcg_tile_stats_into(self._p, C.c_void_p(int(dev_ptr))))
 
+    def nested_rows_into(self, dev_ptr, row_stride, with_points=True):
+        """The last nested run's rows (pts | ll | lp, or ll | lp) written into a caller-owned
+        device buffer of n_total rows x row_stride doubles (an int device address on this
+        context's device), complete on return (include/mcg.h mcg_nested_rows_into)."""
+        self._check(L.lib().mcg_nested_rows_into(self._p, C.c_void_p(int(dev_ptr)), int(row_stride),
+                                                 int(bool(with_points))))
+
     def stats(self):
         D = self.ndim
         mean = np.zeros(D); sd = np.zeros(D); lz = np.zeros(1)

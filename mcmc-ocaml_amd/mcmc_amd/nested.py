@@ -20,6 +20,27 @@ def nested_evidence(log_likelihood, log_prior, epsrel=0.01, nmcmc=1000, nlive=10
     points=False leaves the points on the device (no D2H copy of n x D doubles; points is None):
     log Z, log dZ, the weights and ll / lp are computed all the same."""
     ctx = ctx or Context(seed=seed)
+    r = run_nested(log_likelihood, log_prior, epsrel, nmcmc, nlive, mode_hopping_frac, k, observer, ctx,
+                   max_dead)
+    return fetch(ctx, r, log_likelihood.ndim, points, k)
+
+
+def fetch(ctx, r, ndim, points=True, k=None):
+    """nested_output of the context's last run (r: its McgNestedResult): mcg_nested_get's copies
+    of the points (points=True), ll, lp and the log weights."""
+    n = r.n_total
+    pts = np.zeros((n, ndim)) if points else None
+    ll = np.zeros(n); lp = np.zeros(n); w = np.zeros(n)
+    L.check(L.lib().mcg_nested_get(ctx.ptr, L.dptr(pts) if points else None, L.dptr(ll), L.dptr(lp),
+                                   L.dptr(w)), ctx.ptr)
+    return NestedOutput(r.log_ev, r.log_dev, pts, w, ll, lp, r.n_dead, r.n_gen, bool(r.converged), k)
+
+
+def run_nested(log_likelihood, log_prior, epsrel=0.01, nmcmc=1000, nlive=1000, mode_hopping_frac=0.1,
+               k=1, observer=None, ctx=None, max_dead=0):
+    """The nested run alone (mcg_nested): its points stay on the device, for mcg_nested_get or a
+    device-side exchange (Context.nested_rows_into).  Returns the McgNestedResult (log_ev,
+    log_dev, n_dead, n_total, n_gen, converged); warns when max_dead ended the run."""
     ctx.set_model(log_likelihood, log_prior, None)
     o = L.McgNestedOpts(nlive, nmcmc, k, epsrel, mode_hopping_frac, max_dead)
     r = L.McgNestedResult()
@@ -35,16 +56,11 @@ def nested_evidence(log_likelihood, log_prior, epsrel=0.01, nmcmc=1000, nlive=10
 
     cb = L.OBSERVER(_obs) if observer is not None else L.OBSERVER()
     L.check(L.lib().mcg_nested(ctx.ptr, C.byref(o), C.byref(r), cb, None), ctx.ptr)
-    n = r.n_total
-    pts = np.zeros((n, D)) if points else None
-    ll = np.zeros(n); lp = np.zeros(n); w = np.zeros(n)
-    L.check(L.lib().mcg_nested_get(ctx.ptr, L.dptr(pts) if points else None, L.dptr(ll), L.dptr(lp),
-                                   L.dptr(w)), ctx.ptr)
     if not r.converged:
         warnings.warn("nested_evidence: max_dead (%d dead points) reached before the stop test "
                       "(nested.ml:45-48) fired; log Z comes from an unconverged run" % r.n_dead,
-                      UnconvergedWarning, stacklevel=2)
-    return NestedOutput(r.log_ev, r.log_dev, pts, w, ll, lp, r.n_dead, r.n_gen, bool(r.converged), k)
+                      UnconvergedWarning, stacklevel=3)
+    return r
 
 
 class UnconvergedWarning(RuntimeWarning):

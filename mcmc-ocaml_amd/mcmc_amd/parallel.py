@@ -112,6 +112,46 @@ def allgather_runs(output, nlive, k, device=None, group=None, points=True):
     return runs
 
 
+def allgather_runs_device(ctx, res, nlive, k, device, group=None, points=True):
+    """allgather_runs from the device: the finished run's rows (pts | ll | lp, or ll | lp) are
+    written by mcg_nested_rows_into straight into a torch device buffer padded to the longest run,
+    which is the send buffer of one all_gather_into_tensor (RCCL over xGMI); only the gathered rows
+    come back to the host, for the merge.  res: the run's McgNestedResult (nested.run_nested).
+    Returns [(output, nlive, k)] in rank order, equal to allgather_runs of the same runs."""
+    import torch
+    import torch.distributed as dist
+    rank, world = _world(group)
+    D = ctx.ndim if points else 0
+    w = D + 2
+    meta = torch.tensor([res.n_total, nlive, k, res.n_gen, int(bool(res.converged))], dtype=torch.int64,
+                        device=device)
+    metas = torch.empty((world, meta.numel()), dtype=torch.int64, device=device)
+    if dist.is_available() and dist.is_initialized():
+        dist.all_gather_into_tensor(metas, meta, group=group)
+    else:
+        metas[0] = meta
+    metas = metas.cpu().numpy()
+    cap = int(metas[:, 0].max())
+    send = torch.zeros((cap, w), dtype=torch.float64, device=device)
+    # the buffer comes from torch's caching allocator: let torch's stream finish with it before
+    # the context's stream writes it
+    torch.cuda.synchronize(device)
+    ctx.nested_rows_into(send.data_ptr(), w, points)
+    if dist.is_available() and dist.is_initialized():
+        recv = torch.empty((world * cap, w), dtype=torch.float64, device=device)
+        dist.all_gather_into_tensor(recv, send, group=group)
+    else:
+        recv = send
+    allr = recv.cpu().numpy().reshape(world, cap, w)
+    runs = []
+    for m, r in zip(metas, allr):
+        r = r[:int(m[0])]
+        run = _nested.NestedOutput(0.0, 0.0, r[:, :D].copy() if points else None, None, r[:, D].copy(),
+                                   r[:, D + 1].copy(), int(m[0] - m[1]), int(m[3]), bool(m[4]))
+        runs.append((run, int(m[1]), int(m[2])))
+    return runs
+
+
 def replica_sizes(nlive, k, world):
     """(live points, points retired per generation) of one of `world` replicas: nlive / world
     live points, k clamped to what mcg_nested accepts (1 <= k < nlive, k <= MAX_K)."""
@@ -137,17 +177,29 @@ def nested_evidence_replicas(log_likelihood, log_prior, epsrel=0.01, nmcmc=1000,
         warnings.warn("nested_evidence_replicas: k = %d retired per generation cannot run on "
                       "%d live points per replica; using k = %d (recorded as .k)" % (k, nl, kk),
                       RuntimeWarning, stacklevel=2)
+    # RCCL (comm_device set) with several ranks: the exchange reads the run's rows on the device
+    # (allgather_runs_device); otherwise (one rank, or a gloo rehearsal) the host copy is used
+    dev_x = world > 1 and comm_device is not None
     with Context(seed=replica_seed(seed, rank), device=device) as ctx:
-        out = _nested.nested_evidence(log_likelihood, log_prior, epsrel=epsrel, nmcmc=nmcmc,
-                                      nlive=nl, mode_hopping_frac=mode_hopping_frac, k=kk, ctx=ctx,
-                                      points=points)
+        if dev_x:
+            res = _nested.run_nested(log_likelihood, log_prior, epsrel=epsrel, nmcmc=nmcmc, nlive=nl,
+                                     mode_hopping_frac=mode_hopping_frac, k=kk, ctx=ctx)
+            runs = allgather_runs_device(ctx, res, nl, kk, comm_device, group, points=points)
+            out = runs[rank][0]
+            out = _nested.NestedOutput(res.log_ev, res.log_dev, out[2], None, out.ll, out.lp,
+                                       res.n_dead, res.n_gen, bool(res.converged))
+        else:
+            out = _nested.nested_evidence(log_likelihood, log_prior, epsrel=epsrel, nmcmc=nmcmc,
+                                          nlive=nl, mode_hopping_frac=mode_hopping_frac, k=kk, ctx=ctx,
+                                          points=points)
     if os.environ.get("MCG_DEBUG_REPLICAS"):
         print("replica rank %d: log Z %.6f n_dead %d n_gen %d" % (rank, out[0], out.n_dead, out.n_gen),
               file=sys.stderr, flush=True)
     if world == 1:
         out.k = kk
         return out
-    runs = allgather_runs(out, nl, kk, comm_device, group, points=points)
+    if not dev_x:
+        runs = allgather_runs(out, nl, kk, comm_device, group, points=points)
     merged = _nested.merge_runs(runs)
     if os.environ.get("MCG_DEBUG_REPLICAS"):
         for i, (o, a, b) in enumerate(runs):

@@ -6,7 +6,9 @@ RCCL's own kernels) carries
     a torch device buffer (mcg_tile_stats_into) that is the send buffer of all_gather_into_tensor,
     and the host folds the gathered tiles -- bit-identical to the host path (mcg_tile_stats +
     mcg_combine_tiles);
-  - the nested replica exchange (allgather_runs): counts, then the padded (pts | ll | lp) rows.
+  - the nested replica exchange (allgather_runs): counts, then the padded (pts | ll | lp) rows --
+    from host copies, or from the device (allgather_runs_device: mcg_nested_rows_into writes the
+    run's rows into the RCCL send buffer), bit-identical.
 
 The 2-rank versions of both run on gloo in tests/test_distributed.py."""
 import math
@@ -68,3 +70,34 @@ def test_nested_run_allgather_over_rccl(rccl):
     np.testing.assert_array_equal(got.lp, out.lp)
     merged = nested.merge_runs(runs)
     np.testing.assert_array_equal(merged.ll, out.ll)
+
+
+@pytest.mark.parametrize("points", [True, False])
+def test_nested_device_allgather_equals_host_path(rccl, points):
+    """The device-resident replica exchange (mcg_nested_rows_into -> all_gather_into_tensor) gives
+    the host path's runs bit for bit, and the same merge; D 3 pads to the kernel width 4, so the
+    rows are the caller's dims only."""
+    from mcmc_amd import Context, nested, targets as T
+    from mcmc_amd.parallel import allgather_runs, allgather_runs_device
+    D = 3
+    lik = T.gauss_shell(np.zeros(D), 1.0, 0.2)
+    pri = T.box(-2 * np.ones(D), 2 * np.ones(D))
+    with Context(seed=11) as ctx:
+        res = nested.run_nested(lik, pri, nlive=300, nmcmc=15, k=8, ctx=ctx)
+        host = nested.fetch(ctx, res, D, points=points, k=8)
+        dev_runs = allgather_runs_device(ctx, res, 300, 8, rccl, points=points)
+    host_runs = allgather_runs(host, 300, 8, device=rccl, points=points)
+    assert len(dev_runs) == len(host_runs) == 1
+    (d, dn, dk), (h, hn, hk) = dev_runs[0], host_runs[0]
+    assert (dn, dk) == (hn, hk) == (300, 8)
+    assert d.n_dead == h.n_dead == res.n_dead and d.n_gen == h.n_gen == res.n_gen
+    np.testing.assert_array_equal(d.ll, host.ll)
+    np.testing.assert_array_equal(d.lp, host.lp)
+    if points:
+        np.testing.assert_array_equal(d[2], host[2])
+    else:
+        assert d[2] is None
+    a, b = nested.merge_runs(dev_runs), nested.merge_runs(host_runs)
+    np.testing.assert_array_equal(a.ll, b.ll)
+    np.testing.assert_array_equal(a[3], b[3])
+    assert a[0] == b[0]
