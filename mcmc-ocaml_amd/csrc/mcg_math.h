@@ -279,6 +279,18 @@ __device__ __forceinline__ void pnormal4_lds(const u32x4 w, const double2* tab, 
   }
   double2 a0, a1, a2, a3, b0, b1, b2, b3;
   static_assert(kNrmSeg * 16 == 16384, "second half of the table at offset 16384");
+#if defined(MCG_PROBE_NRM_BCAST)
+  // timing probe (wrong values): every lane gathers row 0 -- the same gathers, broadcast, no
+  // bank conflicts
+#pragma unroll
+  for (int k = 0; k < 4; ++k) ad[k] = base + (ad[k] & 0x80000000u);
+#endif
+#if defined(MCG_PROBE_NRM_NOLDS)
+  // timing probe (wrong values): no table gathers at all, coefficients from the operand
+  a0 = a1 = a2 = a3 = double2{xp[0], 0.5};
+  b0 = b1 = b2 = b3 = double2{xp[1], 0.25};
+  if (0)
+#endif
   asm volatile(
       "ds_read_b128 %0, %8\n\t"
       "ds_read_b128 %4, %8 offset:16384\n\t"
