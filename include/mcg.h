@@ -51,7 +51,12 @@ enum {
    FLAT          : (none)                 ll = 0
    GAUSS_MIX     : m, then per component  ll = log (sum_i exp g_i), g_i = Stats.log_multi_gaussian
                    mu_i[D], sigma_i[D]    mu_i sigma_i x: the multimodal target of
-                                          test/nested_test.ml:41-64 (1 <= m <= MCG_LIK_MIX_MAX)
+                                          test/nested_test.ml:41-64 (1 <= m <= MCG_LIK_MIX_MAX);
+                                          summed max-shifted, so where every g_i < ~-745 the
+                                          result is finite while the reference's literal
+                                          log (exp g1 + ...) underflows to -inf (its own test,
+                                          D = 2, never gets there; the oracle's literal mode
+                                          restates the reference's form)
    Any ndim >= 1 works for FLAT, DIAG_GAUSS, GAUSS_SHELL and GAUSS_MIX (FULLCOV_GAUSS: ndim <= 64):
    a dimension without compiled kernels runs on the next compiled width with zero-padded dims
    (zero likelihood terms, zero proposal steps, unbounded box); the padding never crosses this
@@ -158,6 +163,11 @@ int mcg_kd_export(mcg_ctx* ctx, int32_t* node_dim, double* node_split, int32_t* 
 int mcg_init(mcg_ctx* ctx, int64_t nchains, const double* x_soa, const double* ll,
              const double* lp);
 int mcg_get_state(mcg_ctx* ctx, double* x_soa, double* ll, double* lp);
+/* a counter that every entry point which may change the context's chains, model or RNG bumps
+   (mcg_init, mcg_run, the mcg_set_* calls, mcg_nested, mcg_reseed, the RJ calls, ...): a host
+   binding that keeps the chains device-resident between its own calls (the OCaml
+   make_mcmc_sampler) skips the upload only while the token is the one it saw last */
+uint64_t mcg_state_token(const mcg_ctx* ctx);
 
 /* ---- Mcmc.mcmc_array (mcmc.ml:58-72) over every chain ----
    nbin burn-in steps, record 0 = post-burn-in state, then (n_rec-1)*nskip steps recording

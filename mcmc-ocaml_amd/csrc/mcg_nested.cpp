@@ -274,6 +274,7 @@ extern "C" {
 int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res,
                mcg_observer_fn observer, void* user) {
   if (!ctx || !opts) return MCG_EINVAL;
+  ++ctx->state_token;
   // D: the kernel width of the live rows [n][D] (the caller's ndim Dr, zero-padded to a
   // compiled width; the padding is stripped from every point handed back)
   const int D = ctx->Dk, Dr = ctx->D;
@@ -464,24 +465,15 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
     HC(hipMemsetAsync(B.trace.p, 0, 4 * 1024 * 8 * 8, s), "clear trace");
   }
 #endif
-  // Dead buffers replaced while batches were in flight, tagged with the sequence number of the
-  // batch whose launch replaced them.  Once that batch is done, every kernel and grow copy that
-  // touched the old buffer has finished (stream order), and so has the earlier batch whose
-  // observer copy may read it (batches are handled in launch order): it is freed then (ADVICE
-  // r3), the rest when the run ends.
+  // Dead buffers replaced while batches were in flight (tagged with the sequence number of the
+  // batch whose launch replaced them) are freed when the run ends, after the stream has drained.
+  // Not earlier: they come from hipMalloc, and a hipFree mid-run would wait for the batches in
+  // flight (undoing the refill-before-join overlap), while hipFreeAsync is specified for
+  // stream-ordered pool allocations only.  The buffers double in size at each grow,
+  // so the retired ones hold at most as much as the live one.
   struct RetiredBufs {
     hipStream_t s;
     std::vector<std::pair<int64_t, void*>> bufs;
-    // (a stream-ordered free: hipFree would wait for the batch in flight; where the runtime
-    // refuses hipFreeAsync on this allocation the buffer stays listed until the end)
-    void release_upto(int64_t seq) {
-      size_t w = 0;
-      for (auto& e : bufs) {
-        if (e.first <= seq && hipFreeAsync(e.second, s) == hipSuccess) continue;
-        bufs[w++] = e;
-      }
-      bufs.resize(w);
-    }
     ~RetiredBufs() {
       if (bufs.empty()) return;
       (void)hipStreamSynchronize(s);
@@ -636,7 +628,6 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
       R.lp.insert(R.lp.end(), B.h_stage[2 * q + 1], B.h_stage[2 * q + 1] + (d1 - d0));
     }
     const double* done_dead_x = slot_dead_x[q];      // (before the refill below replaces it)
-    const int64_t done_seq = slot_seq[q];
     const int64_t remaining = max_dead / k - gen;
     if (!st.stopped && remaining > 0) {               // the slot is free again: refill it
       batch = std::min<int64_t>(batch * 2, kMaxBatch);
@@ -656,7 +647,6 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
       observer(user, hx.data(), R.ll.data() + reported, R.lp.data() + reported, m);
       reported = ndead;
     }
-    retired_dead.release_upto(done_seq);
     // the refill above went out before this join: the fold of the last batch never holds up the
     // GPU's next batch
     join_fold();

@@ -37,6 +37,7 @@ int hip_check(mcg_ctx* ctx, hipError_t e, const char* what) {
 // Host-side writes to context buffers (blocking copies, frees) do not order against the
 // context's non-blocking stream: every entry point that rewrites them drains the stream first.
 int quiesce(mcg_ctx* ctx) {
+  ++ctx->state_token;                 // every entry point that may change the context's state
   if (!ctx->stream) return MCG_OK;
   return hip_check(ctx, hipStreamSynchronize(ctx->stream), "drain context stream");
 }
@@ -463,10 +464,16 @@ int mcg_set_likelihood(mcg_ctx* ctx, int32_t kind, int32_t ndim, const double* p
   int prc = pack_likelihood(ctx, kind, D, params, n, dev, &is_cauchy, &data_n);
   if (prc) return prc;
   const int Dk = pad_width(kind, D);
-  if (ctx->D != 0 && (ctx->D != D || ctx->Dk != Dk) && ctx->N > 0)
-    return set_error(ctx, MCG_ESTATE, "ndim changed after mcg_init");
+  if (ctx->D != 0 && ctx->D != D && ctx->N > 0)
+    return set_error(ctx, MCG_ESTATE, "ndim changed after mcg_init (%d -> %d): call mcg_init again", ctx->D, D);
+  if (ctx->D != 0 && ctx->Dk != Dk && ctx->N > 0)
+    return set_error(ctx, MCG_ESTATE,
+                     "likelihood kind %d runs ndim %d at kernel width %d, the chains on the device were "
+                     "initialised at width %d: call mcg_init again after changing the kind",
+                     kind, D, Dk, ctx->Dk);
   dev = pad_lik(kind, D, Dk, dev);
   ctx->rj_active = false;
+  const bool ndim_changed = ctx->D != D;
   // the proposal and prior descriptors are laid out at the old width: re-set them below
   const bool width_changed = ctx->Dk != Dk || ctx->D != D;
   ctx->D = D;
@@ -479,13 +486,25 @@ int mcg_set_likelihood(mcg_ctx* ctx, int32_t kind, int32_t ndim, const double* p
   if (rc) return rc;
   rc = hip_check(ctx, hipMemcpy(ctx->d_lik.p, dev.data(), dev.size() * 8, hipMemcpyHostToDevice), "copy likelihood");
   if (rc) return rc;
-  // keep a padded flat prior / default proposal consistent with D
+  // the prior and proposal at the new width: the same ndim (only the padding moved) keeps the
+  // caller's prior and (Gaussian, wrapping or mixture) proposal, re-laid out; a new ndim starts
+  // from a flat prior and the default proposal
+  const bool same_ndim = ctx->pri_host.size() > 0 && ctx->prior_raw_kind >= 0 && !ndim_changed;
   if (width_changed || ctx->pri_host.size() != (size_t)(4 * Dk + 1)) {
-    double z = 0.0;
-    rc = mcg_set_prior(ctx, MCG_PRIOR_FLAT, &z, 0);
+    if (same_ndim) {
+      const std::vector<double> raw = ctx->prior_raw;
+      const double z = 0.0;
+      rc = mcg_set_prior(ctx, ctx->prior_raw_kind, raw.empty() ? &z : raw.data(), raw.size());
+    } else {
+      double z = 0.0;
+      rc = mcg_set_prior(ctx, MCG_PRIOR_FLAT, &z, 0);
+    }
     if (rc) return rc;
   }
-  if (width_changed) {
+  if (width_changed && same_ndim && ctx->prop_raw_kind >= 0) {
+    const std::vector<double> raw = ctx->prop_raw;
+    if ((rc = mcg_set_proposal(ctx, ctx->prop_raw_kind, raw.data(), raw.size()))) return rc;
+  } else if (width_changed) {
     // every proposal descriptor (and a kD tree) was laid out for the old ndim -- a DE proposal
     // over samples of the old width would read past its rows: back to the default proposal, a
     // unit Gaussian step at the new width, until the caller sets one of this ndim
@@ -561,6 +580,8 @@ int mcg_set_prior(mcg_ctx* ctx, int32_t kind, const double* params, size_t n) {
   if (kind == MCG_PRIOR_DIAG_GAUSS) dev = pad_gauss_prior(D, ctx->Dk, dev);
   else dev = pad_prior(D, ctx->Dk, dev, 0.0, 0.0);
   ctx->prior_kind = kind;
+  ctx->prior_raw_kind = kind;
+  ctx->prior_raw.assign(params ? params : dev.data(), params ? params + n : dev.data());
   ctx->pri_host = dev;
   int rc = hip_check(ctx, ctx->d_pri.ensure(dev.size() * 8), "alloc prior");
   if (rc) return rc;
@@ -605,6 +626,11 @@ int mcg_set_proposal(mcg_ctx* ctx, int32_t kind, const double* params, size_t n)
   }
   ctx->prop_kind = kind;
   ctx->prop_host = dev;
+  // (re-laid out at another kernel width from these; DE and kD need their samples / tree)
+  const bool relayable = kind == MCG_PROP_GAUSS || kind == MCG_PROP_WRAP_UNIFORM ||
+                         (kind == MCG_PROP_MIXTURE && !ctx->kd.built);
+  ctx->prop_raw_kind = relayable ? kind : -1;
+  if (relayable) ctx->prop_raw.assign(params, params + n);
   int rc = hip_check(ctx, ctx->d_prop.ensure(dev.size() * 8), "alloc proposal");
   if (rc) return rc;
   return hip_check(ctx, hipMemcpy(ctx->d_prop.p, dev.data(), dev.size() * 8, hipMemcpyHostToDevice), "copy proposal");
@@ -812,7 +838,10 @@ int choose_lanes(mcg_ctx* ctx) {
 
 extern "C" {
 
+uint64_t mcg_state_token(const mcg_ctx* ctx) { return ctx ? ctx->state_token : 0; }
+
 int mcg_run(mcg_ctx* ctx, const mcg_run_opts* o) {
+  if (ctx) ++ctx->state_token;
   if (!ctx || !o) return MCG_EINVAL;
   if (ctx->N < 1) return set_error(ctx, MCG_ESTATE, "mcg_run before mcg_init");
   if (o->nskip < 1 || o->n_rec < 0 || o->nbin < 0) return set_error(ctx, MCG_EINVAL, "nbin >= 0, nskip >= 1, n_rec >= 0");

@@ -61,9 +61,15 @@ struct mcg_ctx {
   int D = 0;
   int Dk = 0;
   int32_t lik_kind = -1, prior_kind = MCG_PRIOR_FLAT, prop_kind = MCG_PROP_GAUSS;
+  uint64_t state_token = 0;              // bumped by every state-changing entry point (mcg_state_token)
   int32_t is_cauchy = 0;
   int64_t data_n = 0;
   std::vector<double> lik_host, pri_host, prop_host;
+  // the caller's (unpadded) prior and proposal parameters: re-laid out at a new kernel width when
+  // a likelihood of another kind pads the same ndim differently (prop_raw_kind -1: a proposal
+  // that cannot be re-laid out from parameters alone -- kD tree, DE samples)
+  int32_t prior_raw_kind = MCG_PRIOR_FLAT, prop_raw_kind = -1;
+  std::vector<double> prior_raw, prop_raw;
   mcg::DevBuf d_lik, d_pri, d_prop;
   mcg::KdState kd;
   mcg::DevBuf d_de_pts;          // differential_evolution_proposal samples [M][D]

@@ -1,4 +1,5 @@
 """Mirror of the reference's Nested module (nested.mli) over the HIP sampler."""
+import atexit
 import ctypes as C
 import warnings
 
@@ -134,34 +135,49 @@ def log_total_error_estimate(log_ev, log_dev, nlive):
 _default_ctx = {}
 
 
-def _posterior_context(seed):
-    """The context posterior draws use when the caller passes none: one per seed for the
-    process, so repeated calls advance its draw counter and return new samples, as the
-    reference's global Random state does (a fresh context per call would replay call 0)."""
-    c = _default_ctx.get(seed)
+def _close_default_contexts():
+    for c in list(_default_ctx.values()):
+        try:
+            c.close()
+        except Exception:
+            pass
+    _default_ctx.clear()
+
+
+atexit.register(_close_default_contexts)
+
+
+def _posterior_context(seed, device=0):
+    """The context posterior draws use when the caller passes none: one per (seed, device) for
+    the process, so repeated calls advance its draw counter and return new samples, as the
+    reference's global Random state does (a fresh context per call would replay call 0).  Closed
+    at interpreter exit, before the HIP runtime is torn down."""
+    key = (int(seed), int(device))
+    c = _default_ctx.get(key)
     if c is None:
-        c = _default_ctx[seed] = Context(seed=seed)
+        c = _default_ctx[key] = Context(seed=seed, device=device)
     return c
 
 
-def posterior_indices(n, log_wts, ctx=None, seed=0):
+def posterior_indices(n, log_wts, ctx=None, seed=0, device=0):
     """The draws of Nested.posterior_samples (nested.ml:167-178) as indices into the points:
     cumulative weights and the reference's weight_binary_search_index (:152-165) on the device,
     one Philox draw per sample (include/mcg.h mcg_posterior_samples).  Repeated calls on one
     context -- the caller's, or without one the process-wide context of `seed` -- draw new
     samples (the reference's global Random state advances)."""
-    ctx = ctx or _posterior_context(seed)
+    ctx = ctx or _posterior_context(seed, device)
     w = np.ascontiguousarray(log_wts, dtype=np.float64)
     idx = np.zeros(int(n), np.int64)
     L.check(L.lib().mcg_posterior_samples(ctx.ptr, L.dptr(w), len(w), int(n), L.i64ptr(idx)), ctx.ptr)
     return idx
 
 
-def posterior_samples(n, output, ctx=None, seed=0):
+def posterior_samples(n, output, ctx=None, seed=0, device=0):
     """Nested.posterior_samples n output (nested.ml:167-178): n points resampled by weight from a
-    nested_output (points (npts, D) and log weights)."""
+    nested_output (points (npts, D) and log weights); without a ctx, the process-wide context of
+    (seed, device) draws them."""
     _, _, pts, log_wts = output[:4]
     if pts is None:
         raise ValueError("posterior_samples needs the points: run nested_evidence with points=True")
     assert len(pts) == len(log_wts)                 # nested.ml:169
-    return np.asarray(pts)[posterior_indices(n, log_wts, ctx, seed)]
+    return np.asarray(pts)[posterior_indices(n, log_wts, ctx, seed, device)]

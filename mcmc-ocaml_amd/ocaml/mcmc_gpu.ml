@@ -69,6 +69,7 @@ let c_nested_get = fn "mcg_nested_get" (ptr void @-> ptr double @-> ptr double @
 let c_log_total_error = fn "mcg_log_total_error_estimate" (double @-> double @-> int64_t @-> returning double)
 let c_set_de = fn "mcg_set_de_proposal" (ptr void @-> ptr double @-> int64_t @-> double @-> returning int)
 let c_get_state = fn "mcg_get_state" (ptr void @-> ptr double @-> ptr double @-> ptr double @-> returning int)
+let c_state_token = fn "mcg_state_token" (ptr void @-> returning uint64_t)
 let c_posterior = fn "mcg_posterior_samples" (ptr void @-> ptr double @-> int64_t @-> int64_t @-> ptr int64_t @-> returning int)
 (* mcg_observer_fn: void (void* user, const double* pts, const double* ll, const double* lp, int64_t n) *)
 let observer_t = ptr void @-> ptr double @-> ptr double @-> ptr double @-> int64_t @-> returning void
@@ -194,15 +195,28 @@ let set_model ctx lik pri prop =
 type state = mat * vec * vec
 
 (* Mcmc.make_mcmc_sampler (mcmc.ml:37-56) over a batch of chains: one MH step per call.  The
-   chains stay on the device between calls: when the argument is the state this sampler returned
-   last, the step runs from the device copy (mcg_run + mcg_get_state, no mcg_init upload). *)
+   chains stay on the device between calls: the step runs from the device copy (mcg_run +
+   mcg_get_state, no mcg_init upload) only when all of these hold -- the argument is the state
+   this sampler returned last (physically), its contents still equal the sampler's private
+   snapshot of it (a caller may mutate the returned Bigarrays in place), and the context's state
+   token (mcg_state_token) is the one seen right after that step (no other sampler, mcmc_array,
+   nested run or model change used the context in between).  Otherwise the state is uploaded. *)
 let make_mcmc_sampler ctx lik pri prop =
   set_model ctx lik pri (Some prop);
   let last = ref None in
+  let copy2 (a : mat) = let b = Bigarray.Array2.create Bigarray.float64 Bigarray.c_layout
+                                (Bigarray.Array2.dim1 a) (Bigarray.Array2.dim2 a) in
+    Bigarray.Array2.blit a b; b in
+  let copy1 (a : vec) = let b = Bigarray.Array1.create Bigarray.float64 Bigarray.c_layout
+                                (Bigarray.Array1.dim a) in
+    Bigarray.Array1.blit a b; b in
   fun ((x : mat), (ll : vec), (lp : vec)) ->
     let d = Bigarray.Array2.dim1 x and nch = Bigarray.Array2.dim2 x in
     let resident = match !last with
-      | Some (x0, ll0, lp0) -> x == x0 && ll == ll0 && lp == lp0
+      | Some ((x0, ll0, lp0), (sx, sll, slp), tok) ->
+        x == x0 && ll == ll0 && lp == lp0
+        && Unsigned.UInt64.equal tok (c_state_token ctx)
+        && x = sx && ll = sll && lp = slp
       | None -> false in
     if not resident then
       check ctx (c_init ctx (Int64.of_int nch) (bigarray_start array2 x) (bigarray_start array1 ll)
@@ -215,7 +229,7 @@ let make_mcmc_sampler ctx lik pri prop =
     let x' = Array2.create float64 c_layout d nch in
     let ll' = Array1.create float64 c_layout nch and lp' = Array1.create float64 c_layout nch in
     check ctx (c_get_state ctx (bigarray_start array2 x') (bigarray_start array1 ll') (bigarray_start array1 lp'));
-    last := Some (x', ll', lp');
+    last := Some ((x', ll', lp'), (copy2 x', copy1 ll', copy1 lp'), c_state_token ctx);
     (x', ll', lp')
 
 let reset_counters ctx = check ctx (c_reset_counters ctx)

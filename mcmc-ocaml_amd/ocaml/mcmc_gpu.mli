@@ -68,7 +68,10 @@ type state = mat * vec * vec
 
 (** Mcmc.make_mcmc_sampler (mcmc.mli:58-60) over a batch: sets the model on [ctx] and returns the
     step function; each call advances every chain of the state by one MH step (a rejected chain
-    keeps its state, mcmc.ml:55) and continues the context's Philox stream. *)
+    keeps its state, mcmc.ml:55) and continues the context's Philox stream.  Fed back the state
+    it returned last, unmodified, with nothing else run on [ctx] in between (mcg_state_token), a
+    step reuses the device-resident chains; any other argument -- a new state, or the returned
+    Bigarrays mutated in place -- is uploaded first. *)
 val make_mcmc_sampler : ctx -> likelihood -> prior -> proposal -> (state -> state)
 
 (** Mcmc.reset_counters / get_counters (mcmc.mli:29-30) for this context. *)

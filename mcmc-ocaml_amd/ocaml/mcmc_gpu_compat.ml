@@ -20,27 +20,29 @@ let reset_counters () = Mcmc_gpu.reset_counters (Lazy.force default_ctx)
 let get_counters () = Mcmc_gpu.get_counters (Lazy.force default_ctx)
 
 (* Mcmc.make_mcmc_sampler (mcmc.mli:58-60) with descriptors for the four closures: a function of
-   one sample returning the next; a rejected step returns the same physical record (mcmc.ml:55).
-   Fed back its own last result (the usual loop), the step reuses the device-resident chain
-   instead of uploading the record again. *)
+   one sample returning the next; a rejected step returns the same physical record (mcmc.ml:55),
+   decided by the step's accept count (Mcmc_gpu.get_counters before / after), not by comparing
+   values.  Fed back its own last result (the usual loop) with its value array unmodified, the
+   step reuses the device-resident chain (Mcmc_gpu.make_mcmc_sampler checks the context's state
+   token and its own snapshot too) instead of uploading the record again. *)
 let make_mcmc_sampler ?ctx lik pri prop =
   let ctx = match ctx with Some c -> c | None -> Lazy.force default_ctx in
   let step = Mcmc_gpu.make_mcmc_sampler ctx lik pri prop in
   let last = ref None in
   fun (s : float array Mcmc.mcmc_sample) ->
     let state = match !last with
-      | Some (r, st) when r == s -> st
+      | Some (r, v0, st) when r == s && s.Mcmc.value = v0 -> st
       | _ ->
         let d = Array.length s.Mcmc.value in
         let x = Array2.create float64 c_layout d 1 in
         Array.iteri (fun i v -> x.{i, 0} <- v) s.Mcmc.value;
         (x, Array1.of_array float64 c_layout [| s.Mcmc.like_prior.Mcmc.log_likelihood |],
          Array1.of_array float64 c_layout [| s.Mcmc.like_prior.Mcmc.log_prior |]) in
+    let (acc0, _) = Mcmc_gpu.get_counters ctx in
     let (x', ll', lp') as st' = step state in
-    let v = column x' 0 in
-    let r = if v = s.Mcmc.value && ll'.{0} = s.Mcmc.like_prior.Mcmc.log_likelihood then s
-      else sample v ll'.{0} lp'.{0} in
-    last := Some (r, st');
+    let (acc1, _) = Mcmc_gpu.get_counters ctx in
+    let r = if acc1 = acc0 then s else sample (column x' 0) ll'.{0} lp'.{0} in
+    last := Some (r, Array.copy r.Mcmc.value, st');
     r
 
 (* Mcmc.mcmc_array ?nbin ?nskip n ... start (mcmc.mli:70-72): [chains] copies of [start] run

@@ -205,3 +205,64 @@ def test_last_run_lanes_reports_the_lane_split(T):
             ctx.run(nbin=4, nskip=1, n_rec=1, record_x=False, record_llp=False,
                     record_accept=False, accumulate=False)
             assert ctx.lanes() == expect
+
+
+def test_state_token_moves_with_every_state_change(T):
+    """mcg_state_token (include/mcg.h): bumped by init, run, the setters, a nested run and reseed;
+    unchanged by reads (state, counters, records).  The OCaml sampler keeps the chains resident
+    only while it is unchanged since its own step."""
+    import mcmc_amd._lib as L
+    from mcmc_amd import Context, nested
+    lik, pri, prop, mu, sg = c2_model(T)
+    tok = lambda c: int(L.lib().mcg_state_token(c.ptr))
+    with Context(seed=3) as ctx:
+        ctx.set_model(lik, pri, prop)
+        t0 = tok(ctx)
+        ctx.init(np.random.default_rng(0).normal(mu[:, None], sg[:, None], size=(8, 64)))
+        t1 = tok(ctx)
+        ctx.run(nbin=2, nskip=1, n_rec=0, record_x=False, record_llp=False)
+        t2 = tok(ctx)
+        ctx.state(); ctx.counters(); ctx.sync()
+        assert tok(ctx) == t2
+        ctx.set_model(lik, pri, prop)
+        t3 = tok(ctx)
+        nested.nested_evidence(T.diag_gauss(mu, sg), pri, nlive=50, nmcmc=5, k=1, ctx=ctx, max_dead=20)
+        t4 = tok(ctx)
+        L.check(L.lib().mcg_reseed(ctx.ptr, 5), ctx.ptr)
+        t5 = tok(ctx)
+        assert t0 < t1 < t2 < t3 < t4 < t5
+
+
+def test_likelihood_kind_change_keeps_prior_and_proposal(oracle, T):
+    """at ndim 9 DIAG_GAUSS pads to width 12 and FULLCOV_GAUSS to 16.  Changing the
+    kind before mcg_init keeps the caller's box prior and Gaussian proposal (re-laid out at the
+    new width) instead of resetting them to FLAT / GAUSS(1): the run equals the oracle's with
+    that prior and proposal.  After mcg_init the change is refused with an error naming the
+    kernel widths."""
+    import mcmc_amd._lib as L
+    from mcmc_amd import Context
+    D = 9
+    rng = np.random.default_rng(9)
+    mu, sg = rng.uniform(-0.5, 0.5, D), rng.uniform(0.5, 1.5, D)
+    A = rng.normal(size=(D, D))
+    cov = A @ A.T / D + np.eye(D)
+    lo, hi = -1.5 * np.ones(D), 1.5 * np.ones(D)
+    pri, prop = T.box(lo, hi), T.gauss(0.6)
+    fc = T.fullcov_gauss(mu, cov)
+    x0 = rng.uniform(-1, 1, size=(D, 80))
+    with Context(seed=12) as ctx:
+        ctx.set_model(T.diag_gauss(mu, sg), pri, prop)
+        ctx.set_model(fc)                        # likelihood only: prior and proposal stay
+        ctx.init(x0)
+        ctx.run(nbin=0, nskip=1, n_rec=30, record_x=True, record_llp=True, record_accept=True)
+        rx, rll, rlp, bits = ctx.records(x=True, llp=True, accept=True)
+        m = oracle.Model(D, fc.kind, fc.params, pri.kind, pri.params, prop.kind, prop.params)
+        ll0 = np.array([m.loglik(x0[:, i]) for i in range(80)])
+        lp0 = np.array([m.logprior(x0[:, i]) for i in range(80)])
+        o = oracle.mh_run(m, 12, x0, ll0, lp0, nbin=0, nskip=1, n_rec=30, nthreads=8)
+        np.testing.assert_array_equal(rx, o["rec_x"])
+        np.testing.assert_array_equal(rlp, o["rec_lp"])
+        np.testing.assert_array_equal(bits, o["bits"])
+        assert np.all(np.abs(rx) <= 1.5)
+        with pytest.raises(L.McgError, match="kernel width 12"):
+            ctx.set_model(T.diag_gauss(mu, sg))

@@ -175,3 +175,19 @@ def test_gauss_mix_packing_matches_targets():
     d = targets.gauss_mix(mus, sg)
     assert d.params[0] == 2
     np.testing.assert_array_equal(d.params[1:], np.concatenate([mus[0], sg[0], mus[1], sg[1]]))
+
+
+def test_sampler_residency_is_tied_to_the_context_token():
+    """the OCaml make_mcmc_sampler skips the mcg_init upload only when the argument is
+    its last result (physically), still equal to its private snapshot, and the context's state
+    token is unchanged since its own step; the compat layer decides accept / reject by the step's
+    accept count, not by comparing values."""
+    body = ML[ML.index("let make_mcmc_sampler"):ML.index("let reset_counters")]
+    assert "c_state_token ctx" in body and "Unsigned.UInt64.equal tok" in body
+    assert "x = sx && ll = sll && lp = slp" in body
+    assert re.search(r'fn "mcg_state_token" \(ptr void @-> returning uint64_t\)', ML)
+    assert "uint64_t mcg_state_token(const mcg_ctx* ctx);" in HDR
+    compat = (ROOT / "mcmc-ocaml_amd" / "ocaml" / "mcmc_gpu_compat.ml").read_text()
+    c = compat[compat.index("let make_mcmc_sampler"):compat.index("let mcmc_array")]
+    assert "Mcmc_gpu.get_counters ctx" in c and "if acc1 = acc0 then s" in c
+    assert "s.Mcmc.value = v0" in c
