@@ -216,11 +216,18 @@ static_assert(kNrmTabN == 2 * kNrmSeg, "normal table: two rows per segment");
 
 // (w << 1) | 1 and (hi & 0x7FFF) | 0x3FF00000 as single VALU ops (hipcc emits shift + or pairs)
 __device__ __forceinline__ uint32_t nrm_odd(uint32_t w) {
+#ifdef MCG_NRM_NOASM
+  return (w << 1) | 1u;
+#else
   uint32_t r;
   asm("v_lshl_or_b32 %0, %1, 1, 1" : "=v"(r) : "v"(w));
   return r;
+#endif
 }
 __device__ __forceinline__ uint32_t nrm_frac_hi(uint32_t hi) {
+#ifdef MCG_NRM_NOASM
+  return (hi & 0x7FFFu) | 0x3FF00000u;
+#endif
   uint32_t r;
   // gfx9 VOP3: no literal operand and one scalar operand, so the mask comes in a VGPR
   asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(hi), "v"(0x7FFFu), "s"(0x3FF00000u));
@@ -253,8 +260,12 @@ __device__ __forceinline__ double pnormal_finish(const NrmPending& q) {
   p = fma(p, q.x, q.c10.x);
   p = fma(p, q.x, q.c10.y);
   // p_hi ^ (w & 0x80000000): the sign of the word flips z
+#ifdef MCG_NRM_NOASM
+  const uint32_t h = (uint32_t)__double2hiint(p) ^ (q.sign & 0x80000000u);
+#else
   uint32_t h;
   asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x6c" : "=v"(h) : "v"(q.sign), "v"(__double2hiint(p)), "s"(0x80000000u));
+#endif
   return __hiloint2double((int)h, __double2loint(p));
 }
 __device__ __forceinline__ double pnormal(uint32_t w, const double2* tab) {

@@ -379,6 +379,10 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   if (const char* e = std::getenv("MCG_NEST_LANES"))
     a.lanes_hint = !std::strcmp(e, "wide") ? -1 : !std::strcmp(e, "narrow") ? -2 : std::atoi(e);
   a.fuse_retire = a.est_in_rank && !retire_kernel;
+  // k <= 4096 with the draw table: the merge runs in the walk's launch (nest_walk_kernel's merge
+  // role, one kernel boundary a generation instead of two); MCG_NESTED_FM=0 keeps two launches
+  const char* fm_env = std::getenv("MCG_NESTED_FM");
+  const bool fuse_walk_merge = fused_merge && k <= 4096 && !(fm_env && fm_env[0] == '0');
   // the walkers' draws of a generation in a table the previous merge fills (when it fits)
   a.rt_ix = nullptr;
   a.rt_sc = nullptr;
@@ -537,8 +541,16 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
 #endif
       hipEvent_t e0 = nullptr, e1 = nullptr;
       if (ctx->timing) timing_begin(ctx, &e0, &e1);
+      a.mrg_ll = nxt.l();
+      a.mrg_tie = nxt.t();
+      a.mrg_slot = nxt.s();
+      a.fuse_merge = (fuse_walk_merge && a.rt_ix) ? 1 : 0;
       HC(walk(a, s), "nested walk");
       if (ctx->timing) timing_end(ctx, e0, e1, 1);
+      if (a.fuse_merge) {                 // merged in the walk's launch (or right after it)
+        if (check) HC(launch_check_sorted(nxt.l(), nxt.t(), n, g, (long long*)B.chk.p + 1, s), "check");
+        continue;
+      }
       if (fused_merge) {
         // the new keys sorted and merged into the survivors in one launch (merge_fused_kernel)
         HC(launch_merge_fused(a, nxt.l(), nxt.t(), nxt.s(), s), "merge keys");

@@ -24,6 +24,8 @@ struct NestDevState {
   int32_t error;
   long long gen_done;
   double max_ll;            // the largest live ll (the sorted keys' last): the stop test's L_max
+  unsigned int walk_done;   // walker workgroups done, over the run (the fused merge's hand-off)
+  unsigned int pad_;
 };
 
 // The stop / error flags and the generation count are read and written with agent-scope atomics
@@ -79,6 +81,15 @@ struct NestArgs {
   int32_t sym_box;          // box prior with lo[d] == -hi[d] for every d: tested as |y| <= hi
   int32_t lanes_hint;       // lanes per walker requested by MCG_NEST_LANES (0: the default)
   int32_t walk_waves;       // walker waves per draw-table workgroup (1, or 2 beyond 256 waves)
+  // the merge role of the walk kernel (k <= 4096 with the draw table): workgroups past the
+  // walkers' nwalk_blocks wait until walk_done reaches walk_target, then merge the new keys
+  // into mrg_* (merge_fused_block) or fold the estimate
+  int32_t fuse_merge;
+  int32_t nwalk_blocks;
+  uint32_t walk_target;
+  double* mrg_ll;
+  long long* mrg_tie;
+  int* mrg_slot;
   uint32_t row_bytes;       // D * 8: the draw table holds DE pairs as row byte offsets
   double* tv;               // ll + log dv of this generation's dead points (padded pow2)
   const double* prefix;     // [k+1] sum_{j'<j} log1p(-1/(n-j'))
@@ -414,16 +425,78 @@ struct WalkTarget {
   }
 };
 
+#include "mcg_nested_merge.h"
+
 // ---- constrained DE-MCMC walkers (draw_new_live_point, nested.ml:50-74) ----
 // P lanes per walker (P in {1, 2, 4}; the MH kernel's layout: lane `sub` owns the 4-dim blocks
 // c = sub, sub + P, ...).  Every lane of a walker draws the same Philox words, so the DE indices,
 // scale, accept decision and start point agree without communication; the log-target is the
 // canonical sum reduced across the P lanes (reduce_canon).  The DE partner rows of step s + 1
 // depend only on the RNG, so they are loaded while step s computes (one step of prefetch).
+// The merge role of a fused walk kernel (FM): workgroup b = blockIdx.x - nwalk_blocks of the
+// generation's merge (b == nblk: the estimate fold).  It takes the walkers' stop decision from the
+// same inputs (so it never waits for walkers that stopped), waits until every walker workgroup
+// has signalled (walk_done, hand-off row 1 of MI355X_MICROARCH.md: sc1 stores, vmcnt(0), a
+// workgroup barrier, one agent-scope add; here an sc1 poll, then a workgroup barrier), and runs
+// merge_fused_block with sc1 loads of the walkers' outputs.  The wait is bounded: past ~1 s
+// it flags an error (the host then reports a failed run) instead of hanging the grid.
+__device__ __forceinline__ void nest_merge_role(const NestArgs& a) {
+  constexpr int BS = 256, KCAP = kSmallSort;
+  const int b = (int)blockIdx.x - a.nwalk_blocks;
+  const int nblk = (int)((a.n - a.k + BS - 1) / BS);
+  if (b > nblk) return;
+  if (nest_stopped(a.st)) return;
+  if (a.mrep > 0) {
+    const double st_lv = a.st->log_vol, st_mx = a.st->max_ll, st_est = a.st->est;
+    const bool st_err = __hip_atomic_load(&a.st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    const double live = st_lv + st_mx;
+    if (live - plse(st_est, live, kLogTab) <= a.log_epsrel || st_err) return;   // as the walkers
+  }
+  __shared__ union FmLds {
+    MergeLds<BS, KCAP> m;
+    EstLds<BS> e;
+  } lds;
+  __shared__ int s_ok;
+  if (threadIdx.x == 0) {
+    int ok = 1;
+    for (uint32_t it = 0;; ++it) {
+      if (__hip_atomic_load(&a.st->walk_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.walk_target) break;
+      if (it > (1u << 24)) {
+        nest_set(&a.st->error);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    s_ok = ok;
+  }
+  __syncthreads();
+  if (!s_ok) return;
+  if (b == nblk) estimate_body<BS>(a, lds.e);
+  else merge_fused_block<BS, KCAP, true>(a, a.mrg_ll, a.mrg_tie, a.mrg_slot, b, lds.m);
+}
+
+// a walker workgroup of a fused walk kernel (FM) signals the merge role once every one of its
+// waves has finished its stores (stored sc1 where the merge reads them)
+__device__ __forceinline__ void nest_walk_signal(const NestArgs& a) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(&a.st->walk_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // GP: a DIAG_GAUSS prior, whose log density makes the walker's MH test log u < lp(y) - lp(cur)
-// (nested.ml:54-59) a real test (with box priors it holds for every passing proposal)
-template <int D, int LIK, int P, bool TAB, bool SYM, bool GP = false>
+// (nested.ml:54-59) a real test (with box priors it holds for every passing proposal).
+// FM: the generation's merge runs in the same launch (nest_merge_role), by the workgroups past
+// the walkers' (TAB only, k <= 4096: one walker wave per workgroup)
+template <int D, int LIK, int P, bool TAB, bool SYM, bool GP = false, bool FM = false>
 __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
+  static_assert(!FM || TAB, "the fused merge needs the draw table's workgroup shape");
+  if constexpr (FM) {
+    if ((int)blockIdx.x >= a.nwalk_blocks) {
+      nest_merge_role(a);
+      return;
+    }
+  }
   using Lay = WalkLayout<D, P>;
   constexpr int NL = Lay::NL;
   constexpr int W = Lay::W;
@@ -550,6 +623,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
       if (a.trace && (int)threadIdx.x == wl && blockIdx.x < 1024)   // the table-filling waves' end
         a.trace[((size_t)0 * 1024 + blockIdx.x) * 8 + 5] = wall_clock64();
 #endif
+      if constexpr (FM) nest_walk_signal(a);
       return;
     }
   }
@@ -820,22 +894,29 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   NT_STAMP(0, 4);
   const double nl = tgt.lik(cur, sub, a.m);
   const double np = tgt.prior(cur, sub, a.m);
-  if (!active) return;
+  // (FM: the merge role in this launch reads these: stored sc1)
+  auto put = [&](auto* p, auto v) __attribute__((always_inline)) {
+    if constexpr (FM) wt_store(p, v);
+    else *p = v;
+  };
+  if (active) {
 #pragma unroll
-  for (int i = 0; i < Lay::NCL; ++i)
+    for (int i = 0; i < Lay::NCL; ++i)
 #pragma unroll
-    for (int q = 0; q < W; ++q)
-      if (Lay::valid(sub, i, q)) a.nx[w * D + Lay::dim(sub, i, q)] = cur[W * i + q];
-  if (sub == 0) {
-    a.nll[w] = nl;
-    a.nlp[w] = np;
-    if (a.fuse_retire) {                               // the new point's key
-      a.newk_ll[w] = nl;
-      a.newk_tie[w] = -(long long)(a.mrep + w + 1);
-      a.newk_slot[w] = ret_slot;
+      for (int q = 0; q < W; ++q)
+        if (Lay::valid(sub, i, q)) put(a.nx + w * D + Lay::dim(sub, i, q), cur[W * i + q]);
+    if (sub == 0) {
+      put(a.nll + w, nl);
+      put(a.nlp + w, np);
+      if (a.fuse_retire) {                             // the new point's key
+        put(a.newk_ll + w, nl);
+        put(a.newk_tie + w, -(long long)(a.mrep + w + 1));
+        put(a.newk_slot + w, ret_slot);
+      }
+      if (!(nl >= thr)) nest_set(&a.st->error);      // nested.ml:70-72 -> Failure
     }
-    if (!(nl >= thr)) nest_set(&a.st->error);        // nested.ml:70-72 -> Failure
   }
+  if constexpr (FM) nest_walk_signal(a);
 }
 
 // ---- prior draws of the initial live set (nested.ml:126-129, Stats.draw_uniform) ----
@@ -877,6 +958,8 @@ __global__ void __launch_bounds__(256) nest_init_kernel(const NestArgs a, double
   keys_slot[s] = (int)s;
 }
 
+hipError_t launch_merge_fused(const NestArgs& a, double* oll, long long* otie, int* oslot, hipStream_t s);
+
 template <int D, int LIK, int P>
 hipError_t launch_nest_walk_p(const NestArgs& a, hipStream_t st) {
   // small workgroups: a generation has only k * P lanes, so one wave per workgroup spreads them
@@ -890,6 +973,29 @@ hipError_t launch_nest_walk_p(const NestArgs& a, hipStream_t st) {
   b.walk_waves = wwaves > 256 ? 2 : 1;
   const dim3 gt((unsigned)((wwaves + b.walk_waves - 1) / b.walk_waves)), bt(256);
   constexpr bool kSym = WalkTarget<D, P, LIK>::kReg;   // the |y| <= h form needs the register target
+  if (b.fuse_merge && !(b.rt_ix && b.walk_waves == 1 && b.k <= kSmallSort)) {
+    // (the fused merge takes one walker wave per workgroup: otherwise walk, then the merge kernel)
+    NestArgs c = b;
+    c.fuse_merge = 0;
+    hipError_t e = launch_nest_walk_p<D, LIK, P>(c, st);
+    if (e != hipSuccess) return e;
+    return launch_merge_fused(c, c.mrg_ll, c.mrg_tie, c.mrg_slot, st);
+  }
+  if (b.fuse_merge) {
+    // the walk with the generation's merge in the same launch: the merge workgroups after the
+    // walkers' (dispatched in order, so every walker workgroup is placed before any of them)
+    const int64_t nblk = (a.n - a.k + 255) / 256;
+    b.nwalk_blocks = (int32_t)gt.x;
+    b.walk_target = (uint32_t)((a.mrep / a.k + 1) * (int64_t)gt.x);
+    const dim3 gf((unsigned)(gt.x + nblk + 1));
+    if (a.m.prior_kind == MCG_PRIOR_DIAG_GAUSS)
+      hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, false, true, true>), gf, bt, 0, st, b);
+    else if (kSym && b.sym_box)
+      hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, kSym, false, true>), gf, bt, 0, st, b);
+    else
+      hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, false, false, true>), gf, bt, 0, st, b);
+    return hipGetLastError();
+  }
   if (a.m.prior_kind == MCG_PRIOR_DIAG_GAUSS) {
     if (b.rt_ix) hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, false, true>), gt, bt, 0, st, b);
     else hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, false, false, true>), dim3((unsigned)grid), dim3(block), 0, st, a);
