@@ -20,8 +20,6 @@
 //     hands every lane its dims.
 #pragma once
 #include "mcg_mh_kernel.h"
-#include <cstdlib>
-#include <type_traits>
 
 namespace mcg {
 
@@ -236,20 +234,12 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
       double v[4];
       const u32x4 w = w_ahead;
       pnormal4_lds(w, s_nt, v);            // the four normals' eight table gathers, one LDS wait
-#ifdef MCG_PROBE_FC_NOPHILOX
-      // timing probe (wrong values): a 2-multiply hash in place of each Philox call
-      {
-        const uint32_t h = (gid ^ tlo) * 0x9E3779B1u + (uint32_t)(4 * (m + 1) + q) * 0x85EBCA77u;
-        w_ahead = u32x4{h, h * 0xC2B2AE3Du, h ^ 0x27D4EB2Fu, h + 0x165667B1u};
-      }
-#else
       if (m + 1 < F::NM) {
         w_ahead = rng(gid, tlo, (uint32_t)(4 * (m + 1) + q), TAG_MH, thi);
       } else {
         const uint64_t T1 = T + 1;
         w_ahead = rng(gid, (uint32_t)T1, (uint32_t)q, TAG_MH, (uint32_t)(T1 >> 32));
       }
-#endif
       transpose_quadrants(v);                 // v[k'] = z[16 m + 4 k' + q]
 #pragma unroll
       for (int k2 = 0; k2 < 4; ++k2) {
@@ -262,14 +252,8 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
         const double rv = yv - s_mu[q * NL + kb];
 #pragma unroll
         for (int ib = 0; ib < F::NIB; ++ib)
-          if (4 * ib <= kb) {
-#ifdef MCG_PROBE_FC_NOMFMA
-            // timing probe (wrong values): one VALU fma in place of each MFMA
-            e[ib][kb & 3] = fma(s_u[F::frag(ib, kb) * 64 + lane], rv, e[ib][kb & 3]);
-#else
+          if (4 * ib <= kb)
             e[ib] = __builtin_amdgcn_mfma_f64_16x16x4f64(s_u[F::frag(ib, kb) * 64 + lane], rv, e[ib], 0, 0, 0);
-#endif
-          }
       }
     }
     // ---- log-likelihood: S = sum e_i^2 (accumulators k = q for even ib, k = q + 4 for odd ib) --
@@ -347,415 +331,13 @@ __global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_kernel(const MhArgs a)
   }
 }
 
-// ---- the software-pipelined step (round 5) ----
-// mh_fullcov_kernel draws a Philox call's normals, then runs the MFMAs of its columns: one wave
-// issues an f64 MFMA at most every ~66 clocks, so each MFMA group left the wave with nothing to
-// issue but MFMAs (the last call's group holds 16 of the step's 40), and PMC shows the waves
-// issue-stalled half their cycles (profiles/r05/c5_probe).  Here the step is laid out in slices,
-// each a few VALU instructions followed by its share of the MFMAs and a scheduling fence, so the
-// MFMAs are spread over independent VALU work in program order:
-//   phase A: the MFMAs of the columns whose normals were drawn during the previous step,
-//            between the slices of this step's remaining Philox calls (rounds, table gathers,
-//            finishes, transpose) and the proposal of their columns;
-//   phase B: the other columns' MFMAs, between the slices of the NEXT step's first calls, the
-//            staggered accept uniform and the previous step's deferred record (Welford and the
-//            harmonic-mean partial: x, ll and lp only change at this step's accept).
-// The arithmetic is the round-4 step's: e_i accumulates over column blocks in ascending order
-// (the oracle's fma chain), the same normals, y = fma(s, z, x), sums, accept test and records.
-template <int D>
-struct FcSeq {
-  static constexpr int NL = D / 4, NIB = D / 16;
-  static constexpr int NF = 2 * NIB * (NIB + 1);         // MFMAs per step: column kb has kb / 4 + 1
-  // column-order sequence: MFMA i is row block ib_of(i) of column kb_of(i) (compile-time only)
-  static constexpr int kb_of(int i) {
-    int kb = 0;
-    while (i >= kb / 4 + 1) { i -= kb / 4 + 1; ++kb; }
-    return kb;
-  }
-  static constexpr int ib_of(int i) {
-    int kb = 0;
-    while (i >= kb / 4 + 1) { i -= kb / 4 + 1; ++kb; }
-    return i;
-  }
-};
-
-template <int B, int E, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (B < E) {
-    f(std::integral_constant<int, B>{});
-    static_for<B + 1, E>(f);
-  }
-}
-
-// Philox4x32-10 advanced round by round (the rounds of philox(), mcg_math.h, bit for bit)
-struct PhiloxRun {
-  uint32_t c0, c1, c2, c3, k0, k1;
-  __device__ __forceinline__ void start(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t key0,
-                                        uint32_t key1) {
-    c0 = a0; c1 = a1; c2 = a2; c3 = a3; k0 = key0; k1 = key1;
-  }
-  template <int R>
-  __device__ __forceinline__ void round() {
-    if constexpr (R > 0) {
-      k0 += 0x9E3779B9u;
-      k1 += 0xBB67AE85u;
-    }
-    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
-    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-    const uint32_t n0 = xor3((uint32_t)(p1 >> 32), c1, k0);
-    const uint32_t n2 = xor3((uint32_t)(p0 >> 32), c3, k1);
-    c1 = (uint32_t)p1;
-    c3 = (uint32_t)p0;
-    c0 = n0;
-    c2 = n2;
-  }
-};
-
-template <int D, int UNI>
-__global__ void __launch_bounds__(kFcBlock, 1) mh_fullcov_pipe_kernel(const MhArgs a) {
-  using F = FcLayout<D>;
-  using Q = FcSeq<D>;
-  constexpr int NL = F::NKB;
-  constexpr int NM = F::NM;
-  __shared__ double2 s_lt[kLogTabN];
-  __shared__ double2 s_nt[kNrmTabN];
-  __shared__ double s_u[F::NFRAG * 64];
-  __shared__ double s_mu[D + 2];
-  for (int i = threadIdx.x; i < kLogTabN; i += blockDim.x) s_lt[i] = kLogTab[i];
-  for (int i = threadIdx.x; i < kNrmTabN; i += blockDim.x) s_nt[i] = kNrmTab[i];
-  for (int i = threadIdx.x; i < D; i += blockDim.x) s_mu[(i & 3) * (D / 4) + (i >> 2)] = a.lik[i];
-  if (threadIdx.x == 0) {
-    s_mu[D] = a.lik[D];
-    s_mu[D + 1] = a.prior_kind == MCG_PRIOR_FLAT ? 0.0 : a.pri[2 * D];
-  }
-  {
-    const double* __restrict__ U = a.lik + D + 1;
-    for (int e = threadIdx.x; e < F::NFRAG * 64; e += blockDim.x) {
-      const int f = e >> 6, l = e & 63;
-      int ib = 0, rem = f;
-      while (rem >= F::NKB - 4 * ib) { rem -= F::NKB - 4 * ib; ++ib; }
-      const int row = 16 * ib + (l & 15), col = 4 * (4 * ib + rem) + (l >> 4);
-      s_u[e] = col >= row ? U[row * D + col] : 0.0;
-    }
-  }
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int q = lane >> 4;
-  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t chain = wave * 16 + (lane & 15);
-  const bool active = chain < a.N;
-  const int64_t c = active ? chain : 0;
-  const int64_t N = a.N;
-  const Rng rng{a.k0, a.k1};
-  const uint32_t gid = a.chain_offset + (uint32_t)c;
-  auto dim = [&](int kb) { return 4 * kb + q; };
-
-  double x[NL];
-#pragma unroll
-  for (int kb = 0; kb < NL; ++kb) x[kb] = a.x[(int64_t)dim(kb) * N + c];
-  double ll = a.ll[c], lp = a.lp[c];
-  unsigned long long na = 0;
-
-  const bool accum = (a.flags & RUNF_ACCUMULATE) != 0;
-  constexpr int P = 4, NH = 2;
-  __shared__ double s_hm[2 * NH * kFcBlock];
-  auto hcm = [&](int l) -> double& { return s_hm[(2 * l) * kFcBlock + threadIdx.x]; };
-  auto hcs = [&](int l) -> double& { return s_hm[(2 * l + 1) * kFcBlock + threadIdx.x]; };
-  double hm_pv = 0.0;
-  bool hm_pok = false;
-  double rmean[NL], rm2[NL];
-  if (accum) {
-#pragma unroll
-    for (int kb = 0; kb < NL; ++kb) {
-      rmean[kb] = a.mean[(int64_t)dim(kb) * N + c];
-      rm2[kb] = a.m2[(int64_t)dim(kb) * N + c];
-    }
-#pragma unroll
-    for (int l = 0; l < NH; ++l) {
-      hcm(l) = a.hm_m[(int64_t)(q + P * l) * N + c];
-      hcs(l) = a.hm_s[(int64_t)(q + P * l) * N + c];
-    }
-  }
-  auto hm_flush = [&](int64_t R0) {
-    const int li = (int)((R0 & 7) / P);
-    if (hm_pok) hm_update(hcm(li), hcs(li), hm_pv);
-    hm_pok = false;
-  };
-
-  int64_t next_rec = a.next_rec, r = a.next_r;
-  double inv_pf = 0.0;
-  if (accum) inv_pf = welford_weight(a, r - a.next_r0);
-  auto record = [&](int64_t R) __attribute__((always_inline)) {
-    const int64_t s = R - a.rec_base;
-    if ((a.flags & RUNF_RECORD_X) && active) {
-      int64_t n = N;
-      asm volatile("" : "+s"(n));
-      double* px = a.rec_x + (s * D + q) * n + c;
-#pragma unroll
-      for (int kb = 0; kb < NL; ++kb) px[4 * kb * n] = x[kb];
-    }
-    if ((a.flags & RUNF_RECORD_LLP) && active && q == 0) {
-      a.rec_ll[s * N + c] = ll;
-      a.rec_lp[s * N + c] = lp;
-    }
-    if (accum) {
-      const double inv = inv_pf;
-      inv_pf = welford_weight(a, R + 1 - a.next_r0);
-#pragma unroll
-      for (int kb = 0; kb < NL; ++kb) {
-        const double delta = x[kb] - rmean[kb];
-        const double mnew = fma(delta, inv, rmean[kb]);
-        rm2[kb] = fma(delta, x[kb] - mnew, rm2[kb]);
-        rmean[kb] = mnew;
-      }
-      const int jr = (int)(R & (P - 1));
-      if (q == jr) {
-        hm_pv = -ll;
-        hm_pok = true;
-      }
-      if (jr == P - 1) hm_flush(R - (P - 1));
-    }
-  };
-  if (a.flags & RUNF_RECORD_INITIAL) {
-    record(r);
-    ++r;
-  }
-
-  // AH of the NM Philox calls of a step are drawn during the previous step (its phase B); the
-  // other NM - AH during the step's own phase A
-  constexpr int AH = (NM + 1) / 2;
-  constexpr int KA = 4 * AH;                              // columns whose normals come ahead
-  constexpr int NFA = 2 * AH * (AH + 1);                  // their MFMAs (column order: first)
-  constexpr int NCA = NM - AH;                            // calls drawn in phase A
-  // The slices of NC Philox calls m0 .. m0 + NC - 1 of step Tn, advanced together: 10 round
-  // slices, the table gathers, the finishes, the transpose into zz[4 m + k'] (mh_fullcov_kernel:
-  // z[16 m + 4 k' + q]).  slice(s_c) runs slice s; kSlices of them.
-  constexpr int kSlices = 15;
-  struct CallSlices {
-    PhiloxRun ph[2];
-    NrmPending np[2];
-    double v[4];
-  };
-  auto call_slice = [&](CallSlices& cs, auto s_c, auto nc_c, int m0, uint64_t Tn, double* zz)
-      __attribute__((always_inline)) {
-    constexpr int S = decltype(s_c)::value, NC = decltype(nc_c)::value;
-    if constexpr (S < 10) {
-#pragma unroll
-      for (int j = 0; j < NC; ++j) {
-        if constexpr (S == 0)
-          cs.ph[j].start(gid, (uint32_t)Tn, (uint32_t)(4 * (m0 + j) + q),
-                         (TAG_MH << 16) | ((uint32_t)(Tn >> 32) & 0xFFFFu), rng.k0, rng.k1);
-        cs.ph[j].template round<S>();
-      }
-    } else {
-      // the table gathers of half h = S - 10 (normals 2 (h & 1), 2 (h & 1) + 1 of call h >> 1) in
-      // slice 10 + h, their finishes one slice later (two normals' gathers in flight at a time:
-      // 22 registers), a call's transpose with its second half's finishes
-      constexpr int HI = S - 10, HF = S - 11;
-      if constexpr (HF >= 0 && HF < 2 * NC) {
-        cs.v[2 * (HF & 1)] = pnormal_finish(cs.np[0]);
-        cs.v[2 * (HF & 1) + 1] = pnormal_finish(cs.np[1]);
-        if constexpr (HF & 1) {
-          transpose_quadrants(cs.v);
-#pragma unroll
-          for (int k2 = 0; k2 < 4; ++k2) zz[4 * (m0 + (HF >> 1)) + k2] = cs.v[k2];
-        }
-      }
-      if constexpr (HI < 2 * NC) {
-        const PhiloxRun& ph = cs.ph[HI >> 1];
-        cs.np[0] = pnormal_issue((HI & 1) ? ph.c2 : ph.c0, s_nt);
-        cs.np[1] = pnormal_issue((HI & 1) ? ph.c3 : ph.c1, s_nt);
-      }
-    }
-  };
-
-  double lu_own = 0.0;
-  bool pend = false;                     // a record of the previous step, folded in this step
-  int64_t pend_r = 0;
-  auto step = [&](int64_t t, const double* za, double* zn) __attribute__((always_inline)) {
-    const uint64_t T = a.step_base + (uint64_t)t;
-    typedef const __attribute__((address_space(1))) double gdouble;
-    gdouble* qpri = (gdouble*)a.pri;
-    gdouble* qprop = (gdouble*)a.prop;
-    asm volatile("" : "+s"(qpri), "+s"(qprop));
-    // the U fragments' lane offset, opaque per step: their loads stay in the loop (hoisted, the
-    // loop-invariant fragments would take ~80 registers)
-    uint32_t ulane = (uint32_t)lane;
-    asm volatile("" : "+v"(ulane));
-    const double* const su = s_u + ulane;
-    bool ok = true;
-    double y[NL], zb[NL], rvc[NL];
-    // y = x + s z (mcmc.ml:41) and the box test of column kb
-    auto propose = [&](int kb, double zv) __attribute__((always_inline)) {
-      const int d = dim(kb);
-      const double yv = fma(UNI ? a.uni_s : qprop[d], zv, x[kb]);
-      y[kb] = yv;
-      if constexpr (UNI == 2) ok = ok & (__builtin_fabs(yv) <= a.uni_hi);
-      else ok = ok & (yv >= (UNI ? a.uni_lo : qpri[d])) & (yv <= (UNI ? a.uni_hi : qpri[D + d]));
-    };
-#pragma unroll
-    for (int kb = 0; kb < KA; ++kb) propose(kb, za[kb]);
-    dbl4 e[F::NIB];
-#pragma unroll
-    for (int ib = 0; ib < F::NIB; ++ib) e[ib] = dbl4{0.0, 0.0, 0.0, 0.0};
-    auto mfma_i = [&](auto i_c) __attribute__((always_inline)) {
-      constexpr int I = decltype(i_c)::value;
-      constexpr int kb = Q::kb_of(I), ib = Q::ib_of(I);
-      if constexpr (ib == 0) rvc[kb] = y[kb] - s_mu[q * NL + kb];
-      e[ib] = __builtin_amdgcn_mfma_f64_16x16x4f64(su[F::frag(ib, kb) * 64], rvc[kb], e[ib], 0, 0, 0);
-    };
-    // slice s of a phase, then its share of the MFMAs [I0, I1), then a scheduling fence
-    auto mfmas_of_slice = [&](auto s_c, auto i0_c, auto i1_c) __attribute__((always_inline)) {
-      constexpr int S = decltype(s_c)::value, I0 = decltype(i0_c)::value, I1 = decltype(i1_c)::value;
-      static_for<I0 + S * (I1 - I0) / kSlices, I0 + (S + 1) * (I1 - I0) / kSlices>(mfma_i);
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    // ---- phase A: this step's remaining calls; the first columns' MFMAs ----
-    {
-      CallSlices cs;
-      static_for<0, kSlices>([&](auto s_c) __attribute__((always_inline)) {
-        constexpr int S = decltype(s_c)::value;
-        if constexpr (NCA > 0) call_slice(cs, s_c, std::integral_constant<int, NCA>{}, AH, T, zb);
-        if constexpr (S == kSlices - 1) {
-#pragma unroll
-          for (int kb = KA; kb < NL; ++kb) propose(kb, zb[kb]);
-        }
-        mfmas_of_slice(s_c, std::integral_constant<int, 0>{}, std::integral_constant<int, NFA>{});
-      });
-    }
-    // ---- phase B: the next step's first calls, the accept uniform, the deferred record; the
-    //      other columns' MFMAs ----
-    const int qq = (int)(t & (P - 1));
-    {
-      CallSlices cs;
-      static_for<0, kSlices>([&](auto s_c) __attribute__((always_inline)) {
-        constexpr int S = decltype(s_c)::value;
-        call_slice(cs, s_c, std::integral_constant<int, AH>{}, 0, T + 1, zn);
-        if constexpr (S == 3) {
-          // the accept uniform of this step, staggered over the quadrants (mh_fullcov_kernel)
-          if (qq == 0) {
-            const uint64_t Tj = T + (uint64_t)q;
-            const u32x4 wa = rng(gid, (uint32_t)Tj, CALL_ACCEPT, TAG_MH, (uint32_t)(Tj >> 32));
-            lu_own = plog(u53(wa.x, wa.y), s_lt);
-          }
-        }
-        if constexpr (S == 11) {
-          if (pend) {                      // the previous step's record: x, ll, lp are still its
-            record(pend_r);
-            pend = false;
-          }
-        }
-        mfmas_of_slice(s_c, std::integral_constant<int, NFA>{}, std::integral_constant<int, Q::NF>{});
-      });
-    }
-    const double lu = __shfl(lu_own, (lane & 15) | (qq << 4), 64);
-    // ---- log-likelihood, accept (mcmc.ml:42-56) ----
-    double A0 = 0.0, A1 = 0.0;
-#pragma unroll
-    for (int ib = 0; ib < F::NIB; ++ib)
-#pragma unroll
-      for (int ri = 0; ri < 4; ++ri) {
-        if (ib & 1) A1 = fma(e[ib][ri], e[ib][ri], A1);
-        else A0 = fma(e[ib][ri], e[ib][ri], A0);
-      }
-    const double b = A0 + A1;
-    const double cs2 = sum_xor32(b);
-    const double S = sum_xor16(cs2);
-    const double lly = s_mu[D] - 0.5 * S;
-    const int inb = and_xor32_16(ok ? 1 : 0);
-    const double lpy = a.prior_kind == MCG_PRIOR_FLAT ? 0.0 : (inb ? s_mu[D + 1] : -__builtin_inf());
-    const double ratio = (lly + lpy) - (ll + lp);
-    const bool acc = lu < ratio;
-#pragma unroll
-    for (int kb = 0; kb < NL; ++kb) x[kb] = acc ? y[kb] : x[kb];
-    if (acc) {
-      ll = lly;
-      lp = lpy;
-      ++na;
-    }
-    if (a.flags & RUNF_RECORD_ACCEPT) {
-      const uint64_t mb = (uint64_t)__ballot(acc && active) & 0xFFFFull;
-      if (lane == 0 && wave * 16 < N) {
-        uint8_t* row = a.bits + (a.t0 + t) * a.bits_row_bytes;
-        *(uint16_t*)(row + wave * 2) = (uint16_t)mb;
-      }
-    }
-    const int64_t tt1 = a.t0 + t + 1;
-    if (tt1 == next_rec && r < a.rec_end) {
-      pend = true;
-      pend_r = r;
-      ++r;
-      next_rec += a.nskip;
-    }
-  };
-  double zA[KA], zB[KA];
-  if (a.nsteps > 0) {
-#pragma unroll
-    for (int m = 0; m < AH; ++m) {
-      const u32x4 w = rng(gid, (uint32_t)a.step_base, (uint32_t)(4 * m + q), TAG_MH, (uint32_t)(a.step_base >> 32));
-      double v[4] = {pnormal(w.x, s_nt), pnormal(w.y, s_nt), pnormal(w.z, s_nt), pnormal(w.w, s_nt)};
-      transpose_quadrants(v);
-#pragma unroll
-      for (int k2 = 0; k2 < 4; ++k2) zA[4 * m + k2] = v[k2];
-    }
-  }
-  int64_t t = 0;
-  for (; t + 1 < a.nsteps; t += 2) {
-    step(t, zA, zB);
-    step(t + 1, zB, zA);
-  }
-  if (t < a.nsteps) step(t, zA, zB);
-  if (pend) record(pend_r);
-
-  if (!active) return;
-  int64_t n = N;
-  asm volatile("" : "+s"(n));
-  const int64_t o = (int64_t)q * n + c;
-#pragma unroll
-  for (int kb = 0; kb < NL; ++kb) a.x[o + 4 * kb * n] = x[kb];
-  if (q == 0) {
-    a.ll[c] = ll;
-    a.lp[c] = lp;
-    a.nacc[c] += na;
-  }
-  if (accum) {
-#pragma unroll
-    for (int kb = 0; kb < NL; ++kb) {
-      a.mean[o + 4 * kb * n] = rmean[kb];
-      a.m2[o + 4 * kb * n] = rm2[kb];
-    }
-    hm_flush((r - 1) & ~(int64_t)(P - 1));
-#pragma unroll
-    for (int l = 0; l < NH; ++l) {
-      a.hm_m[o + P * l * n] = hcm(l);
-      a.hm_s[o + P * l * n] = hcs(l);
-    }
-  }
-}
-
-// MCG_FC_KERNEL=1 selects the round-4 step (mh_fullcov_kernel) for A/B runs; the default is the
-// software-pipelined step
-inline bool fc_use_v1() {
-  static const bool v1 = [] {
-    const char* e = std::getenv("MCG_FC_KERNEL");
-    return e && e[0] == '1';
-  }();
-  return v1;
-}
-
 template <int D>
 hipError_t launch_mh_fullcov(const MhArgs& a, int64_t nthreads, hipStream_t s) {
   const int64_t grid = (nthreads + kFcBlock - 1) / kFcBlock;   // nthreads = 4 N: 128 chains per block
   const dim3 g((unsigned)grid), b(kFcBlock);
-  if (fc_use_v1()) {
-    if (a.uni && a.uni_lo == -a.uni_hi) hipLaunchKernelGGL((mh_fullcov_kernel<D, 2>), g, b, 0, s, a);
-    else if (a.uni) hipLaunchKernelGGL((mh_fullcov_kernel<D, 1>), g, b, 0, s, a);
-    else hipLaunchKernelGGL((mh_fullcov_kernel<D, 0>), g, b, 0, s, a);
-    return hipGetLastError();
-  }
-  if (a.uni && a.uni_lo == -a.uni_hi) hipLaunchKernelGGL((mh_fullcov_pipe_kernel<D, 2>), g, b, 0, s, a);
-  else if (a.uni) hipLaunchKernelGGL((mh_fullcov_pipe_kernel<D, 1>), g, b, 0, s, a);
-  else hipLaunchKernelGGL((mh_fullcov_pipe_kernel<D, 0>), g, b, 0, s, a);
+  if (a.uni && a.uni_lo == -a.uni_hi) hipLaunchKernelGGL((mh_fullcov_kernel<D, 2>), g, b, 0, s, a);
+  else if (a.uni) hipLaunchKernelGGL((mh_fullcov_kernel<D, 1>), g, b, 0, s, a);
+  else hipLaunchKernelGGL((mh_fullcov_kernel<D, 0>), g, b, 0, s, a);
   return hipGetLastError();
 }
 

@@ -216,18 +216,11 @@ static_assert(kNrmTabN == 2 * kNrmSeg, "normal table: two rows per segment");
 
 // (w << 1) | 1 and (hi & 0x7FFF) | 0x3FF00000 as single VALU ops (hipcc emits shift + or pairs)
 __device__ __forceinline__ uint32_t nrm_odd(uint32_t w) {
-#ifdef MCG_NRM_NOASM
-  return (w << 1) | 1u;
-#else
   uint32_t r;
   asm("v_lshl_or_b32 %0, %1, 1, 1" : "=v"(r) : "v"(w));
   return r;
-#endif
 }
 __device__ __forceinline__ uint32_t nrm_frac_hi(uint32_t hi) {
-#ifdef MCG_NRM_NOASM
-  return (hi & 0x7FFFu) | 0x3FF00000u;
-#endif
   uint32_t r;
   // gfx9 VOP3: no literal operand and one scalar operand, so the mask comes in a VGPR
   asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(hi), "v"(0x7FFFu), "s"(0x3FF00000u));
@@ -260,12 +253,8 @@ __device__ __forceinline__ double pnormal_finish(const NrmPending& q) {
   p = fma(p, q.x, q.c10.x);
   p = fma(p, q.x, q.c10.y);
   // p_hi ^ (w & 0x80000000): the sign of the word flips z
-#ifdef MCG_NRM_NOASM
-  const uint32_t h = (uint32_t)__double2hiint(p) ^ (q.sign & 0x80000000u);
-#else
   uint32_t h;
   asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x6c" : "=v"(h) : "v"(q.sign), "v"(__double2hiint(p)), "s"(0x80000000u));
-#endif
   return __hiloint2double((int)h, __double2loint(p));
 }
 __device__ __forceinline__ double pnormal(uint32_t w, const double2* tab) {
@@ -290,18 +279,6 @@ __device__ __forceinline__ void pnormal4_lds(const u32x4 w, const double2* tab, 
   }
   double2 a0, a1, a2, a3, b0, b1, b2, b3;
   static_assert(kNrmSeg * 16 == 16384, "second half of the table at offset 16384");
-#if defined(MCG_PROBE_NRM_BCAST)
-  // timing probe (wrong values): every lane gathers row 0 -- the same gathers, broadcast, no
-  // bank conflicts
-#pragma unroll
-  for (int k = 0; k < 4; ++k) ad[k] = base + (ad[k] & 0x80000000u);
-#endif
-#if defined(MCG_PROBE_NRM_NOLDS)
-  // timing probe (wrong values): no table gathers at all, coefficients from the operand
-  a0 = a1 = a2 = a3 = double2{xp[0], 0.5};
-  b0 = b1 = b2 = b3 = double2{xp[1], 0.25};
-  if (0)
-#endif
   asm volatile(
       "ds_read_b128 %0, %8\n\t"
       "ds_read_b128 %4, %8 offset:16384\n\t"

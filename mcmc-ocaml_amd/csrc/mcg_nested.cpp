@@ -379,10 +379,11 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   if (const char* e = std::getenv("MCG_NEST_LANES"))
     a.lanes_hint = !std::strcmp(e, "wide") ? -1 : !std::strcmp(e, "narrow") ? -2 : std::atoi(e);
   a.fuse_retire = a.est_in_rank && !retire_kernel;
-  // k <= 4096 with the draw table: the merge runs in the walk's launch (nest_walk_kernel's merge
-  // role, one kernel boundary a generation instead of two); MCG_NESTED_FM=0 keeps two launches
+  // MCG_NESTED_FM=1 (k <= 4096 with the draw table): the merge runs in the walk's launch
+  // (nest_walk_kernel's merge role, one kernel boundary a generation instead of two).  Not the
+  // default: measured slower at C3
   const char* fm_env = std::getenv("MCG_NESTED_FM");
-  const bool fuse_walk_merge = fused_merge && k <= 4096 && !(fm_env && fm_env[0] == '0');
+  const bool fuse_walk_merge = fused_merge && k <= 4096 && fm_env && fm_env[0] == '1';
   // the walkers' draws of a generation in a table the previous merge fills (when it fits)
   a.rt_ix = nullptr;
   a.rt_sc = nullptr;

@@ -25,7 +25,7 @@ struct NestDevState {
   long long gen_done;
   double max_ll;            // the largest live ll (the sorted keys' last): the stop test's L_max
   unsigned int walk_done;   // walker workgroups done, over the run (the fused merge's hand-off)
-  unsigned int pad_;
+  unsigned int merge_seen;  // fused-merge workgroups past their stop test, over the run
 };
 
 // The stop / error flags and the generation count are read and written with agent-scope atomics
@@ -87,6 +87,7 @@ struct NestArgs {
   int32_t fuse_merge;
   int32_t nwalk_blocks;
   uint32_t walk_target;
+  uint32_t merge_target;    // merge_seen once every merge workgroup of this generation has registered
   double* mrg_ll;
   long long* mrg_tie;
   int* mrg_slot;
@@ -435,43 +436,55 @@ struct WalkTarget {
 // depend only on the RNG, so they are loaded while step s computes (one step of prefetch).
 // The merge role of a fused walk kernel (FM): workgroup b = blockIdx.x - nwalk_blocks of the
 // generation's merge (b == nblk: the estimate fold).  It takes the walkers' stop decision from the
-// same inputs (so it never waits for walkers that stopped), waits until every walker workgroup
-// has signalled (walk_done, hand-off row 1 of MI355X_MICROARCH.md: sc1 stores, vmcnt(0), a
-// workgroup barrier, one agent-scope add; here an sc1 poll, then a workgroup barrier), and runs
-// merge_fused_block with sc1 loads of the walkers' outputs.  The wait is bounded: past ~1 s
+// same inputs (so it never waits for walkers that stopped), registers (merge_seen), waits until
+// every walker workgroup has signalled (walk_done, hand-off row 1 of MI355X_MICROARCH.md: sc1
+// stores, vmcnt(0), a workgroup barrier, one agent-scope add; here an sc1 poll, then a workgroup
+// barrier) and every merge workgroup has registered, and runs merge_fused_block with sc1 loads of
+// the walkers' outputs.  The wait is bounded: past ~1 s
 // it flags an error (the host then reports a failed run) instead of hanging the grid.
 __device__ __forceinline__ void nest_merge_role(const NestArgs& a) {
   constexpr int BS = 256, KCAP = kSmallSort;
   const int b = (int)blockIdx.x - a.nwalk_blocks;
   const int nblk = (int)((a.n - a.k + BS - 1) / BS);
   if (b > nblk) return;
-  if (nest_stopped(a.st)) return;
-  if (a.mrep > 0) {
-    const double st_lv = a.st->log_vol, st_mx = a.st->max_ll, st_est = a.st->est;
-    const bool st_err = __hip_atomic_load(&a.st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-    const double live = st_lv + st_mx;
-    if (live - plse(st_est, live, kLogTab) <= a.log_epsrel || st_err) return;   // as the walkers
-  }
+  NT_STAMP(3, 0);
   __shared__ union FmLds {
     MergeLds<BS, KCAP> m;
     EstLds<BS> e;
   } lds;
   __shared__ int s_ok;
   if (threadIdx.x == 0) {
-    int ok = 1;
-    for (uint32_t it = 0;; ++it) {
-      if (__hip_atomic_load(&a.st->walk_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.walk_target) break;
-      if (it > (1u << 24)) {
-        nest_set(&a.st->error);
-        ok = 0;
-        break;
+    // One thread takes the stop decision and registers the workgroup (merge_seen) before any
+    // merge workgroup may write the state it reads: the estimate fold rewrites log_vol / est and
+    // the last key's workgroup max_ll, so a workgroup placed late would otherwise test the next
+    // generation's state.  Every merge workgroup waits for all nblk + 1 registrations (and the
+    // walkers) before it writes anything.
+    int ok = !nest_stopped(a.st);
+    if (ok && a.mrep > 0) {
+      const double st_lv = a.st->log_vol, st_mx = a.st->max_ll, st_est = a.st->est;
+      const bool st_err = __hip_atomic_load(&a.st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+      const double live = st_lv + st_mx;
+      if (live - plse(st_est, live, kLogTab) <= a.log_epsrel || st_err) ok = 0;   // as the walkers
+    }
+    if (ok) {
+      __hip_atomic_fetch_add(&a.st->merge_seen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      for (uint32_t it = 0;; ++it) {
+        if (__hip_atomic_load(&a.st->walk_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.walk_target &&
+            __hip_atomic_load(&a.st->merge_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.merge_target)
+          break;
+        if (it > (1u << 22)) {
+          nest_set(&a.st->error);
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(8);
       }
-      __builtin_amdgcn_s_sleep(2);
     }
     s_ok = ok;
   }
   __syncthreads();
   if (!s_ok) return;
+  NT_STAMP(3, 5);
   if (b == nblk) estimate_body<BS>(a, lds.e);
   else merge_fused_block<BS, KCAP, true>(a, a.mrg_ll, a.mrg_tie, a.mrg_slot, b, lds.m);
 }
@@ -618,7 +631,9 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
           }
         }
       }
-      walk_draws_fill<!Tgt::kFold>(a, a.mrep + a.k, (int64_t)blockIdx.x * nf + (threadIdx.x - wl), (int64_t)gridDim.x * nf, lt);
+      // (the stride counts the walker workgroups only: a fused launch's merge workgroups fill nothing)
+      const int64_t nwb = FM ? (int64_t)a.nwalk_blocks : (int64_t)gridDim.x;
+      walk_draws_fill<!Tgt::kFold>(a, a.mrep + a.k, (int64_t)blockIdx.x * nf + (threadIdx.x - wl), nwb * nf, lt);
 #ifdef MCG_NEST_TRACE
       if (a.trace && (int)threadIdx.x == wl && blockIdx.x < 1024)   // the table-filling waves' end
         a.trace[((size_t)0 * 1024 + blockIdx.x) * 8 + 5] = wall_clock64();
@@ -987,6 +1002,7 @@ hipError_t launch_nest_walk_p(const NestArgs& a, hipStream_t st) {
     const int64_t nblk = (a.n - a.k + 255) / 256;
     b.nwalk_blocks = (int32_t)gt.x;
     b.walk_target = (uint32_t)((a.mrep / a.k + 1) * (int64_t)gt.x);
+    b.merge_target = (uint32_t)((a.mrep / a.k + 1) * (nblk + 1));
     const dim3 gf((unsigned)(gt.x + nblk + 1));
     if (a.m.prior_kind == MCG_PRIOR_DIAG_GAUSS)
       hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, false, true, true>), gf, bt, 0, st, b);

@@ -97,6 +97,32 @@ def valu_framing(name, D, N, S, avg_launch_ms):
             "source": "profiles/pmc_valu_%s.json" % name}
 
 
+F64_MFMA_PEAK_TFS = 78.6   # v_mfma_f64_16x16x4f64: 2,048 flop / 64 cycles / SIMD, 1,024 SIMDs, 2.4 GHz
+
+
+def mfma_framing(D, steps, avg_launch_ms, valu=None):
+    """The full-covariance step's f64 matrix-core framing (mh_fullcov_kernel): 16 chains per MFMA
+    tile, the block lower-triangular L^-1 y as sum_{kb < D/4} (kb / 4 + 1) v_mfma_f64_16x16x4f64
+    per 16 chain-steps (40 at D 64), against the measured f64 MFMA rate (64 cycles per MFMA per
+    SIMD: 78.6 TFLOP/s, scripts/probes/mfma_f64_rate.hip).  achieved: the algorithmic D (D + 1)
+    flop per step (triangular solve + squared norm); issued: the MFMA tiles' 2,048 flop each.
+    f64 VALU work shares the datapath (scripts/probes/mfma_valu_overlap.hip), so the VALU framing
+    rides along as the secondary bound."""
+    if not avg_launch_ms:
+        return None
+    n_mfma = sum(kb // 4 + 1 for kb in range(D // 4))
+    t = avg_launch_ms * 1e-3
+    alg = steps * D * (D + 1) / t / 1e12
+    issued = steps / 16.0 * n_mfma * 2048.0 / t / 1e12
+    r = {"bound": "mfma", "achieved": alg, "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s", "frac": alg / F64_MFMA_PEAK_TFS,
+         "issued": issued, "issued_frac": issued / F64_MFMA_PEAK_TFS, "mfma_per_16_steps": n_mfma,
+         "flop_per_step": D * (D + 1), "peak_source": "measured f64 MFMA rate (64 cycles / MFMA / SIMD)",
+         "avg_launch_ms": avg_launch_ms}
+    if valu:
+        r["valu_secondary"] = valu
+    return r
+
+
 def shell_log_z(D, r, w, half):
     """Analytic log Z of one Gaussian shell in [-half, half]^D (radial quadrature; the shell
     lies well inside the box)."""
@@ -308,11 +334,12 @@ def c5(args):
             "accept_frac": acc / (acc + rej),
             "posterior_check": {"max_abs_mean_err_over_sd": float(np.max(np.abs(mean - mu) / np.sqrt(np.diag(cov)))),
                                 "max_rel_sd_err": float(np.max(np.abs(sd / np.sqrt(np.diag(cov)) - 1)))},
-            "roofline_hbm": hbm_secondary(roofline("mcg::mh_kernel<64,P,FULLCOV,GAUSS>", N * S, 8.0 * (D + 2),
+            "roofline_hbm": hbm_secondary(roofline("mcg::mh_fullcov_kernel<64,0>", N * S, 8.0 * (D + 2),
                                                    ctx.kernel_timing("mh"))),
             "flops_per_step": D * (D + 1)}
-    line["roofline"] = valu_framing("c5", D, N, S, line["roofline_hbm"]["avg_launch_ms"]) or \
-        {"bound": "valu", "frac": None, "note": "no PMC pass committed for this configuration"}
+    ms = line["roofline_hbm"]["avg_launch_ms"]
+    line["roofline"] = mfma_framing(D, N * S, ms, valu_framing("c5", D, N, S, ms)) or \
+        {"bound": "mfma", "frac": None, "note": "no kernel timing"}
     ctx.close()
     return line
 

@@ -5,6 +5,8 @@ mkdir -p gpurun_out/c3fm
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest -x -v --timeout 150 --timeout-method thread tests/test_gpu_nested.py tests/test_gpu_gauss_prior.py tests/test_gpu_gauss_mix.py tests/test_gpu_rccl.py > gpurun_out/c3fm/pytest.log 2>&1
 rc=$?; tail -3 gpurun_out/c3fm/pytest.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u -m pytest -x -v --timeout 150 --timeout-method thread tests/test_gpu_mh.py tests/test_gpu_any_dim.py -k fullcov > gpurun_out/c3fm/pytest_fc.log 2>&1
+rc=$?; tail -3 gpurun_out/c3fm/pytest_fc.log; [ $rc -eq 0 ] || exit $rc
 for i in 1 2; do
   for v in fm two; do
     if [ $v = two ]; then export MCG_NESTED_FM=0; else unset MCG_NESTED_FM; fi

@@ -305,19 +305,39 @@ def test_nested_walker_box_skip_near_the_box_bit_exact(oracle, T, sym):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", ["MCG_NESTED_NO_TABLE", "MCG_NESTED_RETIRE_KERNEL", "both", "MCG_NESTED_MERGE2"])
+@pytest.mark.parametrize("env", ["MCG_NESTED_NO_TABLE", "MCG_NESTED_RETIRE_KERNEL", "both", "MCG_NESTED_MERGE2",
+                                 "MCG_NESTED_FM"])
 @pytest.mark.parametrize("D", [3, 16])
 def test_nested_alternate_paths_bit_exact(oracle, T, monkeypatch, env, D):
     """The paths the default run does not take: walkers drawing their own random numbers (no
     draw table: what a generation too big for the table uses), the separate retire kernel
-    (k > 4096 uses it) and the two-launch counted-rank sort + merge instead of the one-launch
-    fused merge -- the same dead points as the oracle, bit for bit."""
+    (k > 4096 uses it), the two-launch counted-rank sort + merge instead of the one-launch
+    fused merge, and the merge inside the walk's launch (MCG_NESTED_FM=1) -- the same dead points
+    as the oracle, bit for bit."""
     for var in (["MCG_NESTED_NO_TABLE", "MCG_NESTED_RETIRE_KERNEL"] if env == "both" else [env]):
         monkeypatch.setenv(var, "1")
     lik = T.gauss_shell(np.zeros(D), 1.0, 0.2)
     pri = T.box(-2 * np.ones(D), 2 * np.ones(D))
     g = gpu_nested(lik, pri, 14, nlive=300, nmcmc=15, mode_hopping_frac=0.1, k=30, max_dead=30 * 30)
     o = oracle_nested(oracle, lik, pri, 14, nlive=300, nmcmc=15, mode_hop=0.1, k=30, max_iter=30 * 30)
+    assert_nested_same(g, o)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nlive,k,fixed", [(300, 4, False), (300, 16, True), (300, 100, False), (5000, 512, False),
+                                           (20000, 4096, True)])
+def test_nested_walk_merge_one_launch_bit_exact(oracle, T, monkeypatch, nlive, k, fixed):
+    """The walk with the generation's merge in the same launch (MCG_NESTED_FM=1: merge
+    workgroups behind the walkers', in-launch hand-off), run to the stop test: one walker
+    workgroup, several (k 512: 8), 256 (k 4,096) and the two stop rules -- the oracle's run bit
+    for bit.  (A fill stride over the merge workgroups too left holes in the next draw table.)"""
+    monkeypatch.setenv("MCG_NESTED_FM", "1")
+    D = 3
+    lik = T.gauss_shell(np.zeros(D), 1.0, 0.2)
+    pri = T.box(-2 * np.ones(D), 2 * np.ones(D))
+    g = gpu_nested(lik, pri, 5, fixed_stop=fixed, nlive=nlive, nmcmc=15, mode_hopping_frac=0.1, k=k)
+    o = oracle_nested(oracle, lik, pri, 5, quirk=not fixed, nlive=nlive, nmcmc=15, mode_hop=0.1, k=k)
+    assert g.converged
     assert_nested_same(g, o)
 
 
