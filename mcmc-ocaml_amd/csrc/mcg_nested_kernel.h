@@ -24,8 +24,11 @@ struct NestDevState {
   int32_t error;
   long long gen_done;
   double max_ll;            // the largest live ll (the sorted keys' last): the stop test's L_max
-  unsigned int walk_done;   // walker workgroups done, over the run (the fused merge's hand-off)
-  unsigned int merge_seen;  // fused-merge workgroups past their stop test, over the run
+  // the one-launch generation's hand-off counters, each on a 128-B line of its own: the walkers'
+  // first loads read the fields above, which must not share a line with 500 workgroups' atomics
+  alignas(128) unsigned int walk_done;    // walker workgroups done, over the run
+  alignas(128) unsigned int merge_seen;   // merge workgroups past their stop test, over the run
+  char pad_[124];
 };
 
 // The stop / error flags and the generation count are read and written with agent-scope atomics

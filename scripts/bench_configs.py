@@ -120,6 +120,19 @@ def mfma_framing(D, steps, avg_launch_ms, valu=None):
          "avg_launch_ms": avg_launch_ms}
     if valu:
         r["valu_secondary"] = valu
+        # f64 MFMA and f64 VALU share the datapath (scripts/probes/mfma_valu_overlap.hip: MFMA
+        # waves keep 64 clocks per MFMA while a concurrent v_fma_f64 stream slows from 4.78 to
+        # 12.79 clocks, i.e. keeps 0.374 of its rate).  Floor of a launch, per SIMD: the MFMA clocks
+        # plus the VALU clocks that do not fit beside them (4 per wave64 VALU instruction, all
+        # counted as f64); the plain sum is the no-overlap ceiling
+        n_simd, clk, keep = 1024.0, 2.4e9, 4.78 / 12.79
+        mfma_cyc = steps / 16.0 * n_mfma * 64.0 / n_simd
+        valu_cyc = 4.0 * valu["insts_per_launch"] / n_simd
+        floor = mfma_cyc + max(0.0, valu_cyc - keep * mfma_cyc)
+        r["f64_datapath"] = {"mfma_clocks_per_simd": mfma_cyc, "valu_clocks_per_simd": valu_cyc,
+                             "frac": floor / (clk * t), "frac_no_overlap": (mfma_cyc + valu_cyc) / (clk * t),
+                             "valu_rate_kept_beside_mfma": keep, "clock_ghz": 2.4,
+                             "source": "scripts/probes/mfma_valu_overlap.hip (profiles/r05/c5_datapath)"}
     return r
 
 

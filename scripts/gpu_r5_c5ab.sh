@@ -1,4 +1,6 @@
 #!/bin/bash
+# (record of a round-5 experiment: needs the tree of commit a349d96, whose C5 variants and
+# timing-probe macros were removed afterwards; see profiles/r05/c5_datapath)
 # Round 5, C5: the full-covariance parity tests on the default (software-pipelined) kernel, then
 # a same-box A/B of the C5 config line: pipelined step vs the round-4 step (MCG_FC_KERNEL=1),
 # alternated twice.

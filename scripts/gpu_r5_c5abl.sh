@@ -1,4 +1,6 @@
 #!/bin/bash
+# (record of a round-5 experiment: needs the tree of commit a349d96, whose C5 variants and
+# timing-probe macros were removed afterwards; see profiles/r05/c5_datapath)
 # Round 5, C5 ablation (timing probes, wrong values): the round-4 step (MCG_FC_KERNEL=1) as built,
 # with a VALU fma in place of each MFMA (NOMFMA), and with a 2-multiply hash in place of each
 # Philox call (NOPHILOX); plus the product library's pipelined step for reference.
