@@ -47,7 +47,8 @@ struct KeyBuf {
 };
 
 struct NestedBufs {
-  DevBuf x, ll, lp, nx, nll, nlp, tv, prefix, qadd, st, dead_x, dead_ll, dead_lp, rank, sync, trace, chk, rt_ix, rt_sc;
+  DevBuf x, ll, lp, nx, nll, nlp, tv, prefix, qadd, st, dead_x, dead_ll, dead_lp, rank, sync, trace, chk, rt_ix, rt_sc,
+      fm_sync;
   KeyBuf keys[2], newk, newk_tmp;
   int64_t dead_cap = 0;
   // pinned staging of two in-flight batches' dead (ll, lp) and their completion events
@@ -384,6 +385,14 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   // default: measured slower at C3
   const char* fm_env = std::getenv("MCG_NESTED_FM");
   const bool fuse_walk_merge = fused_merge && k <= 4096 && fm_env && fm_env[0] == '1';
+  a.fm_sync = nullptr;
+  if (fuse_walk_merge) {
+    // group counters, top counter and one go flag per merge workgroup, 128 B apart, zeroed per run
+    const int64_t words = (kSyncGroups + 1 + (n - k + 255) / 256 + 1) * kSyncStride;
+    HC(B.fm_sync.ensure(words * 4), "alloc hand-off flags");
+    HC(hipMemsetAsync(B.fm_sync.p, 0, words * 4, s), "clear hand-off flags");
+    a.fm_sync = (uint32_t*)B.fm_sync.p;
+  }
   // the walkers' draws of a generation in a table the previous merge fills (when it fits)
   a.rt_ix = nullptr;
   a.rt_sc = nullptr;

@@ -24,11 +24,6 @@ struct NestDevState {
   int32_t error;
   long long gen_done;
   double max_ll;            // the largest live ll (the sorted keys' last): the stop test's L_max
-  // the one-launch generation's hand-off counters, each on a 128-B line of its own: the walkers'
-  // first loads read the fields above, which must not share a line with 500 workgroups' atomics
-  alignas(128) unsigned int walk_done;    // walker workgroups done, over the run
-  alignas(128) unsigned int merge_seen;   // merge workgroups past their stop test, over the run
-  char pad_[124];
 };
 
 // The stop / error flags and the generation count are read and written with agent-scope atomics
@@ -85,12 +80,11 @@ struct NestArgs {
   int32_t lanes_hint;       // lanes per walker requested by MCG_NEST_LANES (0: the default)
   int32_t walk_waves;       // walker waves per draw-table workgroup (1, or 2 beyond 256 waves)
   // the merge role of the walk kernel (k <= 4096 with the draw table): workgroups past the
-  // walkers' nwalk_blocks wait until walk_done reaches walk_target, then merge the new keys
-  // into mrg_* (merge_fused_block) or fold the estimate
+  // walkers' nwalk_blocks wait for their go flag, then merge the new keys into mrg_*
+  // (merge_fused_block) or fold the estimate
   int32_t fuse_merge;
   int32_t nwalk_blocks;
-  uint32_t walk_target;
-  uint32_t merge_target;    // merge_seen once every merge workgroup of this generation has registered
+  uint32_t* fm_sync;        // [16 group counters | top counter | go flag per merge workgroup], 128 B apart
   double* mrg_ll;
   long long* mrg_tie;
   int* mrg_slot;
@@ -438,66 +432,86 @@ struct WalkTarget {
 // canonical sum reduced across the P lanes (reduce_canon).  The DE partner rows of step s + 1
 // depend only on the RNG, so they are loaded while step s computes (one step of prefetch).
 // The merge role of a fused walk kernel (FM): workgroup b = blockIdx.x - nwalk_blocks of the
-// generation's merge (b == nblk: the estimate fold).  It takes the walkers' stop decision from the
-// same inputs (so it never waits for walkers that stopped), registers (merge_seen), waits until
-// every walker workgroup has signalled (walk_done, hand-off row 1 of MI355X_MICROARCH.md: sc1
-// stores, vmcnt(0), a workgroup barrier, one agent-scope add; here an sc1 poll, then a workgroup
-// barrier) and every merge workgroup has registered, and runs merge_fused_block with sc1 loads of
-// the walkers' outputs.  The wait is bounded: past ~1 s
+// generation's merge (b == nblk: the estimate fold).  Hand-off (row 1 of MI355X_MICROARCH.md's
+// hand-offs): every walker workgroup stores its outputs sc1, waits vmcnt(0), passes a barrier and
+// adds to its group counter (16 counters on 128-B lines of their own, then a top counter); the
+// workgroup that completes the top counter writes each merge workgroup's go flag (own 128-B line,
+// the generation number).  A merge workgroup polls only its flag -- or the stop / error flags: a
+// generation the walkers stop never signals -- then runs merge_fused_block with sc1 loads of the
+// walkers' outputs.  It reads none of the stop test's inputs (log_vol, est, max_ll), which the
+// estimate and the last key's workgroup rewrite in this launch.  The wait is bounded: past ~1 s
 // it flags an error (the host then reports a failed run) instead of hanging the grid.
+__device__ __forceinline__ uint32_t* fm_go(const NestArgs& a, int b) {
+  return a.fm_sync + (size_t)(kSyncGroups + 1 + b) * kSyncStride;
+}
+
 __device__ __forceinline__ void nest_merge_role(const NestArgs& a) {
   constexpr int BS = 256, KCAP = kSmallSort;
   const int b = (int)blockIdx.x - a.nwalk_blocks;
   const int nblk = (int)((a.n - a.k + BS - 1) / BS);
   if (b > nblk) return;
   NT_STAMP(3, 0);
+  if (nest_stopped(a.st)) return;                       // stopped in an earlier launch
   __shared__ union FmLds {
     MergeLds<BS, KCAP> m;
     EstLds<BS> e;
   } lds;
   __shared__ int s_ok;
-  if (threadIdx.x == 0) {
-    // One thread takes the stop decision and registers the workgroup (merge_seen) before any
-    // merge workgroup may write the state it reads: the estimate fold rewrites log_vol / est and
-    // the last key's workgroup max_ll, so a workgroup placed late would otherwise test the next
-    // generation's state.  Every merge workgroup waits for all nblk + 1 registrations (and the
-    // walkers) before it writes anything.
-    int ok = !nest_stopped(a.st);
-    if (ok && a.mrep > 0) {
-      const double st_lv = a.st->log_vol, st_mx = a.st->max_ll, st_est = a.st->est;
-      const bool st_err = __hip_atomic_load(&a.st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-      const double live = st_lv + st_mx;
-      if (live - plse(st_est, live, kLogTab) <= a.log_epsrel || st_err) ok = 0;   // as the walkers
-    }
-    if (ok) {
-      __hip_atomic_fetch_add(&a.st->merge_seen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  // the hand-off: one thread polls the go flag, the workgroup waits at a barrier
+  auto wait = [&]() -> bool {
+    if (threadIdx.x == 0) {
+      const uint32_t gen1 = (uint32_t)(a.mrep / a.k + 1);
+      const uint32_t* go = fm_go(a, b);
+      int ok = 0;
       for (uint32_t it = 0;; ++it) {
-        if (__hip_atomic_load(&a.st->walk_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.walk_target &&
-            __hip_atomic_load(&a.st->merge_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.merge_target)
-          break;
-        if (it > (1u << 22)) {
-          nest_set(&a.st->error);
-          ok = 0;
+        if (ld1(go) >= gen1) {
+          ok = 1;
           break;
         }
-        __builtin_amdgcn_s_sleep(8);
+        if (nest_stopped(a.st) || __hip_atomic_load(&a.st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+        if (it > (1u << 22)) {
+          nest_set(&a.st->error);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(4);
       }
+      s_ok = ok;
     }
-    s_ok = ok;
+    __syncthreads();
+    NT_STAMP(3, 5);
+    return s_ok != 0;
+  };
+  if (b == nblk) {
+    if (wait()) estimate_body<BS>(a, lds.e);
+  } else {
+    // the survivors' keys (the previous launch's output) are loaded before the wait
+    merge_fused_block<BS, KCAP, true>(a, a.mrg_ll, a.mrg_tie, a.mrg_slot, b, lds.m, wait);
   }
-  __syncthreads();
-  if (!s_ok) return;
-  NT_STAMP(3, 5);
-  if (b == nblk) estimate_body<BS>(a, lds.e);
-  else merge_fused_block<BS, KCAP, true>(a, a.mrg_ll, a.mrg_tie, a.mrg_slot, b, lds.m);
 }
 
-// a walker workgroup of a fused walk kernel (FM) signals the merge role once every one of its
-// waves has finished its stores (stored sc1 where the merge reads them)
+// a walker workgroup of a fused walk kernel (FM) signals once every one of its waves has
+// finished its stores (stored sc1 where the merge reads them); the last one sets the go flags
 __device__ __forceinline__ void nest_walk_signal(const NestArgs& a) {
+  __shared__ int s_last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(&a.st->walk_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t gen1 = (uint32_t)(a.mrep / a.k + 1);
+  if (threadIdx.x == 0) {
+    const int nwb = a.nwalk_blocks, g = (int)blockIdx.x % kSyncGroups;
+    const uint32_t members = (uint32_t)((nwb - g + kSyncGroups - 1) / kSyncGroups);
+    const uint32_t ng = (uint32_t)min(nwb, kSyncGroups);
+    int last = 0;
+    if (__hip_atomic_fetch_add(a.fm_sync + (size_t)g * kSyncStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 ==
+        gen1 * members)
+      last = __hip_atomic_fetch_add(a.fm_sync + (size_t)kSyncGroups * kSyncStride, 1u, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT) + 1 == gen1 * ng;
+    s_last = last;
+  }
+  __syncthreads();
+  if (s_last) {
+    const int nblk = (int)((a.n - a.k + 255) / 256);
+    for (int b = threadIdx.x; b <= nblk; b += blockDim.x) st1(fm_go(a, b), gen1);
+  }
 }
 
 // GP: a DIAG_GAUSS prior, whose log density makes the walker's MH test log u < lp(y) - lp(cur)
@@ -1004,8 +1018,6 @@ hipError_t launch_nest_walk_p(const NestArgs& a, hipStream_t st) {
     // walkers' (dispatched in order, so every walker workgroup is placed before any of them)
     const int64_t nblk = (a.n - a.k + 255) / 256;
     b.nwalk_blocks = (int32_t)gt.x;
-    b.walk_target = (uint32_t)((a.mrep / a.k + 1) * (int64_t)gt.x);
-    b.merge_target = (uint32_t)((a.mrep / a.k + 1) * (nblk + 1));
     const dim3 gf((unsigned)(gt.x + nblk + 1));
     if (a.m.prior_kind == MCG_PRIOR_DIAG_GAUSS)
       hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, false, true, true>), gf, bt, 0, st, b);

@@ -144,10 +144,16 @@ struct MergeLds {
 
 // Block b of the merge.  SC1: the walkers' outputs (new keys, points, ll, lp) were handed off
 // inside the same launch (nest_walk_kernel's merge role), so they are loaded sc1 (ld1); after a
-// kernel boundary plain loads.
-template <int BS, int KCAP, bool SC1>
+// kernel boundary plain loads.  wait(): called by every thread once the survivors' loads (the
+// previous generation's keys) are in flight and before any load of the walkers' outputs; false
+// (uniform) ends the block.
+struct MergeNoWait {
+  __device__ bool operator()() const { return true; }
+};
+
+template <int BS, int KCAP, bool SC1, class Wait = MergeNoWait>
 __device__ __forceinline__ void merge_fused_block(const NestArgs& a, double* oll, long long* otie, int* oslot,
-                                                  const int b, MergeLds<BS, KCAP>& L) {
+                                                  const int b, MergeLds<BS, KCAP>& L, const Wait& wait = Wait()) {
   const int64_t n = a.n, k = a.k, ns = n - k;
   const int nblk = (int)((ns + BS - 1) / BS);
   const int t = threadIdx.x;
@@ -171,19 +177,6 @@ __device__ __forceinline__ void merge_fused_block(const NestArgs& a, double* oll
   // g of the k x D block goes to thread g mod (nblk * BS) of the merge workgroups.
   const int64_t D = a.row_bytes / 8, kD = a.fuse_retire ? a.k * D : 0;
   const int64_t g0 = (int64_t)b * BS + t, gstride = (int64_t)nblk * BS;
-  int sj0 = 0;
-  double cx0 = 0.0, cl0 = 0.0, cp0 = 0.0;
-  int64_t d0 = -1;
-  if (g0 < kD) {
-    const int64_t j = g0 / D;
-    d0 = g0 - j * D;
-    sj0 = ldv(a.newk_slot + j);
-    cx0 = ldv(a.nx + g0);
-    if (d0 == 0) {
-      cl0 = ldv(a.nll + j);
-      cp0 = ldv(a.nlp + j);
-    }
-  }
   double kl = 0.0;
   long long kt = 0;
   int ks = 0;
@@ -197,6 +190,20 @@ __device__ __forceinline__ void merge_fused_block(const NestArgs& a, double* oll
   const bool has_hi = i0 + BS < ns;
   const double hi_l = has_hi ? sll[i0 + BS] : 0.0;
   const long long hi_t = has_hi ? stie[i0 + BS] : 0;
+  if (!wait()) return;
+  int sj0 = 0;
+  double cx0 = 0.0, cl0 = 0.0, cp0 = 0.0;
+  int64_t d0 = -1;
+  if (g0 < kD) {
+    const int64_t j = g0 / D;
+    d0 = g0 - j * D;
+    sj0 = ldv(a.newk_slot + j);
+    cx0 = ldv(a.nx + g0);
+    if (d0 == 0) {
+      cl0 = ldv(a.nll + j);
+      cp0 = ldv(a.nlp + j);
+    }
+  }
   constexpr int kPer = KCAP / BS;
   double nv[kPer];
 #pragma unroll
