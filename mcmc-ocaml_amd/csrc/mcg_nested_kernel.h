@@ -1053,6 +1053,12 @@ hipError_t launch_nest_walk(const NestArgs& a, hipStream_t st) {
   }
   if constexpr (sep && (D == 16 || D == 8)) {          // two dims per lane (WalkLayout W = 2)
     if (a.lanes_hint == 2 * P || a.lanes_hint == -1) return launch_nest_walk_p<D, LIK, 2 * P>(a, st);
+    // D 16 beyond 256 walker waves (k > 4,096): 8 lanes of 2 dims put a walker wave on every
+    // SIMD (k 8,192: walk 38.0 -> 35.0 us a generation, same box; at k 4,096 the 4-lane split
+    // stays ahead, 23.7 vs 29.1 us, profiles/r05/lanes)
+    if constexpr (D == 16) {
+      if (a.lanes_hint == 0 && a.k * P > 256 * 64) return launch_nest_walk_p<D, LIK, 2 * P>(a, st);
+    }
   }
   return launch_nest_walk_p<D, LIK, P>(a, st);
 }

@@ -235,9 +235,10 @@ def test_nested_walker_lane_splits_bit_exact(oracle, T, monkeypatch, lanes, D, d
 @pytest.mark.gpu
 @pytest.mark.parametrize("D,nlive,k", [(16, 12000, 6000), (16, 16384, 8192), (32, 16384, 8192)])
 def test_nested_large_k_one_launch_merge_bit_exact(oracle, T, D, nlive, k):
-    """k in (4096, 8192]: two walker waves per draw-table workgroup and the 512-survivor
-    one-launch merge (merge_fused_kernel<512, 8192>, its extra workgroup folding 8192
-    retirements): the oracle's dead points, log Z and weights bit for bit."""
+    """k in (4096, 8192]: two walker waves per draw-table workgroup (at D 16 the default 8-lane
+    split, two dims per lane, beyond 4,096 walkers) and the 512-survivor one-launch merge
+    (merge_fused_kernel<512, 8192>, its extra workgroup folding 8192 retirements): the oracle's
+    dead points, log Z and weights bit for bit."""
     lik = T.gauss_shell(np.zeros(D), 1.0, 0.2)
     pri = T.box(-2 * np.ones(D), 2 * np.ones(D))
     g = gpu_nested(lik, pri, 23, nlive=nlive, nmcmc=8, mode_hopping_frac=0.1, k=k, max_dead=k * 4)
