@@ -343,6 +343,36 @@ def test_nested_walk_merge_one_launch_bit_exact(oracle, T, monkeypatch, nlive, k
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("case", ["diag32", "shell16_asym_box", "diag16_gauss_prior", "shell8_wide"])
+def test_nested_walk_merge_one_launch_targets_bit_exact(oracle, T, monkeypatch, case):
+    """The one-launch walk + merge on the other walker instances: 8 lanes (D 32), a box that is
+    not symmetric (no |y| <= h form), the Gaussian prior (the walkers' MH test is live) and the
+    two-dims-per-lane split -- the oracle's dead points bit for bit."""
+    monkeypatch.setenv("MCG_NESTED_FM", "1")
+    rng = np.random.default_rng(7)
+    if case == "diag32":
+        D = 32
+        lik = T.diag_gauss(rng.uniform(-0.3, 0.3, D), rng.uniform(0.3, 0.6, D))
+        pri = T.box(-2 * np.ones(D), 2 * np.ones(D))
+    elif case == "shell16_asym_box":
+        D = 16
+        lik = T.gauss_shell(np.zeros(D), 1.0, 0.2)
+        pri = T.box(-2 * np.ones(D), 3 * np.ones(D))
+    elif case == "diag16_gauss_prior":
+        D = 16
+        lik = T.diag_gauss(rng.uniform(-0.3, 0.3, D), rng.uniform(0.2, 0.5, D))
+        pri = T.gauss_prior(np.zeros(D), np.ones(D))
+    else:
+        D = 8
+        monkeypatch.setenv("MCG_NEST_LANES", "wide")
+        lik = T.gauss_shell(np.zeros(D), 1.0, 0.2)
+        pri = T.box(-2 * np.ones(D), 2 * np.ones(D))
+    g = gpu_nested(lik, pri, 19, nlive=1000, nmcmc=12, mode_hopping_frac=0.1, k=64, max_dead=64 * 12)
+    o = oracle_nested(oracle, lik, pri, 19, nlive=1000, nmcmc=12, mode_hop=0.1, k=64, max_iter=64 * 12)
+    assert_nested_same(g, o)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("nlive,k", [(300, 200), (257, 256)])
 def test_nested_large_fraction_generations_bit_exact(oracle, T, nlive, k):
     """Generations retiring most of the live set (k > nlive / 2) and all but one point
