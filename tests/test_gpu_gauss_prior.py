@@ -132,6 +132,20 @@ def test_nested_gauss_prior_bit_exact(oracle, T, D, lik_name, k):
     assert_nested_same(g, o)
 
 
+@pytest.mark.parametrize("lik_name", ["diag", "shell"])
+def test_nested_gauss_prior_large_k_eight_lanes_bit_exact(oracle, T, lik_name):
+    """k 8,192 at D 16: the walkers' default 8-lane split (two dims per lane) beyond 4,096
+    walkers, two walker waves per draw-table workgroup, under the Gaussian prior."""
+    D, k = 16, 8192
+    rng = np.random.default_rng(29)
+    lik = (T.diag_gauss(rng.uniform(-0.3, 0.3, D), rng.uniform(0.2, 0.5, D)) if lik_name == "diag"
+           else T.gauss_shell(np.zeros(D), 1.0, 0.2))
+    pri = _prior(T, D, 5, scale=1.0)
+    g = gpu_nested(lik, pri, 31, nlive=16384, nmcmc=6, mode_hopping_frac=0.1, k=k, max_dead=3 * k)
+    o = oracle_nested(oracle, lik, pri, 31, nlive=16384, nmcmc=6, mode_hop=0.1, k=k, max_iter=3 * k)
+    assert_nested_same(g, o)
+
+
 def test_nested_gauss_prior_converged_bit_exact_and_analytic(oracle, T):
     """A converged run (the stop test fires) equal to the oracle, and log Z within 4 sigma of the
     analytic Gaussian x Gaussian evidence."""
