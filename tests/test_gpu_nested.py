@@ -233,7 +233,8 @@ def test_nested_walker_lane_splits_bit_exact(oracle, T, monkeypatch, lanes, D, d
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("D,nlive,k", [(16, 12000, 6000), (16, 16384, 8192), (32, 16384, 8192)])
+@pytest.mark.parametrize("D,nlive,k", [(16, 12000, 6000), (16, 16384, 8192), (32, 16384, 8192), (16, 9000, 4097),
+                                       (8, 16384, 8192)])
 def test_nested_large_k_one_launch_merge_bit_exact(oracle, T, D, nlive, k):
     """k in (4096, 8192]: two walker waves per draw-table workgroup (at D 16 the default 8-lane
     split, two dims per lane, beyond 4,096 walkers) and the 512-survivor one-launch merge
