@@ -51,8 +51,10 @@ struct NestedBufs {
       fm_sync;
   KeyBuf keys[2], newk, newk_tmp;
   int64_t dead_cap = 0;
-  // pinned staging of two in-flight batches' dead (ll, lp) and their completion events
+  // pinned staging of two in-flight batches' dead (ll, lp) and their completion events; coherent
+  // and device-mapped: the kernels that retire points write them there directly (d_stage)
   double* h_stage[4] = {nullptr, nullptr, nullptr, nullptr};
+  double* d_stage[4] = {nullptr, nullptr, nullptr, nullptr};
   int64_t h_cap = 0;
   NestDevState* h_st = nullptr;
   hipEvent_t done[2] = {nullptr, nullptr};
@@ -457,9 +459,16 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
       if (h) (void)hipHostFree(h);
       h = nullptr;
     }
-    for (auto& h : B.h_stage) HC(hipHostMalloc(&h, (size_t)(kMaxBatch * k) * 8, 0), "alloc pinned staging");
+    for (int i = 0; i < 4; ++i) {
+      HC(hipHostMalloc(&B.h_stage[i], (size_t)(kMaxBatch * k) * 8, hipHostMallocMapped | hipHostMallocCoherent),
+         "alloc pinned staging");
+      HC(hipHostGetDevicePointer((void**)&B.d_stage[i], B.h_stage[i], 0), "map pinned staging");
+    }
     B.h_cap = kMaxBatch * k;
   }
+  // MCG_NESTED_STAGE_COPY=1: stage each batch's dead ll / lp by two device-to-host copies behind
+  // its kernels instead (the copies are blit kernels on the same queue, ~38 us each at C3)
+  const bool stage_copy = std::getenv("MCG_NESTED_STAGE_COPY") != nullptr;
   // the state copies land in pinned memory too: an async copy into pageable memory would block
   // the host until the batch completes and serialise the pipeline
   if (!B.h_st) HC(hipHostMalloc((void**)&B.h_st, 2 * sizeof(NestDevState), 0), "alloc pinned state");
@@ -533,6 +542,9 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
     a.dead_x = (double*)B.dead_x.p;
     a.dead_ll = (double*)B.dead_ll.p;
     a.dead_lp = (double*)B.dead_lp.p;
+    a.h_ll = stage_copy ? nullptr : B.d_stage[2 * q];
+    a.h_lp = stage_copy ? nullptr : B.d_stage[2 * q + 1];
+    a.h_m0 = gen * k;
     slot_dead_x[q] = a.dead_x;
     slot_seq[q] = batch_seq++;
     for (int64_t g = gen; g < gen + G; ++g) {
@@ -582,10 +594,12 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
       if (check) HC(launch_check_sorted(nxt.l(), nxt.t(), n, g, (long long*)B.chk.p + 1, s), "check");
     }
     HC(hipMemcpyAsync(&hst[q], B.st.p, sizeof(NestDevState), hipMemcpyDeviceToHost, s), "read state");
-    HC(hipMemcpyAsync(B.h_stage[2 * q], (double*)B.dead_ll.p + gen * k, G * k * 8, hipMemcpyDeviceToHost, s),
-       "stage dead ll");
-    HC(hipMemcpyAsync(B.h_stage[2 * q + 1], (double*)B.dead_lp.p + gen * k, G * k * 8, hipMemcpyDeviceToHost, s),
-       "stage dead lp");
+    if (stage_copy) {
+      HC(hipMemcpyAsync(B.h_stage[2 * q], (double*)B.dead_ll.p + gen * k, G * k * 8, hipMemcpyDeviceToHost, s),
+         "stage dead ll");
+      HC(hipMemcpyAsync(B.h_stage[2 * q + 1], (double*)B.dead_lp.p + gen * k, G * k * 8, hipMemcpyDeviceToHost, s),
+         "stage dead lp");
+    }
     HC(hipEventRecord(B.done[q], s), "record batch");
     gen += G;
     return MCG_OK;

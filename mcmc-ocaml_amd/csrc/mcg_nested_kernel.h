@@ -61,6 +61,11 @@ struct NestArgs {
   double* dead_x;
   double* dead_ll;
   double* dead_lp;
+  // the batch's host staging (pinned, coherent, device-mapped): each retirement's ll / lp also go
+  // straight to host memory at index m - h_m0, so a batch needs no copy of them (null: none)
+  double* h_ll;
+  double* h_lp;
+  int64_t h_m0;
   double* newk_ll;          // unsorted keys of the new points
   long long* newk_tie;
   int* newk_slot;
@@ -110,6 +115,17 @@ struct NestArgs {
 #else
 #define NT_STAMP(kid, slot) do {} while (0)
 #endif
+
+// one retirement's ll / lp into the dead buffers and, when the batch stages on the host, into the
+// pinned staging buffers (posted writes over PCIe; the host reads them after the batch's event)
+__device__ __forceinline__ void put_dead(const NestArgs& a, int64_t m, double ll, double lp) {
+  a.dead_ll[m] = ll;
+  a.dead_lp[m] = lp;
+  if (a.h_ll) {
+    a.h_ll[m - a.h_m0] = ll;
+    a.h_lp[m - a.h_m0] = lp;
+  }
+}
 
 // an output store read by a later kernel as sc1 (a relaxed agent-scope atomic store: written
 // through and dropped from the XCD's L2, so less is left to write back when the kernel ends);
@@ -640,8 +656,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
           a.dead_x[m * D + d] = a.x[(int64_t)rs * D + d];
           if (d == 0) {
             const double lls = a.ll[rs];
-            a.dead_ll[m] = lls;
-            a.dead_lp[m] = a.lp[rs];
+            put_dead(a, m, lls, a.lp[rs]);
             const double lv = a.st->log_vol + a.prefix[wj];
             __hip_atomic_store(a.tv + wj, lls + (lv + a.qadd[wj]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             a.rank[wj] = 0;
@@ -788,8 +803,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
         if (Lay::valid(sub, i, q)) a.dead_x[m * D + Lay::dim(sub, i, q)] = src[Lay::dim(sub, i, q)];
     if (sub == 0) {
       const double lls = a.ll[ret_slot];
-      a.dead_ll[m] = lls;
-      a.dead_lp[m] = a.lp[ret_slot];
+      put_dead(a, m, lls, a.lp[ret_slot]);
       const double lv = a.st->log_vol + a.prefix[w];
       __hip_atomic_store(a.tv + w, lls + (lv + a.qadd[w]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // nested.ml:138-141
       a.rank[w] = 0;

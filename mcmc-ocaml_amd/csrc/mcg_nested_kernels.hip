@@ -479,8 +479,7 @@ __global__ void __launch_bounds__(kRetireBlock) retire_kernel(const NestArgs a, 
     a.x[(int64_t)s * D + d] = a.nx[j * D + d];
     if (d == 0) {
       const double lls = a.ll[s];
-      a.dead_ll[m] = lls;
-      a.dead_lp[m] = a.lp[s];
+      put_dead(a, m, lls, a.lp[s]);
       const double lv = a.st->log_vol + a.prefix[j];
       st1(a.tv + j, lls + (lv + a.qadd[j]));        // nested.ml:138-141 (log_dv incl. :140)
       a.ll[s] = a.nll[j];
