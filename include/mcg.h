@@ -296,6 +296,13 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
 /* all points of the last nested run (dead in retirement order, then live ascending in ll):
    pts [n_total][D] row-major, ll, lp, log_wts [n_total] (nested_output, nested.ml:20) */
 int mcg_nested_get(mcg_ctx* ctx, double* pts, double* ll, double* lp, double* log_wts);
+/* The last nested run's ll, lp and log_wts [n_total] (as mcg_nested_get writes them) handed to
+   the caller without a copy: three malloc'd arrays the caller owns and releases with mcg_free.
+   Afterwards mcg_nested_get still copies the points (pts) but refuses ll / lp / log_wts
+   (MCG_ESTATE) until the next run.  (No reference counterpart: nested_output's arrays are
+   fresh OCaml arrays, nested.ml:20, which this gives a binding without a second copy.) */
+int mcg_nested_take(mcg_ctx* ctx, double** ll, double** lp, double** log_wts);
+void mcg_free(void* p);
 /* The last nested run's points as rows in a caller-owned device buffer on the context's device
    (the send buffer of a replica all-gather over RCCL), device to device: row i of
    [n_total] = (pts[i][0..D) when with_points, ll[i], lp[i]), `row_stride` doubles apart

@@ -450,6 +450,9 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   R.ll.clear();
   R.lp.clear();
   R.wts.clear();
+  R.taken = false;
+  // (the blocks a take left for this run may still be prefaulting: joined before any of them
+  // can be reallocated)
   EvFold fold(n, k);
   // generations per batch: doubling from 4 up to kMaxBatch (MCG_NESTED_MAX_BATCH)
   const char* mb_env = std::getenv("MCG_NESTED_MAX_BATCH");
@@ -656,12 +659,15 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
     // it only within its capacity (the worker is joined first when it must reallocate)
     const int64_t d0 = gstart[q] * k, d1 = st.gen_done * k;
     if (d1 > d0) {
-      if (R.ll.capacity() < R.ll.size() + (size_t)(d1 - d0)) {
+      if (R.ll.capacity() < R.ll.size() + (size_t)(d1 - d0) || R.lp.capacity() < R.lp.size() + (size_t)(d1 - d0)) {
         join_fold();
-        R.ll.reserve(std::max(2 * R.ll.capacity(), R.ll.size() + (size_t)(d1 - d0) + (size_t)(kMaxBatch * k)));
+        R.join_populate();
+        if (!R.ll.reserve(std::max(2 * R.ll.capacity(), R.ll.size() + (size_t)(d1 - d0) + (size_t)(kMaxBatch * k))))
+          return set_error(ctx, MCG_EFAIL, "out of host memory");
       }
-      R.ll.insert(R.ll.end(), B.h_stage[2 * q], B.h_stage[2 * q] + (d1 - d0));
-      R.lp.insert(R.lp.end(), B.h_stage[2 * q + 1], B.h_stage[2 * q + 1] + (d1 - d0));
+      if (!R.ll.append(B.h_stage[2 * q], B.h_stage[2 * q] + (d1 - d0)) ||
+          !R.lp.append(B.h_stage[2 * q + 1], B.h_stage[2 * q + 1] + (d1 - d0)))
+        return set_error(ctx, MCG_EFAIL, "out of host memory");
     }
     const double* done_dead_x = slot_dead_x[q];      // (before the refill below replaces it)
     const int64_t remaining = max_dead / k - gen;
@@ -693,7 +699,8 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
     }
     if (!inflight[q] && !inflight[q ^ 1]) break;      // max_dead reached
     // fold what is final on the worker while this thread keeps the GPU fed
-    R.wts.resize(R.ll.size());
+    if (R.wts.capacity() < R.ll.size()) R.join_populate();
+    if (!R.wts.resize(R.ll.size())) return set_error(ctx, MCG_EFAIL, "out of host memory");
     fw = std::thread([&fold, llp = R.ll.data(), av = (int64_t)R.ll.size(), wp = R.wts.data()] {
       fold.advance(llp, av, wp);
     });
@@ -752,9 +759,9 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   HC(launch_gather_live((const double*)B.x.p, (const double*)B.ll.p, (const double*)B.lp.p, fin.s(), n, D,
                         (double*)B.dead_x.p + ndead * D, (double*)B.dead_ll.p + ndead,
                         (double*)B.dead_lp.p + ndead, s), "gather live");
-  R.ll.resize((size_t)ntot);
-  R.lp.resize((size_t)ntot);
-  R.wts.resize((size_t)ntot);
+  R.join_populate();
+  if (!R.ll.resize((size_t)ntot) || !R.lp.resize((size_t)ntot) || !R.wts.resize((size_t)ntot))
+    return set_error(ctx, MCG_EFAIL, "out of host memory");
   HC(hipMemcpyAsync(R.ll.data() + ndead, (double*)B.dead_ll.p + ndead, n * 8, hipMemcpyDeviceToHost, s), "copy live");
   HC(hipMemcpyAsync(R.lp.data() + ndead, (double*)B.dead_lp.p + ndead, n * 8, hipMemcpyDeviceToHost, s), "copy live");
   HC(hipStreamSynchronize(s), "copy live");
@@ -880,6 +887,8 @@ int mcg_nested_get(mcg_ctx* ctx, double* pts, double* ll, double* lp, double* lo
     if (rc) return rc;
   }
   const auto t1 = std::chrono::steady_clock::now();
+  if (R.taken && (ll || lp || log_wts))
+    return set_error(ctx, MCG_ESTATE, "the run's ll / lp / weights were handed over (mcg_nested_take)");
   {
     // the three host arrays in chunks over 8 threads (first touch of the caller's pages
     // dominates: the destinations get transparent-huge-page advice, as the point copy's)
@@ -917,6 +926,48 @@ int mcg_nested_get(mcg_ctx* ctx, double* pts, double* ll, double* lp, double* lo
                  std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
   return MCG_OK;
 }
+
+int mcg_nested_take(mcg_ctx* ctx, double** ll, double** lp, double** log_wts) {
+  if (!ctx || !ll || !lp || !log_wts) return MCG_EINVAL;
+  NestedState& R = ctx->nested;
+  if (R.n_total == 0) return set_error(ctx, MCG_ESTATE, "no nested run");
+  if (R.taken) return set_error(ctx, MCG_ESTATE, "the run's ll / lp / weights were already handed over");
+  // the log weights normalised in place (w - log Z, as mcg_nested_get's copy does), over 8 threads
+  const size_t n = R.wts.size();
+  double* w = R.wts.data();
+  const double sh = R.wts_shift;
+  constexpr int kT = 8;
+  auto work = [&](int t) {
+    const size_t c0 = n * t / kT, c1 = n * (t + 1) / kT;
+    for (size_t i = c0; i < c1; ++i) w[i] -= sh;
+  };
+  if (n < ((size_t)1 << 16)) {
+    for (int t = 0; t < kT; ++t) work(t);
+  } else {
+    std::thread th[kT - 1];
+    for (int t = 1; t < kT; ++t) th[t - 1] = std::thread(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+  }
+  R.join_populate();
+  *ll = R.ll.release();
+  *lp = R.lp.release();
+  *log_wts = R.wts.release();
+  R.taken = true;
+  // fresh blocks for the next run, sized like this one, prefaulted in the background (the page
+  // zeroing a fresh block costs would otherwise land on the next run's host loop)
+  const size_t cap = (size_t)R.n_total + (size_t)R.n_total / 8;
+  if (R.ll.reserve_fresh(cap) && R.lp.reserve_fresh(cap) && R.wts.reserve_fresh(cap)) {
+    double* blocks[3] = {R.ll.data(), R.lp.data(), R.wts.data()};
+    const size_t bytes = R.ll.capacity() * sizeof(double);
+    R.populate = std::thread([blocks, bytes] {
+      for (double* b : blocks) (void)madvise(b, bytes, MADV_POPULATE_WRITE);
+    });
+  }
+  return MCG_OK;
+}
+
+void mcg_free(void* p) { std::free(p); }
 
 int mcg_nested_rows_into(mcg_ctx* ctx, double* dev_rows, int64_t row_stride, int32_t with_points) {
   if (!ctx || !dev_rows) return MCG_EINVAL;

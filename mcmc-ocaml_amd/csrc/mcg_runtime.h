@@ -2,10 +2,16 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdint>
+#include <cstdlib>
+#include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
+
+#include <sys/mman.h>
 
 #include "mcg.h"
 #include "mcg_device.h"
@@ -33,10 +39,77 @@ struct KdState {
   DevBuf d_nodes, d_logq, d_box, d_pts, d_root, d_pt_leaf;
 };
 
+// A growable host array of doubles in malloc'd memory, so a finished run's arrays can be handed to
+// the caller without a copy (mcg_nested_take; the caller frees them with mcg_free).  No element is
+// initialised by resize (every element is written before it is read); growth is realloc (an
+// mremap for large blocks: no copy).
+class HostArr {
+ public:
+  HostArr() = default;
+  HostArr(const HostArr&) = delete;
+  HostArr& operator=(const HostArr&) = delete;
+  ~HostArr() { std::free(p_); }
+  size_t size() const { return n_; }
+  size_t capacity() const { return cap_; }
+  double* data() { return p_; }
+  const double* data() const { return p_; }
+  double& operator[](size_t i) { return p_[i]; }
+  double operator[](size_t i) const { return p_[i]; }
+  void clear() { n_ = 0; }
+  bool reserve(size_t c) {
+    if (c <= cap_) return true;
+    void* q = std::realloc(p_, c * sizeof(double));
+    if (!q) return false;
+    p_ = (double*)q;
+    cap_ = c;
+    return true;
+  }
+  bool resize(size_t n) {
+    if (n > cap_ && !reserve(std::max(n, 2 * cap_))) return false;
+    n_ = n;
+    return true;
+  }
+  bool append(const double* a, const double* b) {
+    const size_t m = (size_t)(b - a);
+    if (!resize(n_ + m)) return false;
+    std::memcpy(p_ + n_ - m, a, m * sizeof(double));
+    return true;
+  }
+  // an empty array's first block: 2 MiB aligned (transparent huge pages), not yet touched
+  bool reserve_fresh(size_t c) {
+    if (p_ || c == 0) return reserve(c);
+    const size_t bytes = ((c * sizeof(double)) + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+    void* q = std::aligned_alloc((size_t)2 << 20, bytes);
+    if (!q) return false;
+    (void)madvise(q, bytes, MADV_HUGEPAGE);
+    p_ = (double*)q;
+    cap_ = bytes / sizeof(double);
+    return true;
+  }
+  double* release() {                       // ownership to the caller (free)
+    double* q = p_;
+    p_ = nullptr;
+    n_ = cap_ = 0;
+    return q;
+  }
+
+ private:
+  double* p_ = nullptr;
+  size_t n_ = 0, cap_ = 0;
+};
+
 struct NestedState {
   // last run: ll, lp, wts of every point (dead in retirement order, then live ascending); the
   // rows of every point stay in the device dead buffer (the live rows gathered behind the dead)
-  std::vector<double> ll, lp, wts;
+  HostArr ll, lp, wts;
+  bool taken = false;                     // ll / lp / wts handed to the caller (mcg_nested_take)
+  // after a take: the next run's fresh blocks are prefaulted (MADV_POPULATE_WRITE, which leaves
+  // their contents alone, so the run may write them meanwhile); joined before any reallocation
+  std::thread populate;
+  void join_populate() {
+    if (populate.joinable()) populate.join();
+  }
+  ~NestedState() { join_populate(); }
   double wts_shift = 0.0;                 // wts hold log weights + log Z; mcg_nested_get subtracts it
   int64_t n_total = 0, n_dead = 0, n_gen = 0, nlive = 0, ndim = 0;
   int64_t ndim_k = 0;                     // the device rows' width (ndim zero-padded)

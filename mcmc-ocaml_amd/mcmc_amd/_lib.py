@@ -93,6 +93,8 @@ SIGNATURES = {
     "mcg_nested": ([C.c_void_p, C.POINTER(McgNestedOpts), C.POINTER(McgNestedResult), OBSERVER,
                     C.c_void_p], C.c_int),
     "mcg_nested_get": ([C.c_void_p, _dp, _dp, _dp, _dp], C.c_int),
+    "mcg_nested_take": ([C.c_void_p, C.POINTER(_dp), C.POINTER(_dp), C.POINTER(_dp)], C.c_int),
+    "mcg_free": ([C.c_void_p], None),
     "mcg_state_token": ([C.c_void_p], C.c_uint64),
     "mcg_nested_rows_into": ([C.c_void_p, C.c_void_p, C.c_int64, C.c_int32], C.c_int),
     "mcg_log_total_error_estimate": ([C.c_double, C.c_double, C.c_int64], C.c_double),

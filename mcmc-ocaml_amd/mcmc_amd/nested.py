@@ -2,6 +2,7 @@
 import atexit
 import ctypes as C
 import warnings
+import weakref
 
 import numpy as np
 
@@ -26,14 +27,29 @@ def nested_evidence(log_likelihood, log_prior, epsrel=0.01, nmcmc=1000, nlive=10
     return fetch(ctx, r, log_likelihood.ndim, points, k)
 
 
+def _owned(ptr, n):
+    """A numpy view of n doubles the library handed over (mcg_nested_take), released with
+    mcg_free when the last array referring to it is collected."""
+    if n == 0:
+        L.lib().mcg_free(C.cast(ptr, C.c_void_p))
+        return np.zeros(0)
+    a = np.ctypeslib.as_array(ptr, shape=(n,))
+    weakref.finalize(a, L.lib().mcg_free, C.cast(ptr, C.c_void_p).value)
+    return a
+
+
 def fetch(ctx, r, ndim, points=True, k=None):
-    """nested_output of the context's last run (r: its McgNestedResult): mcg_nested_get's copies
-    of the points (points=True), ll, lp and the log weights."""
+    """nested_output of the context's last run (r: its McgNestedResult): the points copied by
+    mcg_nested_get (points=True); ll, lp and the log weights handed over without a copy
+    (mcg_nested_take), once per run."""
     n = r.n_total
-    pts = np.zeros((n, ndim)) if points else None
-    ll = np.zeros(n); lp = np.zeros(n); w = np.zeros(n)
-    L.check(L.lib().mcg_nested_get(ctx.ptr, L.dptr(pts) if points else None, L.dptr(ll), L.dptr(lp),
-                                   L.dptr(w)), ctx.ptr)
+    pts = None
+    if points:
+        pts = np.zeros((n, ndim))
+        L.check(L.lib().mcg_nested_get(ctx.ptr, L.dptr(pts), None, None, None), ctx.ptr)
+    pl, pp, pw = L._dp(), L._dp(), L._dp()
+    L.check(L.lib().mcg_nested_take(ctx.ptr, C.byref(pl), C.byref(pp), C.byref(pw)), ctx.ptr)
+    ll, lp, w = _owned(pl, n), _owned(pp, n), _owned(pw, n)
     return NestedOutput(r.log_ev, r.log_dev, pts, w, ll, lp, r.n_dead, r.n_gen, bool(r.converged), k)
 
 

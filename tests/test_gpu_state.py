@@ -168,6 +168,43 @@ def test_nested_cap_reports_unconverged_and_failed_run_clears_result(T):
     ctx.close()
 
 
+def test_nested_take_hands_over_the_arrays_once_per_run(T):
+    """mcg_nested_take (what nested.fetch uses): the run's ll / lp / log weights handed over
+    without a copy equal mcg_nested_get's copies of the same run (same seed); afterwards get
+    refuses them (points still copy) and a second take fails until the next run; the handed-over
+    arrays outlive the next run and the context."""
+    import gc
+    from mcmc_amd import Context, nested
+    from mcmc_amd import _lib as L
+    from mcmc_amd._lib import McgError
+    lik = T.gauss_shell(np.zeros(4), 1.0, 0.2)
+    pri = T.box(-2 * np.ones(4), 2 * np.ones(4))
+    ctx = Context(seed=21)
+    r = nested.run_nested(lik, pri, nlive=400, nmcmc=10, k=20, ctx=ctx)
+    n = r.n_total
+    p0 = np.zeros((n, 4)); a0, b0, w0 = np.zeros(n), np.zeros(n), np.zeros(n)
+    L.check(L.lib().mcg_nested_get(ctx.ptr, L.dptr(p0), L.dptr(a0), L.dptr(b0), L.dptr(w0)), ctx.ptr)
+    r = nested.run_nested(lik, pri, nlive=400, nmcmc=10, k=20, ctx=ctx)
+    out = nested.fetch(ctx, r, 4, points=True, k=20)
+    np.testing.assert_array_equal(out[2], p0)
+    np.testing.assert_array_equal(out.ll, a0)
+    np.testing.assert_array_equal(out.lp, b0)
+    np.testing.assert_array_equal(out[3], w0)
+    a = np.zeros(n)
+    assert L.lib().mcg_nested_get(ctx.ptr, None, L.dptr(a), None, None) == L.MCG_ESTATE
+    p = np.zeros((n, 4))
+    L.check(L.lib().mcg_nested_get(ctx.ptr, L.dptr(p), None, None, None), ctx.ptr)
+    np.testing.assert_array_equal(p, p0)
+    with pytest.raises(McgError):
+        nested.fetch(ctx, r, 4, points=False)
+    ll_view = out.ll[5:50]                         # a view keeps the handed-over block alive
+    nested.nested_evidence(lik, pri, nlive=300, nmcmc=10, k=20, ctx=ctx)
+    ctx.close()
+    del out
+    gc.collect()
+    np.testing.assert_array_equal(ll_view, a0[5:50])
+
+
 def test_failed_set_rjmcmc_leaves_counters_unchanged(oracle, T):
     """mcg_set_rjmcmc folds the device tallies into the context totals before it validates the
     models; a model it then rejects (unsupported likelihood kind) must leave get_counters where
