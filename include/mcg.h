@@ -299,8 +299,11 @@ int mcg_nested_get(mcg_ctx* ctx, double* pts, double* ll, double* lp, double* lo
 /* The last nested run's ll, lp and log_wts [n_total] (as mcg_nested_get writes them) handed to
    the caller without a copy: three malloc'd arrays the caller owns and releases with mcg_free.
    Afterwards mcg_nested_get still copies the points (pts) but refuses ll / lp / log_wts
-   (MCG_ESTATE) until the next run.  (No reference counterpart: nested_output's arrays are
-   fresh OCaml arrays, nested.ml:20, which this gives a binding without a second copy.) */
+   (MCG_ESTATE) until the next run.  The context then allocates the next run's host blocks,
+   sized like this run's, and prefaults them in the background (about 24 bytes per point of this
+   run stay resident until the next run or mcg_destroy).  (No reference counterpart:
+   nested_output's arrays are fresh OCaml arrays, nested.ml:20, which this gives a binding
+   without a second copy.) */
 int mcg_nested_take(mcg_ctx* ctx, double** ll, double** lp, double** log_wts);
 void mcg_free(void* p);
 /* The last nested run's points as rows in a caller-owned device buffer on the context's device
