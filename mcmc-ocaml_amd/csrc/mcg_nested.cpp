@@ -463,7 +463,8 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
       h = nullptr;
     }
     for (int i = 0; i < 4; ++i) {
-      HC(hipHostMalloc(&B.h_stage[i], (size_t)(kMaxBatch * k) * 8, hipHostMallocMapped | hipHostMallocCoherent),
+      HC(hipHostMalloc(&B.h_stage[i], (size_t)(kMaxBatch * k) * 8,
+                       hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable),
          "alloc pinned staging");
       HC(hipHostGetDevicePointer((void**)&B.d_stage[i], B.h_stage[i], 0), "map pinned staging");
     }
