@@ -157,3 +157,19 @@ def test_nested_random_combinations_bit_exact(oracle, T, case):
     g = gpu_nested(lik, pri, seed, nlive=nl, nmcmc=case["nmcmc"], mode_hopping_frac=0.1, k=k, max_dead=maxd)
     o = oracle_nested(oracle, lik, pri, seed, nlive=nl, nmcmc=case["nmcmc"], mode_hop=0.1, k=k, max_iter=maxd)
     assert_nested_same(g, o)
+
+
+@pytest.mark.parametrize("D", [3, 9, 24, 40, 64])
+@pytest.mark.parametrize("lik_kind", ["diag", "shell", "fullcov", "mix"])
+def test_differential_evolution_every_kind_and_width_bit_exact(oracle, T, D, lik_kind):
+    """Mcmc.differential_evolution_proposal (mcmc.ml:198-218) at compiled and zero-padded widths for
+    every likelihood kind, mode hopping 0.2: GPU == oracle bit for bit."""
+    rng = np.random.default_rng(D * 11 + len(lik_kind))
+    lik = _likelihood(T, rng, lik_kind, D)
+    pri = _prior(T, rng, "box", D)
+    samples = rng.normal(0.0, 0.8, size=(300, D))
+    de = T.differential_evolution_proposal(samples, 0.2)
+    x0 = rng.uniform(-1.0, 1.0, size=(D, 257))
+    g = run_gpu(lik, pri, de, x0, 91, 4, 2, 6)
+    o = run_oracle(oracle, lik, pri, T.Proposal(4, np.concatenate([[0.2, 300], samples.ravel()])), x0, 91, 4, 2, 6)
+    assert_same(g, o)
