@@ -424,9 +424,19 @@ __global__ void __launch_bounds__(BS) merge_fused_kernel(const NestArgs a, doubl
 
 hipError_t launch_merge_fused(const NestArgs& a, double* oll, long long* otie, int* oslot, hipStream_t s) {
   if (a.k > kFusedMax || a.k < 1 || !a.est_in_rank) return hipErrorInvalidValue;
-  if (a.k <= kSmallSort) {
+  // k <= 4096: 512 survivors a workgroup by default.  Every workgroup classifies all k new keys
+  // (f64 / i64 compares, the launch's bulk), so halving the workgroups halves that work; 256 a
+  // workgroup (MCG_MERGE_BS=256, the round-4 shape) classifies twice as much in total
+  static const int merge_bs = [] {
+    const char* e = getenv("MCG_MERGE_BS");
+    return e && atoi(e) == 256 ? 256 : 512;
+  }();
+  if (a.k <= kSmallSort && merge_bs == 256) {
     const unsigned nblk = (unsigned)((a.n - a.k + 255) / 256);
     hipLaunchKernelGGL((merge_fused_kernel<256, kSmallSort>), dim3(nblk + 1), dim3(256), 0, s, a, oll, otie, oslot);
+  } else if (a.k <= kSmallSort) {
+    const unsigned nblk = (unsigned)((a.n - a.k + 511) / 512);
+    hipLaunchKernelGGL((merge_fused_kernel<512, kSmallSort>), dim3(nblk + 1), dim3(512), 0, s, a, oll, otie, oslot);
   } else {
     const unsigned nblk = (unsigned)((a.n - a.k + 511) / 512);
     hipLaunchKernelGGL((merge_fused_kernel<512, kFusedMax>), dim3(nblk + 1), dim3(512), 0, s, a, oll, otie, oslot);
