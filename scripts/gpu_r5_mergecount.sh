@@ -1,4 +1,5 @@
 #!/bin/bash
+# (needs lib/libmcg_old.so built from commit 47b1624 and lib/libmcg_trace.so from the counting-form sources, both since removed)
 # Round 5, C3: the merge's counting form for small subsets (every survivor against every subset
 # key, wave-ballot counts; no binary searches) and 32-bit tie compares -- nested parity, then a
 # same-box A/B of the C3 line against lib/libmcg_old.so (the previous commit's merge), alternated,

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (needs lib/libmcg_trace.so: the nested objects rebuilt with -DMCG_NEST_TRACE and linked beside the rest, as in LABLOG round 5)
 # Round 5, C3: merge workgroups of 512 survivors at k <= 4096 (half the workgroups, so half the
 # new-key classification) -- nested parity, then a same-box A/B of the C3 line against
 # MCG_MERGE_BS=256, alternated, then the phase stamps of generation 200 for both from
