@@ -14,7 +14,7 @@ timeout -k 10 400 python3 scripts/bench_configs.py c3 c3k8 c3n1k --out gpurun_ou
 python3 -c "
 import json
 for l in open('gpurun_out/end/configs_c3.jsonl'):
-    d=json.loads(l); print(d['config'] if isinstance(d['config'], str) else d['config'].get("workload"), '%.4g' % d['value'], d['roofline'].get('frac'))"
+    d=json.loads(l); print(d['config'] if isinstance(d['config'], str) else d['config'].get('workload'), '%.4g' % d['value'], d['roofline'].get('frac'))"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/end/trace -o run --output-format csv -- \
   python3 scripts/bench_configs.py c3 --out gpurun_out/end/trace_configs.jsonl > gpurun_out/end/trace.log 2>&1 || exit 1
 python3 - <<'PY'
