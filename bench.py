@@ -254,6 +254,10 @@ def main():
     dist = world > 1 or backend == "nccl"
     if os.environ.get("MCG_BENCH_DEVICE"):
         local = int(os.environ["MCG_BENCH_DEVICE"])
+    elif backend == "nccl" and world > torch.cuda.device_count():
+        # one GPU per rank: fewer visible GPUs than ranks would put two ranks on one card (or
+        # fail inside RCCL); refuse before any GPU work
+        raise SystemExit("bench: %d ranks over RCCL but only %d visible GPU(s)" % (world, torch.cuda.device_count()))
     if dist:
         import torch.distributed as tdist
         torch.cuda.set_device(local)
@@ -305,12 +309,25 @@ def main():
         mean, sd, log_z_hm = reduce_stats(D, ctx.tile_stats(), device=comm)
     barrier()
     elapsed = time.perf_counter() - t0
+    elapsed_own = elapsed
     if dist:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=comm)
         tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
         elapsed = float(tt.item())
     timing = ctx.kernel_timing("mh")
     acc, rej = ctx.counters()
+    # per-rank record for the line's self-check (gathered to rank 0): which GPU this rank drove,
+    # its own elapsed time and mean launch time
+    props = torch.cuda.get_device_properties(dev)
+    me = {"rank": rank, "local_rank": local, "device": torch.cuda.current_device(),
+          "pci_bus_id": getattr(props, "pci_bus_id", None), "uuid": str(getattr(props, "uuid", "")),
+          "elapsed_s": elapsed_own, "avg_launch_ms": timing["total_ms"] / max(timing["launches"], 1),
+          "launches": timing["launches"]}
+    if dist:
+        ranks = [None] * world
+        tdist.all_gather_object(ranks, me)
+    else:
+        ranks = [me]
     # |delta log-evidence| leg (outside the timed region and `value`): Nested.nested_evidence on
     # the same target, one replica of --nested-nlive live points per GPU merged over the ranks
     nest = None
@@ -366,6 +383,10 @@ def main():
             tdist.destroy_process_group()
         return
     # rank 0 only, at every N (the other ranks wait in the final barrier)
+    rk = rank_check(ranks, world, backend, dist, tdist if dist else None)
+    if backend == "nccl" and not (rk["one_gpu_per_rank"] and rk["world_matches"]):
+        raise SystemExit("bench: %d ranks over RCCL drove %d distinct GPU(s) (world %d): %s"
+                         % (world, rk["distinct_gpus"], rk["rccl_world"], json.dumps(rk["per_rank"])))
     cpu = None if args.no_cpu_baseline else cpu_baseline(args, mu, sg, s)
     line = {
         "metric": METRIC,
@@ -397,6 +418,7 @@ def main():
                                       "K timed mh_kernel launches (mcg_kernel_timing), averaged",
                      "valu": pmc_valu(D, N, S, per_launch)},
         "cpu_baseline": cpu,
+        "ranks": rk,
         "accept_frac": acc / max(acc + rej, 1),
         "log_evidence": log_evidence_line(nest, log_z_hm, lz_true),
         "posterior_check": {"max_abs_mean_err": float(np.max(np.abs(mean - mu))),
@@ -406,6 +428,23 @@ def main():
     if dist:
         tdist.barrier()
         tdist.destroy_process_group()
+
+
+def rank_check(ranks, world, backend, dist, tdist):
+    """The line's self-check of a multi-GPU run: the process group's own size and backend, each
+    rank's GPU (ordinal, PCI bus, UUID), elapsed time and mean launch time, their spread, and
+    whether every rank drove a GPU of its own (RCCL: one GPU per rank; a gloo rehearsal may share)."""
+    el = [r["elapsed_s"] for r in ranks]
+    lm = [r["avg_launch_ms"] for r in ranks]
+    gpus = {(r["pci_bus_id"], r["uuid"], r["device"]) for r in ranks}
+    return {"rccl_world": tdist.get_world_size() if dist else 1,
+            "backend": tdist.get_backend() if dist else "none",
+            "world_matches": (tdist.get_world_size() if dist else 1) == world == len(ranks),
+            "distinct_gpus": len(gpus), "one_gpu_per_rank": len(gpus) == len(ranks),
+            "per_rank": sorted(ranks, key=lambda r: r["rank"]),
+            "elapsed_s_min": min(el), "elapsed_s_max": max(el),
+            "avg_launch_ms_min": min(lm), "avg_launch_ms_max": max(lm),
+            "launch_spread": max(lm) / min(lm) - 1.0 if min(lm) > 0 else None}
 
 
 def log_evidence_line(nest, log_z_hm, lz_true):

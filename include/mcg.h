@@ -83,7 +83,7 @@ enum {
    Stats.draw_uniform, stats.ml:126-128) or a DIAG_GAUSS prior (draw_prior = mu + sigma z per
    dim, Stats.draw_gaussian, stats.ml:113-124); with the Gaussian prior the walkers' constrained
    MH test log u < log_prior y - log_prior x (nested.ml:54-59) is a real test.  The reversible
-   jump sampler (mcg_set_rjmcmc) takes FLAT and box priors only. */
+   jump sampler (mcg_set_rjmcmc) takes every prior kind per model (lpa / lpb, mcmc.ml:116-118). */
 enum { MCG_PRIOR_FLAT = 0, MCG_PRIOR_BOX = 1, MCG_PRIOR_OPEN_BOX = 2, MCG_PRIOR_DIAG_GAUSS = 3 };
 
 /* ---- proposal kinds (replace jump_proposal / log_jump_prob, mcmc.mli:58-60) ----
@@ -108,7 +108,10 @@ enum { MCG_PRIOR_FLAT = 0, MCG_PRIOR_BOX = 1, MCG_PRIOR_OPEN_BOX = 2, MCG_PRIOR_
                   always its density log q(y)).  Weights are normalised by their sum; the mixture
                   log_jump_prob folds log p_i + ljp_i with the reference's log(1 + exp) log-sum
                   (mcmc.ml:155-163).  A KD_INTERP component requires mcg_set_kd_proposal first
-                  (which itself selects the plain KD proposal; set the MIXTURE after it). */
+                  (which itself selects the plain KD proposal; set the MIXTURE after it).
+                  Weights whose rounded normalised walk lets the largest uniform draw (1 - 2^-53)
+                  pass every component are refused with MCG_EFAIL: the reference raises Failure
+                  for such a draw (mcmc.ml:173), and the walk is monotone in the draw. */
 enum { MCG_PROP_GAUSS = 1, MCG_PROP_WRAP_UNIFORM = 2, MCG_PROP_KD_INTERP = 3, MCG_PROP_DE = 4,
        MCG_PROP_MIXTURE = 5 };
 enum { MCG_MIX_GAUSS = 1, MCG_MIX_SHIFT_UNIFORM = 2, MCG_MIX_WRAP_UNIFORM = 3,
@@ -196,12 +199,12 @@ int64_t mcg_last_run_steps(const mcg_ctx* ctx);
 int mcg_last_run_lanes(const mcg_ctx* ctx);
 
 /* ---- reversible-jump MCMC between two models (Mcmc.make_rjmcmc_sampler / rjmcmc_array,
-   mcmc.ml:84-153) ----
+   mcmc.ml:83-153) ----
    Each chain carries a model tag (0 = A, 1 = B) and a point of that model's dimension (padded
    with zeros to max(ndim_A, ndim_B) in the [Dmax][N] state).  A step draws u ~ U[0,1): with
    probability p_tag an internal jump of the current model, else a transition into the other
-   model (mcmc.ml:93-103); log_jump_prob and the model log prior log p_m + lp_m follow
-   mcmc.ml:104-116.  Likelihood kinds: FLAT, DIAG_GAUSS, GAUSS_SHELL, FULLCOV_GAUSS; priors as
+   model (mcmc.ml:92-102); log_jump_prob and the model log prior log p_m + lp_m follow
+   mcmc.ml:103-118.  Likelihood kinds: FLAT, DIAG_GAUSS, GAUSS_SHELL, FULLCOV_GAUSS; priors as
    above.  Jump kinds (internal and into):
      MCG_RJ_JUMP_GAUSS       s[1] or s[D]   random walk y = x + s z, log_jump_prob 0
      MCG_RJ_JUMP_WRAP        lo, hi, dx     Mcmc.uniform_wrapping per dim, log_jump_prob 0
@@ -221,19 +224,19 @@ typedef struct {
   int32_t into_kind;  const double* into_params;  size_t n_into;   /* jump into this model (jintoa, ljpintoa) */
   const double* kd_pts; int64_t kd_M;              /* [M][ndim] tree points for the KD kinds */
   const double* kd_low; const double* kd_high;     /* tree bounds (Interpolate_pdf.make) */
-  double model_prior;                              /* pa / pb (pa + pb = 1, mcmc.ml:91) */
+  double model_prior;                              /* pa / pb (pa + pb = 1, mcmc.ml:90) */
 } mcg_rj_model;
 
 int mcg_set_rjmcmc(mcg_ctx* ctx, const mcg_rj_model* a, const mcg_rj_model* b);
-/* model[N] (0 = A, 1 = B) or NULL for rjmcmc_array's fair coin per chain (mcmc.ml:120);
+/* model[N] (0 = A, 1 = B) or NULL for rjmcmc_array's fair coin per chain (mcmc.ml:123);
    xa [ndim_A][N], xb [ndim_B][N]: the start point of each chain in model A and in model B (the
    (a, b) pair of rjmcmc_array, per chain); the chain starts from the one of its model.  ll / lp
-   are evaluated on the device (lp includes log p_model, mcmc.ml:122-124).  Then mcg_run runs
-   rjmcmc_array's schedule (mcmc.ml:125-132) over every chain; the state and records use the
+   are evaluated on the device (lp includes log p_model, mcmc.ml:126-128).  Then mcg_run runs
+   rjmcmc_array's schedule (mcmc.ml:129-139) over every chain; the state and records use the
    padded [Dmax][N] layout (dims beyond the chain's model are 0). */
 int mcg_rj_init(mcg_ctx* ctx, int64_t nchains, const uint8_t* model, const double* xa, const double* xb);
 /* model tags: current state [N] and recorded samples [n_rec][N] of the last run (any may be
-   NULL); counts = rjmcmc_model_counts over every recorded sample of every chain (mcmc.ml:136-144) */
+   NULL); counts = rjmcmc_model_counts over every recorded sample of every chain (mcmc.ml:141-149) */
 int mcg_rj_get_models(mcg_ctx* ctx, uint8_t* state_model, uint8_t* rec_model);
 int mcg_rj_model_counts(mcg_ctx* ctx, uint64_t* na, uint64_t* nb);
 

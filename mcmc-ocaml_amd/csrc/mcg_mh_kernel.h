@@ -1014,7 +1014,8 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP, UNI>::kBlock), (MhSh
       else if constexpr (PROP == MCG_PROP_MIXTURE) {
         static_assert(P == 1, "MIXTURE: one lane per chain");
         // pick a component: Random.float 1.0 walked down the normalised weights (mcmc.ml:168-173);
-        // a u past the last weight (rounding of the normalised sum) takes the last component
+        // (a u past the last weight cannot occur: mcg_set_proposal refuses weights whose walk
+        // lets the largest draw fall through, pack_mixture)
         using M = MixLayout<D>;
         const int nc = (int)qprop[0];
         const u32x4 ws = rng(gid, tlo, CALL_MIX, TAG_MH, thi);

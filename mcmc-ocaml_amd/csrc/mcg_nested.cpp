@@ -344,7 +344,7 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   }
   HC(hipMemcpyAsync(B.prefix.p, prefix.data(), (k + 1) * 8, hipMemcpyHostToDevice, s), "copy prefix");
   HC(hipMemcpyAsync(B.qadd.p, qadd.data(), k * 8, hipMemcpyHostToDevice, s), "copy qadd");
-  NestDevState st0{0.0, -HUGE_VAL, 0, 0, 0, -HUGE_VAL};
+  NestDevState st0{{0.0, 0.0}, {-HUGE_VAL, -HUGE_VAL}, 0, 0, 0, -HUGE_VAL};
   HC(hipMemcpyAsync(B.st.p, &st0, sizeof st0, hipMemcpyHostToDevice, s), "copy state");
 
   NestArgs a{};
@@ -412,6 +412,37 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
     a.rt_ix = (unsigned long long*)B.rt_ix.p;
     a.rt_sc = (double2*)B.rt_sc.p;
   }
+  // Split merge (MCG_NESTED_SPLIT=1, opt-in): the head of each
+  // generation's merge (keys [0, k), kernel merge_head_kernel) on the critical path, its tail
+  // (positions >= k) and the generation's estimate inside the next walk's launch.  Needs the draw
+  // table's walk layout and the in-walk retirement.  Bit-exact, but measured slower at C3 than
+  // the one-launch merge of every position (the default)
+  int base_off = 0;                                  // set once the initial sort has run
+  auto base_keys = [&](int64_t g) { return base_off + g; };
+  const char* sp_env = std::getenv("MCG_NESTED_SPLIT");
+  const bool split = fused_merge && !fuse_walk_merge && k <= kSmallSort && a.fuse_retire && a.rt_ix &&
+                     sp_env && sp_env[0] == '1';
+  const int32_t tail_nblk = (int32_t)((n - k + 255) / 256);
+  auto set_tail = [&](int64_t gp) {                  // the tail of generation gp
+    KeyBuf& in = B.keys[(base_keys(gp)) % 2];
+    KeyBuf& out = B.keys[(base_keys(gp + 1)) % 2];
+    KeyBuf& nk = (gp & 1) ? B.newk_tmp : B.newk;
+    a.tl_nblk = tail_nblk;
+    a.tl_mrep = gp * k;
+    a.tl_gen1 = gp + 1;
+    a.tl_key_ll = in.l();
+    a.tl_key_tie = in.t();
+    a.tl_key_slot = in.s();
+    a.tl_newk_ll = nk.l();
+    a.tl_newk_slot = nk.s();
+    a.tl_out_ll = out.l();
+    a.tl_out_tie = out.t();
+    a.tl_out_slot = out.s();
+    a.tl_samp_ll = out.sl();
+    a.tl_samp_tie = out.st();
+  };
+  a.split = split ? 1 : 0;
+  a.est_in_walk = split ? 1 : 0;
   a.sync = (uint32_t*)B.sync.p;
   a.tv = (double*)B.tv.p;
   a.prefix = (const double*)B.prefix.p;
@@ -439,6 +470,7 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
   HC(launch_sort_keys(B.keys[0].l(), B.keys[0].t(), B.keys[0].s(), B.keys[1].l(), B.keys[1].t(),
                       B.keys[1].s(), n, &in_tmp, s, nullptr), "sort live keys");
   const int base = in_tmp ? 1 : 0;                   // generation g reads keys[(base + g) % 2]
+  base_off = base;
   HC(launch_key_sample(B.keys[base].l(), B.keys[base].t(), n, B.keys[base].sl(), B.keys[base].st(), s, a.st),
      "sample live keys");
   HC(launch_walk_draws(a, 0, s), "first draws");
@@ -571,8 +603,23 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
       a.mrg_tie = nxt.t();
       a.mrg_slot = nxt.s();
       a.fuse_merge = (fuse_walk_merge && a.rt_ix) ? 1 : 0;
+      if (split) {
+        // this generation's new keys go to half g & 1 (the tail in this launch reads the other)
+        KeyBuf& nk = (g & 1) ? B.newk_tmp : B.newk;
+        a.newk_ll = nk.l();
+        a.newk_tie = nk.t();
+        a.newk_slot = nk.s();
+        if (g > 0) set_tail(g - 1);
+        else a.tl_nblk = 0;
+      }
       HC(walk(a, s), "nested walk");
       if (ctx->timing) timing_end(ctx, e0, e1, 1);
+      if (split) {
+        // generation g - 1's keys are complete once this walk (its tail) has run
+        if (check && g > 0) HC(launch_check_sorted(cur.l(), cur.t(), n, g - 1, (long long*)B.chk.p + 1, s), "check");
+        HC(launch_merge_head(a, nxt.l(), nxt.t(), nxt.s(), s), "merge head");
+        continue;
+      }
       if (a.fuse_merge) {                 // merged in the walk's launch (or right after it)
         if (check) HC(launch_check_sorted(nxt.l(), nxt.t(), n, g, (long long*)B.chk.p + 1, s), "check");
         continue;
@@ -648,6 +695,8 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
     st = hst[q];
     if (st.error) {
       if (inflight[q ^ 1]) (void)hipEventSynchronize(B.done[q ^ 1]);
+      if (st.error == 2)                             // (MCG_NESTED_FM) a merge workgroup's bounded wait
+        return set_error(ctx, MCG_EFAIL, "nested: the walk -> merge hand-off timed out (MCG_NESTED_FM)");
       return set_error(ctx, MCG_EFAIL, "Error in draw_new_live_point: new log(L) below the threshold");
     }
     auto join_fold = [&] {
@@ -706,6 +755,15 @@ int mcg_nested(mcg_ctx* ctx, const mcg_nested_opts* opts, mcg_nested_result* res
       fold.advance(llp, av, wp);
     });
     q ^= 1;
+  }
+  if (split && st.gen_done > 0) {
+    // the last generation's tail: run by the walk that found the stop, not at all when the run
+    // ended at max_dead; idempotent, so it is always enqueued
+    set_tail(st.gen_done - 1);
+    HC(launch_merge_tail(a, s), "merge tail");
+    if (check)
+      HC(launch_check_sorted(B.keys[(base + st.gen_done) % 2].l(), B.keys[(base + st.gen_done) % 2].t(), n,
+                             st.gen_done - 1, (long long*)B.chk.p + 1, s), "check");
   }
   const auto t_gen = now();
 #ifdef MCG_NEST_TRACE

@@ -17,9 +17,12 @@
 
 namespace mcg {
 
+// log_vol / est are double-buffered by generation parity: generation g reads half g & 1 (its stop
+// test, its dead points' log dv) and its estimate fold writes half (g + 1) & 1, so a fold that runs
+// while generation g's walk is still reading (the split merge's in-walk estimate) never races it
 struct NestDevState {
-  double log_vol;
-  double est;
+  double log_vol[2];
+  double est[2];
   int32_t stopped;
   int32_t error;
   long long gen_done;
@@ -93,6 +96,26 @@ struct NestArgs {
   double* mrg_ll;
   long long* mrg_tie;
   int* mrg_slot;
+  // split merge (round 6): the head kernel writes the merged keys [0, k); the
+  // tail (positions >= k) of generation g runs in walk g + 1's launch, in tl_nblk workgroups past
+  // its nwalk_blocks walker workgroups (0: none), from generation g's inputs below, and only when
+  // generation g's head ran (gen_done >= tl_gen1)
+  int32_t split;
+  int32_t est_in_walk;      // split merge: the generation's estimate is folded during its walk by
+                            // one workgroup past the tail's, once every table-filling wave has
+                            // stored its dead points' tv (counter a.sync[0])
+  int32_t tl_nblk;
+  int64_t tl_mrep, tl_gen1;
+  const double* tl_key_ll;  // generation g's keys (the merge's input)
+  const long long* tl_key_tie;
+  const int* tl_key_slot;
+  double* tl_newk_ll;       // generation g's new keys (double-buffered by generation parity)
+  int* tl_newk_slot;
+  double* tl_out_ll;        // the merged keys (this walk's keys: positions >= k)
+  long long* tl_out_tie;
+  int* tl_out_slot;
+  double* tl_samp_ll;
+  long long* tl_samp_tie;
   uint32_t row_bytes;       // D * 8: the draw table holds DE pairs as row byte offsets
   double* tv;               // ll + log dv of this generation's dead points (padded pow2)
   const double* prefix;     // [k+1] sum_{j'<j} log1p(-1/(n-j'))
@@ -115,6 +138,8 @@ struct NestArgs {
 #else
 #define NT_STAMP(kid, slot) do {} while (0)
 #endif
+
+__device__ __forceinline__ int gen_par(const NestArgs& a) { return (int)((a.mrep / a.k) & 1); }
 
 // one retirement's ll / lp into the dead buffers and, when the batch stages on the host, into the
 // pinned staging buffers (posted writes over PCIe; the host reads them after the batch's event)
@@ -486,7 +511,8 @@ __device__ __forceinline__ void nest_merge_role(const NestArgs& a) {
         }
         if (nest_stopped(a.st) || __hip_atomic_load(&a.st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
         if (it > (1u << 22)) {
-          nest_set(&a.st->error);
+          // the hand-off's own error code (2): reported as a timeout, not as a failed draw
+          __hip_atomic_store(&a.st->error, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
         __builtin_amdgcn_s_sleep(4);
@@ -503,6 +529,65 @@ __device__ __forceinline__ void nest_merge_role(const NestArgs& a) {
     // the survivors' keys (the previous launch's output) are loaded before the wait
     merge_fused_block<BS, KCAP, true>(a, a.mrg_ll, a.mrg_tie, a.mrg_slot, b, lds.m, wait);
   }
+}
+
+// The deferred tail of generation g's merge (split merge): survivor block b of the BS = 256
+// partition (the walk kernel's workgroup size), positions >= k only.  It reads nothing this
+// launch's walkers write (generation g's keys and new keys; the walkers write generation g + 1's
+// new keys into the other half) and writes positions the walkers do not read (they read [0, k)).
+__device__ __forceinline__ void nest_tail_block(const NestArgs& a, int b) {
+  if (__hip_atomic_load(&a.st->gen_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.tl_gen1) return;
+  NestArgs t = a;
+  t.key_ll = a.tl_key_ll;
+  t.key_tie = a.tl_key_tie;
+  t.key_slot = a.tl_key_slot;
+  t.newk_ll = a.tl_newk_ll;
+  t.newk_slot = a.tl_newk_slot;
+  t.mrep = a.tl_mrep;
+  t.out_samp_ll = a.tl_samp_ll;
+  t.out_samp_tie = a.tl_samp_tie;
+  t.fuse_retire = 0;
+  __shared__ MergeLds<256, kSmallSort> ml;
+  merge_fused_block<256, kSmallSort, false, MergeNoWait, kMergeTail>(t, a.tl_out_ll, a.tl_out_tie, a.tl_out_slot, b, ml);
+}
+
+// The split merge's estimate of generation g, folded inside walk g: the workgroup past the tail's
+// makes the generation's stop test (as every walk workgroup does; a stopping generation retires
+// nothing), waits until every table-filling wave has stored its tv (a.sync[0] counts them; bounded,
+// error 2 past ~1 s) and folds est / log_vol into half (g + 1) & 1 -- which this generation's
+// stop test and tv never read.  Off the generation's serial path: the walk runs ~20 us, the tv
+// stores land in the first ~2.
+__device__ __forceinline__ void nest_est_role(const NestArgs& a, uint32_t nfill) {
+  if (nest_stopped(a.st)) return;
+  if (a.mrep > 0) {
+    const int g = gen_par(a);
+    const double live = a.st->log_vol[g] + a.st->max_ll;
+    const bool err = __hip_atomic_load(&a.st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    if (live - plse(a.st->est[g], live, kLogTab) <= a.log_epsrel || err) return;
+  }
+  __shared__ int s_ok;
+  if (threadIdx.x == 0) {
+    int ok = 0;
+    for (uint32_t it = 0;; ++it) {
+      if (ld1(a.sync) >= nfill) {
+        ok = 1;
+        break;
+      }
+      if (__hip_atomic_load(&a.st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+      if (it > (1u << 22)) {
+        __hip_atomic_store(&a.st->error, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+    if (ok) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    s_ok = ok;
+  }
+  __syncthreads();
+  if (!s_ok) return;
+  __shared__ EstLds<256> el;
+  estimate_body<256>(a, el);
+  if (threadIdx.x == 0) st1(a.sync, 0u);                 // (the only reader: reset for walk g + 1)
 }
 
 // a walker workgroup of a fused walk kernel (FM) signals once every one of its waves has
@@ -542,6 +627,15 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
       nest_merge_role(a);
       return;
     }
+  } else if constexpr (TAB) {
+    if ((int)blockIdx.x >= a.nwalk_blocks) {            // split merge: the estimate, the previous tail
+      // (the estimate's workgroup right behind the walkers': dispatched in order, it is placed
+      // before the tail's ~500 workgroups queue for CUs)
+      const int b = (int)blockIdx.x - a.nwalk_blocks - a.est_in_walk;
+      if (b < 0) nest_est_role(a, (uint32_t)(a.nwalk_blocks * (4 - a.walk_waves)));
+      else nest_tail_block(a, b);
+      return;
+    }
   }
   using Lay = WalkLayout<D, P>;
   constexpr int NL = Lay::NL;
@@ -556,7 +650,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
   // group's draws and the partner-row indices of the ring.  All are plain reads of buffers the
   // previous kernels finished.
   const bool stopped0 = nest_stopped(a.st);
-  const double st_lv = a.st->log_vol, st_mx = a.st->max_ll, st_est = a.st->est;
+  const double st_lv = a.st->log_vol[gen_par(a)], st_mx = a.st->max_ll, st_est = a.st->est[gen_par(a)];
   const bool st_err = __hip_atomic_load(&a.st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
   // with the draw table a 256-thread workgroup holds ww walker waves (waves 0 .. ww-1, one SIMD
   // each) and 4 - ww table-filling waves: one walker wave per SIMD of the chip up to 1,024
@@ -657,14 +751,19 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
           if (d == 0) {
             const double lls = a.ll[rs];
             put_dead(a, m, lls, a.lp[rs]);
-            const double lv = a.st->log_vol + a.prefix[wj];
+            const double lv = a.st->log_vol[gen_par(a)] + a.prefix[wj];
             __hip_atomic_store(a.tv + wj, lls + (lv + a.qadd[wj]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             a.rank[wj] = 0;
           }
         }
+        if (a.est_in_walk) {                           // this wave's tv are stored: count it
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if ((threadIdx.x & 63) == 0)
+            __hip_atomic_fetch_add(a.sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
       // (the stride counts the walker workgroups only: a fused launch's merge workgroups fill nothing)
-      const int64_t nwb = FM ? (int64_t)a.nwalk_blocks : (int64_t)gridDim.x;
+      const int64_t nwb = (int64_t)a.nwalk_blocks;
       walk_draws_fill<!Tgt::kFold>(a, a.mrep + a.k, (int64_t)blockIdx.x * nf + (threadIdx.x - wl), nwb * nf, lt);
 #ifdef MCG_NEST_TRACE
       if (a.trace && (int)threadIdx.x == wl && blockIdx.x < 1024)   // the table-filling waves' end
@@ -804,7 +903,7 @@ __global__ void __launch_bounds__(256) nest_walk_kernel(const NestArgs a) {
     if (sub == 0) {
       const double lls = a.ll[ret_slot];
       put_dead(a, m, lls, a.lp[ret_slot]);
-      const double lv = a.st->log_vol + a.prefix[w];
+      const double lv = a.st->log_vol[gen_par(a)] + a.prefix[w];
       __hip_atomic_store(a.tv + w, lls + (lv + a.qadd[w]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // nested.ml:138-141
       a.rank[w] = 0;
     }
@@ -1041,13 +1140,16 @@ hipError_t launch_nest_walk_p(const NestArgs& a, hipStream_t st) {
       hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, false, false, true>), gf, bt, 0, st, b);
     return hipGetLastError();
   }
+  // TAB: the previous generation's merge tail (split merge) in tl_nblk workgroups past the walkers'
+  b.nwalk_blocks = (int32_t)gt.x;
+  const dim3 gts((unsigned)(gt.x + (b.split ? b.tl_nblk : 0) + (b.est_in_walk ? 1 : 0)));
   if (a.m.prior_kind == MCG_PRIOR_DIAG_GAUSS) {
-    if (b.rt_ix) hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, false, true>), gt, bt, 0, st, b);
+    if (b.rt_ix) hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, false, true>), gts, bt, 0, st, b);
     else hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, false, false, true>), dim3((unsigned)grid), dim3(block), 0, st, a);
     return hipGetLastError();
   }
-  if (b.rt_ix && kSym && b.sym_box) hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, kSym>), gt, bt, 0, st, b);
-  else if (b.rt_ix) hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, false>), gt, bt, 0, st, b);
+  if (b.rt_ix && kSym && b.sym_box) hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, kSym>), gts, bt, 0, st, b);
+  else if (b.rt_ix) hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, true, false>), gts, bt, 0, st, b);
   else hipLaunchKernelGGL((nest_walk_kernel<D, LIK, P, false, false>), dim3((unsigned)grid), dim3(block), 0, st, a);
   return hipGetLastError();
 }
@@ -1109,6 +1211,10 @@ hipError_t launch_key_sample(const double* ll, const long long* tie, int64_t n, 
 // k <= 4096: the generation's unsorted new keys merged into the survivors in one launch (plus the
 // estimate and the slot writes): keys -> o*
 hipError_t launch_merge_fused(const NestArgs& a, double* oll, long long* otie, int* oslot, hipStream_t s);
+// split merge (k <= 4096): the head (merged keys [0, k), estimate, L_max, the new points' slot
+// writes) and a stand-alone tail (the last generation's positions >= k, when no walk ran it)
+hipError_t launch_merge_head(const NestArgs& a, double* oll, long long* otie, int* oslot, hipStream_t s);
+hipError_t launch_merge_tail(const NestArgs& a, hipStream_t s);
 // k <= 4096: new keys sorted into o* by counting ranks (a.rank zeroed by the retire kernel)
 hipError_t launch_sort_new_small(const NestArgs& a, double* oll, long long* otie, int* oslot,
                                  hipStream_t st);

@@ -444,6 +444,65 @@ hipError_t launch_merge_fused(const NestArgs& a, double* oll, long long* otie, i
   return hipGetLastError();
 }
 
+// Split merge, head (mcg_nested_merge.h): workgroups [0, nb) are the merge's first survivor
+// blocks (512 survivors each, positions < k), workgroup nb folds L_max and the generation count
+// (the estimate was folded during the walk, nest_est_role), workgroups past it put the new points into the slots they replace (the
+// next walk reads them).  The tail (positions >= k) runs in the next walk's launch
+// (nest_tail_block) or, after the last generation, in merge_tail_kernel.
+__global__ void __launch_bounds__(kHeadT) merge_head_kernel(const NestArgs a, double* oll, long long* otie,
+                                                            int* oslot, int nb) {
+  NT_STAMP(3, 0);
+  if (nest_stopped(a.st)) return;                         // grid-uniform: set by an earlier launch
+  __shared__ union HeadU {
+    MergeLds<kHeadT, kSmallSort> m;
+    EstLds<kHeadT> e;
+  } lds;
+  const int b = (int)blockIdx.x;
+  if (b < nb) {
+    NestArgs h = a;
+    h.fuse_retire = 0;
+    merge_fused_block<kHeadT, kSmallSort, false, MergeNoWait, kMergeHead>(h, oll, otie, oslot, b, lds.m);
+  } else if (b == nb) {
+    // (the estimate was folded during the walk: nest_est_role)
+    head_lmax(a, head_lmax_load(a), lds.e.sv);
+    NT_STAMP(1, 4);
+  } else {
+    const int64_t D = a.row_bytes / 8, kD = a.k * D;
+    const int64_t stride = (int64_t)(gridDim.x - nb - 1) * kHeadT;
+    for (int64_t g = (int64_t)(b - nb - 1) * kHeadT + threadIdx.x; g < kD; g += stride) {
+      const int64_t j = g / D;
+      const int64_t d = g - j * D;
+      const int sj = a.newk_slot[j];
+      a.x[(int64_t)sj * D + d] = a.nx[g];
+      if (d == 0) {
+        a.ll[sj] = a.nll[j];
+        a.lp[sj] = a.nlp[j];
+      }
+    }
+  }
+}
+
+hipError_t launch_merge_head(const NestArgs& a, double* oll, long long* otie, int* oslot, hipStream_t s) {
+  if (a.k > kSmallSort || a.k < 1 || !a.est_in_rank || a.tv_len > kEstPer * kHeadT) return hipErrorInvalidValue;
+  const int64_t ns = a.n - a.k;
+  const int nb = (int)std::min<int64_t>((a.k + kHeadT - 1) / kHeadT, (ns + kHeadT - 1) / kHeadT);
+  const int64_t kD = a.k * (a.row_bytes / 8);
+  const unsigned nsw = (unsigned)std::max<int64_t>(1, std::min<int64_t>((kD + kHeadT - 1) / kHeadT, 256));
+  hipLaunchKernelGGL(merge_head_kernel, dim3(nb + 1 + nsw), dim3(kHeadT), 0, s, a, oll, otie, oslot, nb);
+  return hipGetLastError();
+}
+
+// the tail of the last generation's merge when no walk ran it (the run ended at max_dead)
+__global__ void __launch_bounds__(256) merge_tail_kernel(const NestArgs a) {
+  nest_tail_block(a, (int)blockIdx.x);
+}
+
+hipError_t launch_merge_tail(const NestArgs& a, hipStream_t s) {
+  if (a.tl_nblk <= 0) return hipSuccess;
+  hipLaunchKernelGGL(merge_tail_kernel, dim3((unsigned)a.tl_nblk), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
 __global__ void __launch_bounds__(256) key_sample_kernel(const double* ll, const long long* tie,
                                                          int64_t n, double* sll, long long* stie,
                                                          NestDevState* st) {
@@ -490,7 +549,7 @@ __global__ void __launch_bounds__(kRetireBlock) retire_kernel(const NestArgs a, 
     if (d == 0) {
       const double lls = a.ll[s];
       put_dead(a, m, lls, a.lp[s]);
-      const double lv = a.st->log_vol + a.prefix[j];
+      const double lv = a.st->log_vol[gen_par(a)] + a.prefix[j];
       st1(a.tv + j, lls + (lv + a.qadd[j]));        // nested.ml:138-141 (log_dv incl. :140)
       a.ll[s] = a.nll[j];
       a.lp[s] = a.nlp[j];

@@ -74,8 +74,13 @@ __device__ __forceinline__ void estimate_body(const NestArgs& a, EstLds<B>& L) {
     // the same tree (v[i] += v[i + s], s = p2/2 .. 1) with its levels where the data are:
     // s >= B pairs elements of one thread (i and i + s are both t mod B), in its registers;
     // 512 .. 64 in LDS after one barrier; 32 .. 1 by shuffles inside wave 0
+    // (rows q B .. q B + B - 1 past k skip their exps: a uniform branch; the k = 4096 estimate of
+    // a 1024-thread workgroup evaluated 16 exps a thread for 4 it needed)
 #pragma unroll
-    for (int q = 0; q < kEstPer; ++q) e[q] = ((int64_t)q * B + t < k) ? pexp(e[q] - M) : 0.0;
+    for (int q = 0; q < kEstPer; ++q) {
+      if ((int64_t)q * B < k) e[q] = ((int64_t)q * B + t < k) ? pexp(e[q] - M) : 0.0;
+      else e[q] = 0.0;
+    }
     int64_t s = p2 >> 1;
     for (; s >= B; s >>= 1) {
       const int d = (int)(s / B);
@@ -108,8 +113,9 @@ __device__ __forceinline__ void estimate_body(const NestArgs& a, EstLds<B>& L) {
   NT_STAMP(1, 7);
   if (t == 0) {
     const double G = k == 1 ? v_first : (M == -__builtin_inf() ? M : M + plog(x, s_lt));
-    a.st->est = plse(a.st->est, G, s_lt);
-    a.st->log_vol = a.st->log_vol + a.prefix[k];
+    const int g0 = gen_par(a), g1 = g0 ^ 1;
+    a.st->est[g1] = plse(a.st->est[g0], G, s_lt);
+    a.st->log_vol[g1] = a.st->log_vol[g0] + a.prefix[k];
   }
 }
 
@@ -139,6 +145,7 @@ struct MergeLds {
   double s_subl[KCAP];                                    // subset: new ll and walker index j,
   short s_sub[KCAP];                                      // in gather order
   short s_srt[KCAP];                                      // subset positions in key order
+  int s_subslot[KCAP];                                    // subset slots (loaded with the ll)
   int s_scan[2 * (BS / 64)];
 };
 
@@ -151,9 +158,15 @@ struct MergeNoWait {
   __device__ bool operator()() const { return true; }
 };
 
-template <int BS, int KCAP, bool SC1, class Wait = MergeNoWait>
+// PART (split merge): kMergeAll stores every position; kMergeHead only
+// positions < k (the head kernel, whose other workgroups fold the estimate, L_max and the
+// generation count and write the new points' slots); kMergeTail only positions >= k (the
+// deferred tail).  Head and tail run with a.fuse_retire = 0: no slot writes here.
+constexpr int kMergeAll = 0, kMergeHead = 1, kMergeTail = 2;
+template <int BS, int KCAP, bool SC1, class Wait = MergeNoWait, int PART = kMergeAll>
 __device__ __forceinline__ void merge_fused_block(const NestArgs& a, double* oll, long long* otie, int* oslot,
                                                   const int b, MergeLds<BS, KCAP>& L, const Wait& wait = Wait()) {
+  [[maybe_unused]] constexpr int kMergeKid = PART == kMergeTail ? 2 : 3;   // trace stamps: tail apart
   const int64_t n = a.n, k = a.k, ns = n - k;
   const int nblk = (int)((ns + BS - 1) / BS);
   const int t = threadIdx.x;
@@ -206,10 +219,12 @@ __device__ __forceinline__ void merge_fused_block(const NestArgs& a, double* oll
   }
   constexpr int kPer = KCAP / BS;
   double nv[kPer];
-#pragma unroll
+  int nsl[kPer];                                          // their slots: no global load after
+#pragma unroll                                            // the subset is known
   for (int r = 0; r < kPer; ++r) {
     const int64_t j = (int64_t)r * BS + t;
     nv[r] = ldv(a.newk_ll + (j < k ? j : k - 1));
+    nsl[r] = ldv(a.newk_slot + (j < k ? j : k - 1));
   }
   if (g0 < kD) {
     wt_store(&a.x[(int64_t)sj0 * D + d0], cx0);
@@ -249,7 +264,7 @@ __device__ __forceinline__ void merge_fused_block(const NestArgs& a, double* oll
     wsub += __popcll(__ballot(in));
     wbelow += __popcll(__ballot(ok & !ge_lo));
   }
-  NT_STAMP(3, 1);
+  NT_STAMP(kMergeKid, 1);
   if (t < nsb) {
     s_sv_l[t] = kl;
     s_sv_t[t] = kt;
@@ -277,11 +292,12 @@ __device__ __forceinline__ void merge_fused_block(const NestArgs& a, double* oll
     if (in) {
       s_sub[o + below_lane] = (short)(r * BS + t);
       s_subl[o + below_lane] = nv[r];
+      L.s_subslot[o + below_lane] = nsl[r];
     }
     o += __popcll(bm);
   }
   __syncthreads();
-  NT_STAMP(3, 2);
+  NT_STAMP(kMergeKid, 2);
   // rank the subset among itself (counting), place it sorted, write the subset keys out
   for (int e = t; e < m; e += BS) {
     const int j = s_sub[e];
@@ -299,20 +315,21 @@ __device__ __forceinline__ void merge_fused_block(const NestArgs& a, double* oll
       else hi = md;
     }
     const int64_t pos = i0 + lo + c_lo + lr;
+    if ((PART == kMergeTail && pos < k) || (PART == kMergeHead && pos >= k)) continue;
     wt_store(&oll[pos], x);
     wt_store(&otie[pos], xt);
-    wt_store(&oslot[pos], ldv(a.newk_slot + j));
+    wt_store(&oslot[pos], L.s_subslot[e]);
     if (pos % kKeySample == kKeySample - 1) {
       a.out_samp_ll[pos / kKeySample] = x;
       a.out_samp_tie[pos / kKeySample] = xt;
     }
-    if (pos == n - 1) {
+    if (PART == kMergeAll && pos == n - 1) {
       a.st->max_ll = x;
       __hip_atomic_fetch_add(&a.st->gen_done, 1LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   __syncthreads();
-  NT_STAMP(3, 3);
+  NT_STAMP(kMergeKid, 3);
   if (t < nsb) {                                          // survivors: i + c_lo + #subset below
     int lo = 0, hi = m;
     while (lo < hi) {
@@ -322,6 +339,7 @@ __device__ __forceinline__ void merge_fused_block(const NestArgs& a, double* oll
       else hi = md;
     }
     const int64_t pos = i0 + t + c_lo + lo;
+    if ((PART != kMergeTail || pos >= k) && (PART != kMergeHead || pos < k)) {
     wt_store(&oll[pos], kl);
     wt_store(&otie[pos], kt);
     wt_store(&oslot[pos], ks);
@@ -329,10 +347,51 @@ __device__ __forceinline__ void merge_fused_block(const NestArgs& a, double* oll
       a.out_samp_ll[pos / kKeySample] = kl;
       a.out_samp_tie[pos / kKeySample] = kt;
     }
-    if (pos == n - 1) {
+    }
+    if (PART == kMergeAll && pos == n - 1) {
       a.st->max_ll = kl;
       __hip_atomic_fetch_add(&a.st->gen_done, 1LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  NT_STAMP(3, 4);
+  NT_STAMP(kMergeKid, 4);
+}
+
+// ---- split merge (round 6): the head of a generation's merge on the critical path, its tail
+// deferred into the next walk's launch ----
+//
+// The next walk needs only the k lowest keys of the merged order (its threshold key[k-1], the
+// slots key_slot[0..k) that its walkers retire and replace) and the stop test's inputs; walkers
+// start at random live slots, not at sorted ranks.  Survivor block b of the merge writes
+// positions >= B b, so blocks b < ceil(k / B) hold every position < k: the head kernel runs just
+// those blocks (merge_fused_block<..., kMergeHead>), and the tail (kMergeTail, positions >= k,
+// every block) runs in the workgroups of the next walk kernel behind its walkers.
+constexpr int kHeadT = 512;                                // the head kernel's workgroup size
+constexpr int kHeadR = kSmallSort / kHeadT;                // new keys per thread (L_max)
+
+// the generation's L_max (the merged keys' last ll: the larger of the survivors' and the new keys'
+// largest ll) and its count, after the estimate (same workgroup, k <= 4096)
+__device__ __forceinline__ double head_lmax_load(const NestArgs& a) {   // issued before the estimate
+  double mx = -__builtin_inf();
+#pragma unroll
+  for (int r = 0; r < kHeadR; ++r) {
+    const int64_t j = r * kHeadT + threadIdx.x;
+    if (j < a.k) mx = fmax(mx, a.newk_ll[j]);
+  }
+  return mx;
+}
+__device__ __forceinline__ void head_lmax(const NestArgs& a, double mx, double* s_red) {
+  constexpr int T = kHeadT;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+  __syncthreads();
+  if ((t & 63) == 0) s_red[t >> 6] = mx;
+  __syncthreads();
+  if (t == 0) {
+    double M = a.st->max_ll;
+#pragma unroll
+    for (int w = 0; w < T / 64; ++w) M = fmax(M, s_red[w]);
+    a.st->max_ll = M;
+    a.st->gen_done = a.st->gen_done + 1;
+  }
 }

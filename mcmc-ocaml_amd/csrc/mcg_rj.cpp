@@ -1,5 +1,5 @@
 // mcg_rj.cpp -- host side of the reversible-jump sampler (Mcmc.make_rjmcmc_sampler /
-// rjmcmc_array / rjmcmc_model_counts, mcmc.ml:84-153): packs the two model descriptors into
+// rjmcmc_array / rjmcmc_model_counts, mcmc.ml:83-153): packs the two model descriptors into
 // the padded device layout of mcg_rj_kernel.h, builds the models' kD trees, starts the chains.
 // mcg_run drives the steps (mcg_runtime.cpp dispatches to the RJ kernel when rj_active).
 #include <algorithm>
@@ -64,7 +64,7 @@ int mcg_set_rjmcmc(mcg_ctx* ctx, const mcg_rj_model* a, const mcg_rj_model* b) {
   const mcg_rj_model* m[2] = {a, b};
   if (!(std::fabs(a->model_prior + b->model_prior - 1.0) < std::sqrt(2.220446049250313e-16)) ||
       !(a->model_prior > 0.0) || !(b->model_prior > 0.0))
-    return set_error(ctx, MCG_EINVAL, "RJ: model priors pa + pb must be 1 (mcmc.ml:91)");
+    return set_error(ctx, MCG_EINVAL, "RJ: model priors pa + pb must be 1 (mcmc.ml:90)");
   const int DM = std::max(a->ndim, b->ndim);
   if (a->ndim < 1 || b->ndim < 1) return set_error(ctx, MCG_EINVAL, "RJ: ndim >= 1");
   if (!find_rj_kernel(DM)) return set_error(ctx, MCG_EINVAL, "RJ: no compiled kernel for max ndim %d", DM);
@@ -80,8 +80,6 @@ int mcg_set_rjmcmc(mcg_ctx* ctx, const mcg_rj_model* a, const mcg_rj_model* b) {
     if (q->lik_kind != MCG_LIK_FLAT && q->lik_kind != MCG_LIK_DIAG_GAUSS && q->lik_kind != MCG_LIK_GAUSS_SHELL &&
         q->lik_kind != MCG_LIK_FULLCOV_GAUSS)
       return set_error(ctx, MCG_EINVAL, "RJ: likelihood kind %d not supported", q->lik_kind);
-    if (q->prior_kind == MCG_PRIOR_DIAG_GAUSS)
-      return set_error(ctx, MCG_EINVAL, "RJ: FLAT, BOX or OPEN_BOX priors only");
     std::vector<double> lik, pri, jmp, into;
     if ((rc = pack_likelihood(ctx, q->lik_kind, D, q->lik_params, q->n_lik, lik, nullptr, nullptr))) return rc;
     if ((rc = pack_prior(ctx, q->prior_kind, D, q->prior_params, q->n_prior, pri))) return rc;
@@ -117,7 +115,9 @@ int mcg_set_rjmcmc(mcg_ctx* ctx, const mcg_rj_model* a, const mcg_rj_model* b) {
     };
     const std::vector<double> plik = pad_lik(q->lik_kind, D, DM, lik);
     // (dev grows below: re-take the header pointer afterwards)
-    const double o_lik = put(plik), o_pri = put(pad_prior(D, DM, pri, -HUGE_VAL, HUGE_VAL)), o_j = put(jmp), o_i = put(into);
+    const std::vector<double> ppri = q->prior_kind == MCG_PRIOR_DIAG_GAUSS ? pad_gauss_prior(D, DM, pri)
+                                                                         : pad_prior(D, DM, pri, -HUGE_VAL, HUGE_VAL);
+    const double o_lik = put(plik), o_pri = put(ppri), o_j = put(jmp), o_i = put(into);
     double* hh = &dev[16 * (size_t)k];
     hh[7] = o_lik; hh[8] = o_pri; hh[9] = o_j; hh[10] = o_i;
   }

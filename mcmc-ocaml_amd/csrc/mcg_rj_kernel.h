@@ -1,5 +1,5 @@
 // mcg_rj_kernel.h -- batched reversible-jump MH between two models (Mcmc.make_rjmcmc_sampler,
-// mcmc.ml:89-116, driven by rjmcmc_array's schedule mcmc.ml:118-132).
+// mcmc.ml:89-119, driven by rjmcmc_array's schedule mcmc.ml:121-139).
 //
 // One lane per chain.  The chain carries a model tag (0 = A, 1 = B) and a point padded with zeros
 // to DM = max(D_A, D_B); every model block on the device is padded to DM the same way
@@ -9,7 +9,8 @@
 // Device descriptor (double[]): per model m a 16-double header at 16 m
 //   [0] D_m  [1] log p_m  [2] p_m  [3] lik kind  [4] prior kind  [5] jump kind  [6] into kind
 //   [7] lik block offset  [8] prior block offset  [9] jump block offset  [10] into block offset
-// blocks: likelihood in the MH kernel's layout at DM; prior [lo, hi, lp_in, lo, hi] at DM;
+// blocks: likelihood in the MH kernel's layout at DM; prior [lo, hi, lp_in, lo, hi] at DM (a
+// DIAG_GAUSS prior: [mu/s, 1/s, C, mu, s] at DM, zero-padded);
 // jumps: GAUSS s[DM]; WRAP lo, hi, dx [DM]; INDEP_GAUSS mu[DM], s[DM], 1/s[DM], mu/s[DM], C.
 #pragma once
 #include "mcg_mh_kernel.h"
@@ -28,9 +29,12 @@ __device__ __forceinline__ double rj_lik(const double* y, const MhArgs& a, int k
   }
 }
 
+// lpa / lpb (mcmc.ml:116-118): FLAT, a box, or Stats.log_multi_gaussian mu sigma (DIAG_GAUSS:
+// the DIAG_GAUSS likelihood's canonical constants padded to DM with zeros, so the pad dims add +0)
 template <int DM>
-__device__ __forceinline__ double rj_prior(const double* y, int kind, const double* q) {
+__device__ __forceinline__ double rj_prior(const double* y, const MhArgs& a, int kind, const double* q) {
   if (kind == MCG_PRIOR_FLAT) return 0.0;
+  if (kind == MCG_PRIOR_DIAG_GAUSS) return eval_lik<DM, 1, MCG_LIK_DIAG_GAUSS>(y, 0, a, q);
   int inb = 1;
 #pragma unroll
   for (int d = 0; d < DM; ++d) inb &= (int)(y[d] >= q[d]) & (int)(y[d] <= q[DM + d]);
@@ -161,7 +165,7 @@ __global__ void __launch_bounds__(256) rj_kernel(const MhArgs a) {
   for (int64_t t = 0; t < a.nsteps; ++t) {
     const uint64_t T = a.step_base + (uint64_t)t;
     const uint32_t tlo = (uint32_t)T, thi = (uint32_t)(T >> 32);
-    // ---- jump_proposal (mcmc.ml:93-103): internal with prob p_tag, else into the other model ----
+    // ---- jump_proposal (mcmc.ml:92-102): internal with prob p_tag, else into the other model ----
     const u32x4 ws = rng(gid, tlo, CALL_RJ, TAG_MH, thi);
     const double* hm = H + 16 * tag;
     const bool internal = u53(ws.x, ws.y) < hm[2];
@@ -171,7 +175,7 @@ __global__ void __launch_bounds__(256) rj_kernel(const MhArgs a) {
     const int jk = internal ? (int)hy[5] : (int)hy[6];
     const double* jq = H + (int64_t)(internal ? hy[9] : hy[10]);
     const int leaf = rj_draw<DM>(x, y, Dy, jk, jq, a.rj_kd[ytag], rng, gid, tlo, thi, s_lt, s_nt);
-    // ---- log_jump_prob (mcmc.ml:104-112) ----
+    // ---- log_jump_prob (mcmc.ml:103-112) ----
     double lf, lb;
     if (internal) {
       lf = hy[1] + rj_ljp_to<DM>(y, Dy, jk, jq, a.rj_kd[ytag], leaf);
@@ -182,9 +186,9 @@ __global__ void __launch_bounds__(256) rj_kernel(const MhArgs a) {
       lf = hy[1] + rj_ljp_to<DM>(y, Dy, jk, jq, a.rj_kd[ytag], leaf);
       lb = hm[1] + rj_ljp_to<DM>(x, (int)hm[0], bk, bq, a.rj_kd[tag], -1);
     }
-    // ---- log_like / log_prior of the proposed model (mcmc.ml:113-116) ----
+    // ---- log_like / log_prior of the proposed model (mcmc.ml:113-118) ----
     const double lly = rj_lik<DM>(y, a, (int)hy[3], H + (int64_t)hy[7]);
-    const double lpy = hy[1] + rj_prior<DM>(y, (int)hy[4], H + (int64_t)hy[8]);
+    const double lpy = hy[1] + rj_prior<DM>(y, a, (int)hy[4], H + (int64_t)hy[8]);
     const double ratio = (((lly + lpy) - (ll + lp)) + lb) - lf;
     const u32x4 wa = rng(gid, tlo, CALL_ACCEPT, TAG_MH, thi);
     const bool acc = plog(u53(wa.x, wa.y), s_lt) < ratio;
@@ -218,7 +222,7 @@ __global__ void __launch_bounds__(256) rj_kernel(const MhArgs a) {
   if (a.flags & RUNF_ACCUMULATE) a.rj_nb[c] += nb_rec;
 }
 
-// rjmcmc_array's start (mcmc.ml:120-124): the fair coin per chain when no tags are given, the
+// rjmcmc_array's start (mcmc.ml:123-128): the fair coin per chain when no tags are given, the
 // start point of the chain's model (xa [D_A][N] or xb [D_B][N]), then ll, lp (with log p_model)
 template <int DM>
 __global__ void __launch_bounds__(256) rj_init_kernel(const MhArgs a, int draw_tags, const double* xa,
@@ -243,7 +247,7 @@ __global__ void __launch_bounds__(256) rj_init_kernel(const MhArgs a, int draw_t
     a.x[(int64_t)d * a.N + c] = x[d];
   }
   a.ll[c] = rj_lik<DM>(x, a, (int)h[3], a.rj + (int64_t)h[7]);
-  a.lp[c] = rj_prior<DM>(x, (int)h[4], a.rj + (int64_t)h[8]) + h[1];
+  a.lp[c] = rj_prior<DM>(x, a, (int)h[4], a.rj + (int64_t)h[8]) + h[1];
 }
 
 template <int DM>

@@ -212,6 +212,21 @@ static int pack_mixture(mcg_ctx* ctx, const double* params, size_t n, std::vecto
     }
     q[4] = C;
   }
+  // The pick (mcmc.ml:168-173) walks u down the normalised weights, u - p_1 - p_2 ...; when the
+  // rounded weights leave u past the last one the reference raises Failure (:173).  Every step of
+  // the walk is monotone in u, so that can happen for some draw iff it happens for the largest
+  // draw u53 can make, 1 - 2^-53: such weights are refused here, with the reference's message,
+  // instead of failing (or, in a kernel, silently picking a component) at some later step.
+  double u = 1.0 - 0x1p-53;
+  bool picked = false;
+  for (int c = 0; c < nc && !picked; ++c) {
+    const double pc = dev[1 + c * stride];
+    if (u < pc) picked = true;
+    else u = u - pc;
+  }
+  if (!picked)
+    return mcg::set_error(ctx, MCG_EFAIL, "combine_jump_proposals: internal error: no jump proposal to select "
+                          "(mcmc.ml:173): the normalised weights sum below the largest uniform draw");
   return MCG_OK;
 }
 
@@ -1029,6 +1044,7 @@ int mcg_get_counters(mcg_ctx* ctx, uint64_t* naccept, uint64_t* nreject) {
 
 int mcg_reset_counters(mcg_ctx* ctx) {
   if (!ctx) return MCG_EINVAL;
+  ++ctx->state_token;                 // the counters changed: a sampler's cached count is stale
   ctx->nsteps_total = 0;
   ctx->acc_base = ctx->rej_base = 0;
   if (ctx->N < 1) return MCG_OK;

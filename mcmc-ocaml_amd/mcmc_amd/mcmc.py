@@ -74,22 +74,22 @@ def make_mcmc_sampler(log_likelihood, log_prior, jump_proposal, ctx=None):
 
 @dataclass
 class RjSamples:
-    """('a, 'b) rjmcmc_sample array (mcmc.ml:86-87) for N chains, structure-of-arrays: value is
+    """('a, 'b) rjmcmc_sample array (mcmc.ml:87) for N chains, structure-of-arrays: value is
     padded to max(ndim_A, ndim_B) (dims beyond the sample's model are 0)."""
     model: np.ndarray            # (n, N) uint8: 0 = A, 1 = B
     value: np.ndarray            # (n, Dmax, N)
     log_likelihood: np.ndarray   # (n, N)
-    log_prior: np.ndarray        # (n, N) includes log p_model (mcmc.ml:115-116)
+    log_prior: np.ndarray        # (n, N) includes log p_model (mcmc.ml:116-118)
     counts: tuple = (0, 0)       # rjmcmc_model_counts over every recorded sample
 
 
 def rjmcmc_array(n, model_a, model_b, start, nchains=1, nbin=0, nskip=1, ctx=None, models=None,
                  record_x=True):
     """Mcmc.rjmcmc_array ?nbin ?nskip n lls lps jps ljps jintos ljpintos (pa, pb) (a, b)
-    (mcmc.ml:118-132) for `nchains` chains.  model_a / model_b are targets.RjModel descriptors
+    (mcmc.ml:121-139) for `nchains` chains.  model_a / model_b are targets.RjModel descriptors
     (likelihood, prior, internal jump, jump into the model, model prior); start = (a, b) start
     points (a (D_A,) / (D_A, N) array, likewise b).  Each chain starts in A or B by a fair coin
-    (mcmc.ml:120) unless models (N,) gives the start models."""
+    (mcmc.ml:123) unless models (N,) gives the start models."""
     import ctypes as C
     from . import _lib as L
     ctx = ctx or default_context()
@@ -111,7 +111,7 @@ def rjmcmc_array(n, model_a, model_b, start, nchains=1, nbin=0, nskip=1, ctx=Non
 
 
 def rjmcmc_model_counts(ctx_or_samples):
-    """Mcmc.rjmcmc_model_counts (mcmc.ml:134-142): (#A, #B) over the recorded samples."""
+    """Mcmc.rjmcmc_model_counts (mcmc.ml:141-149): (#A, #B) over the recorded samples."""
     if isinstance(ctx_or_samples, RjSamples):
         nb = int(ctx_or_samples.model.sum())
         return ctx_or_samples.model.size - nb, nb
@@ -122,7 +122,7 @@ def rjmcmc_model_counts(ctx_or_samples):
 
 
 def rjmcmc_evidence_ratio(samples):
-    """Mcmc.rjmcmc_evidence_ratio (mcmc.ml:144-146): #A / #B."""
+    """Mcmc.rjmcmc_evidence_ratio (mcmc.ml:151-153): #A / #B."""
     na, nb = samples.counts if isinstance(samples, RjSamples) else rjmcmc_model_counts(samples)
     return float(na) / float(nb)
 

@@ -187,7 +187,7 @@ def combine_jump_proposals(components, ndim):
     return Mixture(components, ndim)
 
 
-# ---- reversible-jump descriptors (Mcmc.make_rjmcmc_sampler, mcmc.ml:89-116) ----
+# ---- reversible-jump descriptors (Mcmc.make_rjmcmc_sampler, mcmc.ml:89-119) ----
 class RjJump:
     """A jump of one RJ model: kind MCG_RJ_JUMP_* with its parameters (include/mcg.h)."""
 

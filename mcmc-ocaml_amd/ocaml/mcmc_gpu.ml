@@ -194,16 +194,27 @@ let set_model ctx lik pri prop =
 
 type state = mat * vec * vec
 
+let get_counters ctx =
+  let a = allocate uint64_t Unsigned.UInt64.zero and r = allocate uint64_t Unsigned.UInt64.zero in
+  check ctx (c_get_counters ctx a r);
+  (Unsigned.UInt64.to_int !@a, Unsigned.UInt64.to_int !@r)
+
 (* Mcmc.make_mcmc_sampler (mcmc.ml:37-56) over a batch of chains: one MH step per call.  The
    chains stay on the device between calls: the step runs from the device copy (mcg_run +
    mcg_get_state, no mcg_init upload) only when all of these hold -- the argument is the state
    this sampler returned last (physically), its contents still equal the sampler's private
    snapshot of it (a caller may mutate the returned Bigarrays in place), and the context's state
    token (mcg_state_token) is the one seen right after that step (no other sampler, mcmc_array,
-   nested run or model change used the context in between).  Otherwise the state is uploaded. *)
-let make_mcmc_sampler ctx lik pri prop =
+   nested run, model change or reset_counters used the context in between).  Otherwise the state
+   is uploaded, and when the token moved the sampler first sets its own model again, so it never
+   steps under another sampler's target.  [count]: also the number of accepted chains of the
+   step, from the context's accept total -- read once per step (after it), the total before it
+   being the one this sampler read after its own last step while the token is unchanged. *)
+let make_core ~count ctx lik pri prop =
   set_model ctx lik pri (Some prop);
   let last = ref None in
+  let tok_mine = ref (c_state_token ctx) in     (* the token right after this sampler's last use *)
+  let acc_mine = ref None in                    (* the accept total read then *)
   let copy2 (a : mat) = let b = Bigarray.Array2.create Bigarray.float64 Bigarray.c_layout
                                 (Bigarray.Array2.dim1 a) (Bigarray.Array2.dim2 a) in
     Bigarray.Array2.blit a b; b in
@@ -212,15 +223,19 @@ let make_mcmc_sampler ctx lik pri prop =
     Bigarray.Array1.blit a b; b in
   fun ((x : mat), (ll : vec), (lp : vec)) ->
     let d = Bigarray.Array2.dim1 x and nch = Bigarray.Array2.dim2 x in
-    let resident = match !last with
-      | Some ((x0, ll0, lp0), (sx, sll, slp), tok) ->
+    let ours = Unsigned.UInt64.equal !tok_mine (c_state_token ctx) in
+    if not ours then set_model ctx lik pri (Some prop);
+    let resident = ours && match !last with
+      | Some ((x0, ll0, lp0), (sx, sll, slp), _) ->
         x == x0 && ll == ll0 && lp == lp0
-        && Unsigned.UInt64.equal tok (c_state_token ctx)
         && x = sx && ll = sll && lp = slp
       | None -> false in
     if not resident then
       check ctx (c_init ctx (Int64.of_int nch) (bigarray_start array2 x) (bigarray_start array1 ll)
                    (bigarray_start array1 lp));
+    let acc0 = if not count then 0 else match !acc_mine with
+      | Some a when ours -> a
+      | _ -> fst (get_counters ctx) in
     let o = make run_opts in
     setf o r_nbin 1L; setf o r_nskip 1L; setf o r_nrec 0L;
     setf o r_rx 0l; setf o r_rllp 0l; setf o r_racc 0l; setf o r_accum 0l; setf o r_append 0l;
@@ -229,17 +244,21 @@ let make_mcmc_sampler ctx lik pri prop =
     let x' = Array2.create float64 c_layout d nch in
     let ll' = Array1.create float64 c_layout nch and lp' = Array1.create float64 c_layout nch in
     check ctx (c_get_state ctx (bigarray_start array2 x') (bigarray_start array1 ll') (bigarray_start array1 lp'));
+    let acc1 = if count then fst (get_counters ctx) else 0 in
+    acc_mine := Some acc1;
     last := Some ((x', ll', lp'), (copy2 x', copy1 ll', copy1 lp'), c_state_token ctx);
-    (x', ll', lp')
+    tok_mine := c_state_token ctx;
+    ((x', ll', lp'), acc1 - acc0)
+
+let make_mcmc_sampler ctx lik pri prop =
+  let step = make_core ~count:false ctx lik pri prop in
+  fun st -> fst (step st)
+
+let make_mcmc_step ctx lik pri prop = make_core ~count:true ctx lik pri prop
 
 let reset_counters ctx = check ctx (c_reset_counters ctx)
 
 let reseed ctx seed = check ctx (c_reseed ctx (Unsigned.UInt64.of_int64 seed))
-
-let get_counters ctx =
-  let a = allocate uint64_t Unsigned.UInt64.zero and r = allocate uint64_t Unsigned.UInt64.zero in
-  check ctx (c_get_counters ctx a r);
-  (Unsigned.UInt64.to_int !@a, Unsigned.UInt64.to_int !@r)
 
 let bptr (b : (float, Bigarray.float64_elt, Bigarray.c_layout) Bigarray.Genarray.t) =
   bigarray_start genarray b
@@ -306,7 +325,7 @@ let posterior_samples ctx n (_, _, (pts : float array array), (log_wts : float a
   check ctx (c_posterior ctx (carr log_wts) (Int64.of_int npts) (Int64.of_int n) (CArray.start idx));
   Array.init n (fun i -> pts.(Int64.to_int (CArray.get idx i)))
 
-(* ---- reversible jump (Mcmc.rjmcmc_array, mcmc.ml:118-132) ---- *)
+(* ---- reversible jump (Mcmc.rjmcmc_array, mcmc.ml:121-139) ---- *)
 type rj_jump =
   | Rj_gauss of float array
   | Rj_wrap of float array * float array * float array
@@ -404,7 +423,7 @@ let rjmcmc_array ?(nbin = 0) ?(nskip = 1) ctx n (ma : rj_model) (mb : rj_model) 
   check ctx (c_rj_get_models ctx (from_voidp uint8_t null) (bigarray_start array2 models));
   (models, xs, ll, lp)
 
-(* Mcmc.rjmcmc_model_counts / rjmcmc_evidence_ratio (mcmc.ml:134-146) over the last run *)
+(* Mcmc.rjmcmc_model_counts / rjmcmc_evidence_ratio (mcmc.ml:141-153) over the last run *)
 let rjmcmc_model_counts ctx =
   let a = allocate uint64_t Unsigned.UInt64.zero and b = allocate uint64_t Unsigned.UInt64.zero in
   check ctx (c_rj_counts ctx a b);

@@ -74,6 +74,10 @@ type state = mat * vec * vec
     Bigarrays mutated in place -- is uploaded first. *)
 val make_mcmc_sampler : ctx -> likelihood -> prior -> proposal -> (state -> state)
 
+(** [make_mcmc_sampler] whose step also returns how many chains accepted (from the context's
+    accept total: one mcg_get_counters round trip per step while the sampler owns the context). *)
+val make_mcmc_step : ctx -> likelihood -> prior -> proposal -> (state -> state * int)
+
 (** Mcmc.reset_counters / get_counters (mcmc.mli:29-30) for this context. *)
 val reset_counters : ctx -> unit
 
@@ -128,7 +132,7 @@ type rj_model = {
   rj_tree : (float array array * float array * float array) option; rj_model_prior : float }
 
 (** [rjmcmc_array ctx n a b start_a start_b]: start_a is D_A x N, start_b D_B x N (the (a, b)
-    pair per chain); each chain starts by a fair coin (mcmc.ml:120).  Returns the record model
+    pair per chain); each chain starts by a fair coin (mcmc.ml:123).  Returns the record model
     tags (n x N), values (n x Dmax x N, zero-padded), log-likelihoods and log-priors. *)
 val rjmcmc_array :
   ?nbin:int -> ?nskip:int -> ctx -> int -> rj_model -> rj_model -> mat -> mat ->

@@ -27,7 +27,7 @@ let get_counters () = Mcmc_gpu.get_counters (Lazy.force default_ctx)
    token and its own snapshot too) instead of uploading the record again. *)
 let make_mcmc_sampler ?ctx lik pri prop =
   let ctx = match ctx with Some c -> c | None -> Lazy.force default_ctx in
-  let step = Mcmc_gpu.make_mcmc_sampler ctx lik pri prop in
+  let step = Mcmc_gpu.make_mcmc_step ctx lik pri prop in
   let last = ref None in
   fun (s : float array Mcmc.mcmc_sample) ->
     let state = match !last with
@@ -38,10 +38,10 @@ let make_mcmc_sampler ?ctx lik pri prop =
         Array.iteri (fun i v -> x.{i, 0} <- v) s.Mcmc.value;
         (x, Array1.of_array float64 c_layout [| s.Mcmc.like_prior.Mcmc.log_likelihood |],
          Array1.of_array float64 c_layout [| s.Mcmc.like_prior.Mcmc.log_prior |]) in
-    let (acc0, _) = Mcmc_gpu.get_counters ctx in
-    let (x', ll', lp') as st' = step state in
-    let (acc1, _) = Mcmc_gpu.get_counters ctx in
-    let r = if acc1 = acc0 then s else sample (column x' 0) ll'.{0} lp'.{0} in
+    let ((x', ll', lp') as st', nacc) = step state in
+    (* a rejected step returns the same record (mcmc.ml:53-56): decided by the step's accept
+       count (one counter read per step, Mcmc_gpu.make_mcmc_step), not by comparing values *)
+    let r = if nacc = 0 then s else sample (column x' 0) ll'.{0} lp'.{0} in
     last := Some (r, Array.copy r.Mcmc.value, st');
     r
 
@@ -60,7 +60,8 @@ let mcmc_array ?ctx ?(nbin = 0) ?(nskip = 1) ?(chains = 1) n lik pri prop (start
       sample (Array.init d (fun i -> Genarray.get xs [| r; i; c |])) ll.{r, c} lp.{r, c})
 
 (* Nested.nested_evidence ?observer ?epsrel ?nmcmc ?nlive ?mode_hopping_frac (nested.mli:50-61)
-   with the likelihood descriptor and a box prior (draw_prior = uniform in the box) *)
+   with the likelihood descriptor and a box prior (draw_prior = uniform in the box) or a
+   Gauss_prior (draw_prior = Stats.draw_gaussian per dim, log_prior = Stats.log_multi_gaussian) *)
 let nested_evidence ?ctx ?observer ?epsrel ?nmcmc ?nlive ?mode_hopping_frac ?k lik pri :
     float array Nested.nested_output =
   let ctx = match ctx with Some c -> c | None -> Lazy.force default_ctx in

@@ -291,11 +291,24 @@ struct mix_comp {
 
 static void prep_free(prep_t* p) {
   free(p->mu); free(p->isig); free(p->ctr); free(p->s); free(p->gm); free(p->gp);
-  for (int c = 0; c < p->nmix; ++c) { free(p->mix[c].inv_s); free(p->mix[c].width); }
+  if (p->mix)
+    for (int c = 0; c < p->nmix; ++c) { free(p->mix[c].inv_s); free(p->mix[c].width); }
   free(p->mix);
 }
 
+static int prep_model_(const or_model* m, prep_t* p);
+
+/* the model's constants; on invalid parameters everything allocated so far is freed */
 static int prep_model(const or_model* m, prep_t* p) {
+  const int rc = prep_model_(m, p);
+  if (rc != 0) {
+    prep_free(p);
+    memset(p, 0, sizeof(*p));
+  }
+  return rc;
+}
+
+static int prep_model_(const or_model* m, prep_t* p) {
   memset(p, 0, sizeof(*p));
   int D = m->ndim;
   p->D = D; p->lik = m->lik_kind; p->prior = m->prior_kind; p->prop = m->prop_kind;
@@ -760,7 +773,8 @@ static int mh_step(const prep_t* p, uint64_t seed, uint32_t gid, uint64_t T, cha
     }
     case MCG_PROP_MIXTURE: {
       /* propose: Random.float 1.0 walked down the normalised weights (mcmc.ml:168-173); the
-         reference raises Failure past the last weight -- here the last component is taken */
+         reference raises Failure past the last weight (:173) -- the product refuses such weights at
+         configuration (pack_mixture); the walk here keeps the last component */
       uint32_t w[4];
       rng4(seed, gid, lo, CALL_MIX, TAG_MH, hi, w);
       double u = or_u53(w[0], w[1]);
@@ -1009,8 +1023,8 @@ int or_mh_run(const or_model* m, uint64_t seed, uint32_t chain_offset, int64_t N
 }
 
 /* ======================================================================================
- * Reversible jump between two models (Mcmc.make_rjmcmc_sampler, mcmc.ml:89-116; rjmcmc_array's
- * schedule mcmc.ml:118-132), RNG injected: selector call CALL_RJ, start coin CALL_RJ_START
+ * Reversible jump between two models (Mcmc.make_rjmcmc_sampler, mcmc.ml:89-119; rjmcmc_array's
+ * schedule mcmc.ml:121-139), RNG injected: selector call CALL_RJ, start coin CALL_RJ_START
  * ====================================================================================== */
 #define CALL_RJ 0xFFFF0006u
 #define CALL_RJ_START 0xFFFF0007u
@@ -1095,7 +1109,7 @@ static void* rj_worker(void* arg) {
   for (int64_t i = j->i0; i < j->i1; ++i) {
     uint32_t gid = (uint32_t)i;
     int tag = j->tag[i];
-    if (j->draw_tags) {              /* rjmcmc_array: is_a = Random.float 1.0 < 0.5 (mcmc.ml:120) */
+    if (j->draw_tags) {              /* rjmcmc_array: is_a = Random.float 1.0 < 0.5 (mcmc.ml:123) */
       uint32_t w[4];
       rng4(j->seed, gid, 0u, CALL_RJ_START, TAG_MH, 0u, w);
       tag = or_u53(w[0], w[1]) < 0.5 ? 0 : 1;
@@ -1103,7 +1117,7 @@ static void* rj_worker(void* arg) {
     int D0 = R->m[tag]->ndim;
     const double* src = tag ? j->xb : j->xa;
     for (int d = 0; d < DM; ++d) x[d] = d < D0 ? src[(int64_t)d * N + i] : 0.0;
-    /* start record: log_like and lpa a + log pa (mcmc.ml:121-124) */
+    /* start record: log_like and lpa a + log pa (mcmc.ml:126-128) */
     double ll = lik_eval(&R->p[tag], x), lp = prior_eval(&R->p[tag], x) + R->logp[tag];
     uint64_t na = 0, nb = 0;
 #define RJ_RECORD(r) do { \
@@ -1117,7 +1131,7 @@ static void* rj_worker(void* arg) {
       uint32_t w[4];
       rng4(j->seed, gid, lo, CALL_RJ, TAG_MH, hi, w);
       const or_rj_model* mc = R->m[tag];
-      int internal = or_u53(w[0], w[1]) < mc->model_prior;          /* mcmc.ml:95,100 */
+      int internal = or_u53(w[0], w[1]) < mc->model_prior;          /* mcmc.ml:94,99 */
       int ytag = internal ? tag : 1 - tag;
       const or_rj_model* my = R->m[ytag];
       int kind = internal ? my->jump_kind : my->into_kind;

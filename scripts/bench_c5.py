@@ -117,6 +117,8 @@ def main():
     backend = os.environ.get("MCG_BENCH_BACKEND", "nccl")
     if os.environ.get("MCG_BENCH_DEVICE"):
         local = int(os.environ["MCG_BENCH_DEVICE"])
+    elif backend == "nccl" and world > torch.cuda.device_count():
+        raise SystemExit("bench_c5: %d ranks over RCCL but only %d visible GPU(s)" % (world, torch.cuda.device_count()))
     dist = world > 1
     if dist:
         import torch.distributed as tdist
@@ -160,7 +162,19 @@ def main():
     mean, sd, log_z_hm = reduce_stats(D, ctx.tile_stats(), device=comm)
     barrier()
     elapsed = time.perf_counter() - t0
+    elapsed_own = elapsed
     acc, rej = ctx.counters()
+    timing = ctx.kernel_timing("mh")
+    props = torch.cuda.get_device_properties(dev)
+    me = {"rank": rank, "local_rank": local, "device": torch.cuda.current_device(),
+          "pci_bus_id": getattr(props, "pci_bus_id", None), "uuid": str(getattr(props, "uuid", "")),
+          "elapsed_s": elapsed_own, "avg_launch_ms": timing["total_ms"] / max(timing["launches"], 1),
+          "launches": timing["launches"]}
+    if dist:
+        ranks = [None] * world
+        tdist.all_gather_object(ranks, me)
+    else:
+        ranks = [me]
     if dist:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=comm)
         tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
@@ -168,7 +182,6 @@ def main():
         cc = torch.tensor([acc, rej], dtype=torch.float64, device=comm)
         tdist.all_reduce(cc)
         acc, rej = (int(v) for v in cc.cpu().numpy())
-    timing = ctx.kernel_timing("mh")
     per_launch = timing["total_ms"] / max(timing["launches"], 1)
     # a bench step of S sweeps may run as several launches (the runtime caps a launch at
     # min(4096, 2^26 / N) sweeps): the framing uses the kernel time of all the timed launches
@@ -180,6 +193,11 @@ def main():
     ach_tfs = step_chain_steps * flops_per_step / (kernel_ms_per_step * 1e-3) / 1e12
     total_chains = N * world
     if rank == 0:
+        from bench import rank_check
+        rk = rank_check(ranks, world, backend, dist, tdist if dist else None)
+        if dist and backend == "nccl" and not (rk["one_gpu_per_rank"] and rk["world_matches"]):
+            raise SystemExit("bench_c5: %d ranks over RCCL drove %d distinct GPU(s): %s"
+                             % (world, rk["distinct_gpus"], json.dumps(rk["per_rank"])))
         cpu = None if args.no_cpu_baseline else cpu_baseline(mu, cov, s, args.cpu_seconds)
         sdt = np.sqrt(np.diag(cov))
         line = {
@@ -209,6 +227,7 @@ def main():
                                          "unit": "TFLOP/s", "frac": ach_tfs / FP64_MATRIX_PEAK_TFS,
                                          "flops_per_step": flops_per_step}},
             "cpu_baseline": cpu,
+            "ranks": rk,
             "accept_frac": acc / max(acc + rej, 1),
             "log_z_harmonic_mean": log_z_hm,
             "posterior_check": {"max_abs_mean_err_over_sd": float(np.max(np.abs(mean - mu) / sdt)),

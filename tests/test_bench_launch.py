@@ -74,10 +74,13 @@ def test_c5_runner_cpu_baseline_is_the_fullcov_oracle():
 
 
 @pytest.mark.gpu
-def test_bench_two_gloo_ranks_on_one_gpu():
-    """The real bench over two ranks sharing cuda:0 (gloo collectives): one JSON line, n_gpus 2,
-    value = both ranks' steps over the max-over-ranks time, cpu_baseline present on rank 0."""
-    cmd = [sys.executable, BENCH, "--gpus", "2", "--steps", "2", "--warmup", "1", "--sweeps", "50",
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_gloo_ranks_on_one_gpu(n):
+    """The real bench over n ranks sharing cuda:0 (gloo collectives): one JSON line, n_gpus n,
+    value = every rank's steps over the max-over-ranks time, cpu_baseline present on rank 0; the
+    self-check block lists every rank (its device, elapsed and launch times) with the spread and
+    the process group's own size; the nested replicas of all n ranks are merged."""
+    cmd = [sys.executable, BENCH, "--gpus", str(n), "--steps", "2", "--warmup", "1", "--sweeps", "50",
            "--chains", "4096", "--nested-nlive", "2048", "--nested-k", "64", "--nested-nmcmc", "20",
            "--nested-seeds", "1", "--cpu-seconds", "0.1"]
     p = subprocess.run(cmd, env=_env(MCG_BENCH_BACKEND="gloo", MCG_BENCH_DEVICE="0"),
@@ -86,7 +89,28 @@ def test_bench_two_gloo_ranks_on_one_gpu():
     lines = _json_lines(p.stdout)
     assert len(lines) == 1, p.stdout
     line = lines[0]
-    assert line["n_gpus"] == 2
-    assert line["value"] == pytest.approx(2 * 4096 * 50 * 2 / (line["ms_per_step"] * 2 * 1e-3), rel=1e-9)
+    assert line["n_gpus"] == n
+    assert line["value"] == pytest.approx(n * 4096 * 50 * 2 / (line["ms_per_step"] * 2 * 1e-3), rel=1e-9)
     assert line["cpu_baseline"] is not None and line["cpu_baseline"]["value"] > 0
-    assert line["log_evidence"]["seed_sweep"]["runs"] == 2
+    assert line["log_evidence"]["seed_sweep"]["runs"] == n
+    assert line["log_evidence"]["nested_run"]["nlive"] == 2048 * n
+    rk = line["ranks"]
+    assert rk["rccl_world"] == n and rk["backend"] == "gloo" and rk["world_matches"]
+    assert [r["rank"] for r in rk["per_rank"]] == list(range(n))
+    assert all(r["device"] == 0 and r["launches"] == 2 and r["avg_launch_ms"] > 0 for r in rk["per_rank"])
+    assert rk["distinct_gpus"] == 1 and not rk["one_gpu_per_rank"]       # shared card: gloo only
+    assert rk["elapsed_s_max"] == pytest.approx(line["ms_per_step"] * 2 * 1e-3, rel=1e-9)
+    assert rk["elapsed_s_min"] <= rk["elapsed_s_max"]
+
+
+@pytest.mark.gpu
+def test_bench_rccl_refuses_more_ranks_than_gpus():
+    """Under RCCL (the driver's backend) a bench of more ranks than visible GPUs fails loudly
+    before any GPU work instead of stacking ranks on one card."""
+    import torch
+    n = torch.cuda.device_count() + 1
+    cmd = [sys.executable, BENCH, "--gpus", str(n), "--steps", "1", "--warmup", "1", "--sweeps", "10",
+           "--chains", "1024", "--nested-nlive", "0", "--no-cpu-baseline"]
+    p = subprocess.run(cmd, env=_env(), capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert p.returncode != 0
+    assert "visible GPU" in p.stderr, p.stderr[-2000:]

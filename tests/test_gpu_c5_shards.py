@@ -37,9 +37,17 @@ def test_c5_sharded_runner_is_rank_count_invariant(tmp_path):
     port = 29500 + random.randint(4001, 6000)
     one = _run(1, tmp_path, port)
     two = _run(2, tmp_path, port + 1, self_launch=True)
+    four = _run(4, tmp_path, port + 2, self_launch=True)
     assert one["config"]["chains_total"] == two["config"]["chains_total"] == 16384
     assert two["n_gpus"] == 2 and two["scaling"] == "strong"
-    assert one["moments_digest"] == two["moments_digest"]
+    assert one["moments_digest"] == two["moments_digest"] == four["moments_digest"]
+    # the self-check block: the group's size, every rank's device and times, their spread
+    rk = four["ranks"]
+    assert four["n_gpus"] == 4 and rk["rccl_world"] == 4 and rk["world_matches"]
+    assert [r["rank"] for r in rk["per_rank"]] == [0, 1, 2, 3]
+    assert all(r["launches"] >= 2 and r["avg_launch_ms"] > 0 for r in rk["per_rank"])
+    assert rk["elapsed_s_max"] == pytest.approx(four["ms_per_step"] * 2 * 1e-3, rel=1e-9)
+    assert one["ranks"]["rccl_world"] == 1 and one["ranks"]["backend"] == "none"
     assert one["log_z_harmonic_mean"] == two["log_z_harmonic_mean"]
     assert one["accept_frac"] == two["accept_frac"]
     assert 0.05 < one["accept_frac"] < 0.6

@@ -59,7 +59,10 @@ def assert_same(g, o):
     np.testing.assert_array_equal(g["rec_lp"], o["rec_lp"])
     np.testing.assert_array_equal(g["x"], o["x"])
     np.testing.assert_array_equal(g["ll"], o["ll"])
+    np.testing.assert_array_equal(g["lp"], o["lp"])
     assert g["nacc"] == int(o["nacc"].sum())
+    # every step of every chain is counted once, accepted or rejected (mcmc.ml:27-35)
+    assert g["nrej"] == o["x"].shape[1] * o["nsteps"] - int(o["nacc"].sum())
     if g["tiles"] is not None:
         np.testing.assert_array_equal(g["tiles"], o["tiles"])
 

@@ -374,6 +374,35 @@ def test_nested_walk_merge_one_launch_targets_bit_exact(oracle, T, monkeypatch, 
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nlive,k,D,max_gen", [(1000, 1, 3, 40), (300, 16, 3, 0), (2000, 64, 16, 9),
+                                               (70000, 4096, 4, 0), (70000, 4096, 16, 3)])
+def test_nested_split_merge_bit_exact(oracle, T, monkeypatch, capfd, nlive, k, D, max_gen):
+    """The split merge (MCG_NESTED_SPLIT=1, round 6: the head kernel writes keys [0, k), the next
+    walk's launch the rest and folds the estimate) against the default one-launch merge of every
+    key and the oracle, run to the stop test (the stopping walk runs the last tail) and cut at
+    max_dead (the host's flush kernel runs it), with MCG_NESTED_CHECK's device sortedness test of
+    every generation's keys."""
+    lik = T.gauss_shell(np.zeros(D), 1.0, 0.2)
+    pri = T.box(-2 * np.ones(D), 2 * np.ones(D))
+    kw = dict(nlive=nlive, nmcmc=6, mode_hopping_frac=0.1, k=k)
+    if max_gen:
+        kw["max_dead"] = k * max_gen
+    monkeypatch.setenv("MCG_NESTED_CHECK", "1")
+    monkeypatch.setenv("MCG_NESTED_SPLIT", "1")
+    g = gpu_nested(lik, pri, 29, **kw)
+    err = capfd.readouterr().err
+    assert "merged 0; final keys vs live ll mismatches 0, unsorted keys 0" in err, err[-2000:]
+    monkeypatch.setenv("MCG_NESTED_SPLIT", "0")
+    g0 = gpu_nested(lik, pri, 29, **kw)
+    o = oracle_nested(oracle, lik, pri, 29, nlive=nlive, nmcmc=6, mode_hop=0.1, k=k,
+                      **({"max_iter": k * max_gen} if max_gen else {}))
+    assert g.converged == (max_gen == 0)
+    assert_nested_same(g, o)
+    assert_nested_same(g0, o)
+    assert np.all(np.diff(g.ll[g.n_dead:]) >= 0)       # the final live set in key order
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("nlive,k", [(300, 200), (257, 256)])
 def test_nested_large_fraction_generations_bit_exact(oracle, T, nlive, k):
     """Generations retiring most of the live set (k > nlive / 2) and all but one point

@@ -4,7 +4,8 @@ final states and counters; the reference's statistical tests on the GPU path."""
 import numpy as np
 import pytest
 
-from test_rjmcmc import LIK_DIAG, LIK_FLAT, LIK_SHELL, PRIOR_BOX, PRIOR_FLAT, gaussians_models, top_hat_models
+from test_rjmcmc import (LIK_DIAG, LIK_FLAT, LIK_SHELL, PRIOR_BOX, PRIOR_FLAT, PRIOR_GAUSS, gauss_prior_models,
+                         gaussians_models, top_hat_models)
 
 pytestmark = pytest.mark.gpu
 
@@ -24,6 +25,8 @@ def to_desc(T, m, kd_pts=None):
         if kind == PRIOR_FLAT:
             return T.flat_prior()
         D = m["ndim"]
+        if kind == PRIOR_GAUSS:
+            return T.gauss_prior(p[:D], p[D:2 * D])
         return T.box(p[:D], p[D:2 * D], p[2 * D])
 
     kd = T.rj_kd(kd_pts, np.zeros(m["ndim"]), np.ones(m["ndim"])) if kd_pts is not None else None
@@ -104,3 +107,16 @@ def test_rj_top_hats_evidence_ratio_on_gpu(oracle):
                           ctx=ctx, record_x=False)
     ctx.close()
     assert abs(mcmc.rjmcmc_evidence_ratio(s) - 4.0) < 0.1
+
+
+def test_rj_gaussian_priors_bit_exact(oracle):
+    """DIAG_GAUSS priors per model (lpa / lpb, mcmc.ml:116-118), models of different dimension
+    (the smaller one's prior padded with zero constants): records, tags, state and counters equal
+    the oracle's bit for bit, and the model count ratio is the analytic pa Z_A / (pb Z_B)."""
+    a, b, ratio = gauss_prior_models()
+    N = 512
+    s, st, o = run_both(oracle, a, b, np.full((1, N), 0.1), np.full((2, N), 0.1), 21, 20, 3, 200)
+    assert_rj_same(s, st, o)
+    np.testing.assert_array_equal(st[2], o["lp"])
+    na, nb = s.counts
+    assert abs(na / nb / ratio - 1.0) < 0.08, (na / nb, ratio)

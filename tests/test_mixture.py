@@ -93,3 +93,59 @@ def test_mixture_argument_errors(gpu_lib):
     from mcmc_amd import targets as T
     with pytest.raises(ValueError):
         T.combine_jump_proposals([(1.0, T.Proposal(L.PROP_DE, [0.0]))], 2)
+
+
+def _walk_falls_through(w, u):
+    """the pick of mcmc.ml:168-173 in IEEE double: True when u passes every weight"""
+    for p in w:
+        if u < p:
+            return False
+        u = u - p
+    return True
+
+
+def _normalised(p):
+    tot = 0.0
+    for x in p:
+        tot = tot + x
+    return [x / tot for x in p]
+
+
+# weights whose rounded normalised walk lets the largest draw through (found by search)
+FALL_THROUGH_WEIGHTS = [float.fromhex(h) for h in ("0x1.7fad7432340e0p+8", "0x1.0569a03eef9cap-10",
+                                                    "0x1.ea6aec618a7e9p+9")]
+
+
+def test_mixture_pick_fall_through_is_decided_by_the_largest_draw():
+    """The reference raises Failure when u passes every normalised weight (mcmc.ml:173).  The
+    walk is monotone in u, so that happens for some draw iff it happens for the largest u53 draw,
+    1 - 2^-53 -- the check mcg_set_proposal makes (pack_mixture).  Random weight vectors: no
+    smaller draw falls through when the largest does not; the crafted vector falls through for the
+    largest draw only near the top of (0, 1)."""
+    rng = np.random.default_rng(3)
+    umax = 1.0 - 2.0 ** -53
+    for _ in range(3000):
+        w = _normalised(list(rng.random(rng.integers(2, 9)) * rng.choice([1.0, 1e-3, 1e3], 1)))
+        if not _walk_falls_through(w, umax):
+            us = np.concatenate([rng.random(64), umax - rng.integers(1, 64, 16) * 2.0 ** -53])
+            assert not any(_walk_falls_through(w, float(u)) for u in us)
+    w = _normalised(FALL_THROUGH_WEIGHTS)
+    assert _walk_falls_through(w, umax)
+    assert not _walk_falls_through(w, 0.5)
+
+
+@pytest.mark.gpu
+def test_mixture_refuses_fall_through_weights():
+    """mcg_set_proposal refuses weights the reference's pick can fall through, with MCG_EFAIL
+    (Failure) and the reference's message; the same components with ordinary weights run."""
+    from mcmc_amd import Context, targets as T
+    from mcmc_amd._lib import Failure
+    lik = T.diag_gauss([0.0], [1.0])
+    pri = T.flat_prior()
+    comps = lambda ws: [(w, T.gauss([0.5])) for w in ws]
+    with Context(seed=1) as ctx:
+        with pytest.raises(Failure, match="no jump proposal to select"):
+            ctx.set_model(lik, pri, T.combine_jump_proposals(comps(FALL_THROUGH_WEIGHTS), 1))
+        ctx.set_model(lik, pri, T.combine_jump_proposals(comps([1.0, 2.0, 3.0]), 1))
+        ctx.init(np.zeros((1, 64)))
+        ctx.run(nbin=10, nskip=1, n_rec=1)

@@ -11,6 +11,7 @@ import pytest
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 HDR = (ROOT / "include" / "mcg.h").read_text()
 ML = (ROOT / "mcmc-ocaml_amd" / "ocaml" / "mcmc_gpu.ml").read_text()
+MLI = (ROOT / "mcmc-ocaml_amd" / "ocaml" / "mcmc_gpu.mli").read_text()
 
 
 def _strip_comments(s):
@@ -160,7 +161,7 @@ def test_mcmc_array_run_options_match_the_python_mirror():
     assert o["racc"].strip() == "0l" and o["append"].strip() == "0l"
     src = inspect.getsource(mcmc.mcmc_array)
     assert "record_x=True" in src and "record_llp=True" in src
-    s = _ml_run_opts("make_mcmc_sampler")
+    s = _ml_run_opts("make_core")
     assert s["nbin"].strip() == "1L" and s["nrec"].strip() == "0L" and s["accum"].strip() == "0l"
 
 
@@ -182,12 +183,17 @@ def test_sampler_residency_is_tied_to_the_context_token():
     its last result (physically), still equal to its private snapshot, and the context's state
     token is unchanged since its own step; the compat layer decides accept / reject by the step's
     accept count, not by comparing values."""
-    body = ML[ML.index("let make_mcmc_sampler"):ML.index("let reset_counters")]
-    assert "c_state_token ctx" in body and "Unsigned.UInt64.equal tok" in body
+    body = ML[ML.index("let make_core"):ML.index("let reset_counters")]
+    assert "c_state_token ctx" in body and "Unsigned.UInt64.equal !tok_mine" in body
     assert "x = sx && ll = sll && lp = slp" in body
+    # ADVICE r5: a moved token re-applies the sampler's own model before stepping
+    assert "if not ours then set_model ctx lik pri (Some prop)" in body
     assert re.search(r'fn "mcg_state_token" \(ptr void @-> returning uint64_t\)', ML)
     assert "uint64_t mcg_state_token(const mcg_ctx* ctx);" in HDR
     compat = (ROOT / "mcmc-ocaml_amd" / "ocaml" / "mcmc_gpu_compat.ml").read_text()
     c = compat[compat.index("let make_mcmc_sampler"):compat.index("let mcmc_array")]
-    assert "Mcmc_gpu.get_counters ctx" in c and "if acc1 = acc0 then s" in c
+    # ADVICE r5: one counter read per step (make_mcmc_step), not two
+    assert "Mcmc_gpu.make_mcmc_step ctx" in c and "if nacc = 0 then s" in c
+    assert "Mcmc_gpu.get_counters" not in c
+    assert "val make_mcmc_step" in MLI
     assert "s.Mcmc.value = v0" in c

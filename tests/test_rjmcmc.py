@@ -3,7 +3,7 @@ reference's own statistical tests (test/mcmc_test.ml:114-182) restated on the or
 import numpy as np
 
 LIK_FLAT, LIK_DIAG, LIK_SHELL = 0, 1, 3
-PRIOR_FLAT, PRIOR_BOX = 0, 1
+PRIOR_FLAT, PRIOR_BOX, PRIOR_GAUSS = 0, 1, 3
 RJ_GAUSS, RJ_WRAP, RJ_INDEP, RJ_KD = 1, 2, 3, 4
 
 
@@ -73,3 +73,35 @@ def test_rjmcmc_records_follow_schedule_and_padding(oracle):
     assert np.all(r["rec_x"][:, 2, :][inA] == 0.0)
     np.testing.assert_allclose(r["rec_lp"][inA], np.log(0.3))
     np.testing.assert_allclose(r["rec_lp"][~inA], np.log(0.7))
+
+
+def gauss_prior_models():
+    """Two models with Gaussian priors lpa / lpb (Stats.log_multi_gaussian, mcmc.ml:116-118): a
+    Gaussian likelihood N(mu, s) under a N(0, tau) prior per dim, so Z = prod_d N(mu_d; 0,
+    sqrt(s_d^2 + tau_d^2)); internal and transition jumps are independence draws from the exact
+    posterior N(m, v) (precision 1/s^2 + 1/tau^2)."""
+    def m(mu, s, tau, p):
+        mu, s, tau = (np.asarray(v, float) for v in (mu, s, tau))
+        prec = 1 / s ** 2 + 1 / tau ** 2
+        post = (RJ_INDEP, list(mu / s ** 2 / prec) + list(1 / np.sqrt(prec)))
+        z = np.prod(np.exp(-mu ** 2 / (2 * (s ** 2 + tau ** 2))) / np.sqrt(2 * np.pi * (s ** 2 + tau ** 2)))
+        return dict(ndim=len(mu), lik=(LIK_DIAG, list(mu) + list(s)), prior=(PRIOR_GAUSS, [0.0] * len(mu) + list(tau)),
+                    jump=post, into=post, p=p), z
+    (a, za), (b, zb) = m([0.3], [0.5], [1.0], 0.4), m([0.2, -0.4], [0.6, 0.8], [1.5, 1.5], 0.6)
+    return a, b, (0.4 * za) / (0.6 * zb)
+
+
+def test_rjmcmc_gaussian_priors_evidence_ratio(oracle):
+    """Gaussian model priors in the reversible-jump sampler: the model count ratio estimates
+    pa Z_A / (pb Z_B) (analytic, ~4.1), within 3 %; a chain in model A has lp = log pa + the
+    prior's log density."""
+    a, b, ratio = gauss_prior_models()
+    N = 1000
+    r = oracle.rj_run(a, b, 17, np.full((2, N), 0.1), np.full((2, N), 0.1), nbin=50, nskip=5, n_rec=600)
+    nb = int(r["rec_tag"].sum())
+    na = r["rec_tag"].size - nb
+    assert abs(na / nb / ratio - 1.0) < 0.03, (na / nb, ratio)
+    inA = r["rec_tag"] == 0
+    x = r["rec_x"][:, 0, :][inA]
+    lp_expect = np.log(0.4) - 0.5 * np.log(2 * np.pi) - 0.5 * x ** 2
+    np.testing.assert_allclose(r["rec_lp"][inA], lp_expect, rtol=1e-12, atol=1e-12)
