@@ -47,8 +47,9 @@ def combos():
         out.append(("DATA", "WRAP", D, 1))
     # the kD interpolated proposal (Interpolate_pdf) at widths 1-8 and 16, unpadded (its tree is
     # built at the caller's ndim); one lane per chain on every likelihood, split over lanes on
-    # the separable ones.  (A one-lane kD kernel at D 64 spills ~3.8 KB a lane and its final
-    # state store came out wrong for one dim in tests/test_gpu_fuzz.py: kD stays at D <= 16.)
+    # the separable ones.  (A one-lane kD kernel at D 64 spills ~3.8 KB a lane, and the compiler
+    # miscompiles it: its final state store reads x[3]'s high dword from a register it never
+    # restored (profiles/r06/kd64_miscompile).  kD stays at D <= 16.)
     for lik in ("FLAT", "DIAG", "SHELL", "GMIX", "FULLCOV"):
         for D in SMALL + [16]:
             out.append((lik, "KD", D, 1))
@@ -70,6 +71,13 @@ def combos():
         out.append(("FULLCOV", "MIX", D, 1))
     for D in (2, 4, 6, 8):
         out.append(("DATA", "MIX", D, 1))
+    # the wrapping-uniform and DE proposals on the lane-split likelihoods at the wide widths, split
+    # so a lane holds at most 16 dims (D 24 / 32 on 2 lanes, 48 / 64 on 4): one lane per chain
+    # spills 0.2-1.7 KB a lane at D 48 / 64 (round 6)
+    for lik in ("FLAT", "DIAG", "SHELL", "GMIX"):
+        for prop in ("WRAP", "DE"):
+            for D, P in ((24, 2), (32, 2), (48, 4), (64, 4)):
+                out.append((lik, prop, D, P))
     # Mcmc.differential_evolution_proposal over a caller-supplied sample array (one lane per chain)
     for lik in ("FLAT", "DIAG", "SHELL", "GMIX"):
         for D in PAD:

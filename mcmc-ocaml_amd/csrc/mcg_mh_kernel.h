@@ -935,15 +935,21 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP, UNI>::kBlock), (MhSh
             if (L::valid(sub, i, k)) y[kW * i + k] = fma(qprop[L::dim(sub, i, k)], z[k], x[kW * i + k]);
         }
       } else if constexpr (PROP == MCG_PROP_WRAP_UNIFORM) {
-        static_assert(P == 1, "WRAP: one lane per chain");
+        // dims 2c and 2c + 1 from Philox call c, the lane's own four-dim blocks (one lane: every
+        // dim; P lanes: blocks sub, sub + P, ... -- the same draws, so any split is bit-identical)
+        static_assert(kW == 4, "WRAP: four-dim lane blocks");
 #pragma unroll
-        for (int d = 0; d < D; d += 2) {
-          const u32x4 w = rng(gid, tlo, (uint32_t)(d >> 1), TAG_MH, thi);
-          y[d] = wrap_uniform(qprop[d], qprop[D + d], qprop[2 * D + d], x[d], u53(w.x, w.y));
-          if (d + 1 < D)
-            y[d + 1] = wrap_uniform(qprop[d + 1], qprop[D + d + 1], qprop[2 * D + d + 1], x[d + 1],
-                                    u53(w.z, w.w));
-        }
+        for (int i = 0; i < L::NCL; ++i)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            if (!L::valid(sub, i, 2 * h)) continue;
+            const int d = L::dim(sub, i, 2 * h), j = 4 * i + 2 * h;
+            const u32x4 w = rng(gid, tlo, (uint32_t)(d >> 1), TAG_MH, thi);
+            y[j] = wrap_uniform(qprop[d], qprop[D + d], qprop[2 * D + d], x[j], u53(w.x, w.y));
+            if (L::valid(sub, i, 2 * h + 1))
+              y[j + 1] = wrap_uniform(qprop[d + 1], qprop[D + d + 1], qprop[2 * D + d + 1], x[j + 1],
+                                      u53(w.z, w.w));
+          }
       } else if constexpr (PROP == MCG_PROP_KD_INTERP) {
         static_assert(P == 1 || D % (kW * P) == 0, "KD: P lanes need D % WP == 0");
         // Interpolate_pdf.draw (interpolate_pdf.ml:114-119) from the leaf and box loaded ahead;
@@ -992,7 +998,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP, UNI>::kBlock), (MhSh
         lb = lq;    // log_jump_prob proposed start = log q(start)
       }
       else if constexpr (PROP == MCG_PROP_DE) {
-        static_assert(P == 1, "DE: one lane per chain");
+        static_assert(kW == 4, "DE: four-dim lane blocks");
         // Mcmc.differential_evolution_proposal (mcmc.ml:198-218) over the caller's samples:
         // pick_samples i != j (:199-203; j drawn from the n - 1 others, no retry loop), the scale
         // 1.0 with probability mode_hopping_frac (no draw consulted when it is 0, :209) else
@@ -1008,8 +1014,15 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP, UNI>::kBlock), (MhSh
         const double dsc = (mh != 0.0 && u53(ws.x, ws.y) < mh) ? 1.0 : qprop[1] * pnormal(ws.z, s_nt);
         const double* __restrict__ si = a.de_pts + (int64_t)ii * D;
         const double* __restrict__ sj = a.de_pts + (int64_t)jd * D;
+        // every lane draws the same indices and scale; lane `sub` moves its own dims
 #pragma unroll
-        for (int d = 0; d < D; ++d) y[d] = x[d] + dsc * (sj[d] - si[d]);
+        for (int i = 0; i < L::NCL; ++i)
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (L::valid(sub, i, k)) {
+              const int d = L::dim(sub, i, k);
+              y[4 * i + k] = x[4 * i + k] + dsc * (sj[d] - si[d]);
+            }
       }
       else if constexpr (PROP == MCG_PROP_MIXTURE) {
         static_assert(P == 1, "MIXTURE: one lane per chain");

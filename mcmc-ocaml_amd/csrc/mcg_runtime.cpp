@@ -829,16 +829,26 @@ int choose_lanes(mcg_ctx* ctx) {
   const bool kd_split = ctx->prop_kind == MCG_PROP_KD_INTERP &&
                         (ctx->lik_kind == MCG_LIK_DIAG_GAUSS || ctx->lik_kind == MCG_LIK_GAUSS_SHELL ||
                          ctx->lik_kind == MCG_LIK_FLAT);
+  // the wrapping-uniform and DE proposals on a lane-split likelihood: wide chains split so a lane
+  // holds at most 16 dims (a one-lane D 48 / 64 kernel spills 0.2-1.7 KB a lane)
+  const bool wide_split = (ctx->prop_kind == MCG_PROP_WRAP_UNIFORM || ctx->prop_kind == MCG_PROP_DE) &&
+                          (ctx->lik_kind == MCG_LIK_DIAG_GAUSS || ctx->lik_kind == MCG_LIK_GAUSS_SHELL ||
+                           ctx->lik_kind == MCG_LIK_FLAT || ctx->lik_kind == MCG_LIK_GAUSS_MIX);
   // (the kD draw also splits two dims per lane when D = 2P: mcg_mh_kernel.h Layout W = 2)
   auto splits = [&](int P) {
     return (D % (4 * P) == 0 || (kd_split && D == 2 * P)) && find_mh_kernel(D, P, ctx->lik_kind, ctx->prop_kind);
   };
   if (want > 0) {
     if (want == 1) return 1;
-    if ((separable || fullcov_mfma || kd_split) && splits(want)) return want;
+    if ((separable || fullcov_mfma || kd_split || wide_split) && splits(want)) return want;
     return 1;
   }
   if (fullcov_mfma) return 4;
+  if (wide_split) {
+    for (int P : {1, 2, 4})
+      if (D <= 16 * P && (P == 1 || splits(P))) return P;
+    return 1;
+  }
   if (!separable && !kd_split) return 1;
   const int64_t lanes_target = (int64_t)std::max(ctx->num_cus, 1) * 4 * 4 * 64;  // 4 waves/SIMD
   int best = 1;

@@ -129,6 +129,37 @@ def test_wide_one_lane_proposals_bit_exact(oracle, T, D, lik_kind, prop_kind):
     assert_same(g, o)
 
 
+@pytest.mark.parametrize("D,lanes_auto", [(16, 1), (32, 2), (48, 4), (64, 4)])
+@pytest.mark.parametrize("lik_kind", ["diag", "mix"])
+@pytest.mark.parametrize("prop_kind", ["wrap", "de"])
+def test_wide_proposals_split_over_lanes_bit_exact(oracle, T, D, lanes_auto, lik_kind, prop_kind):
+    """Round 6: the wrapping-uniform and DE proposals on a separable or mixture likelihood split a
+    wide chain over lanes (at most 16 dims a lane: the one-lane D 48 / 64 kernels spilled 0.2-1.7
+    KB a lane).  The runtime picks the split; one lane forced and the split both equal the oracle
+    bit for bit."""
+    from mcmc_amd import Context
+    rng = np.random.default_rng(D * 13 + len(lik_kind) + len(prop_kind))
+    lik = _likelihood(T, rng, lik_kind, D)
+    pri = _prior(T, rng, "asym_box", D)
+    if prop_kind == "wrap":
+        prop = T.uniform_wrapping(-3 * np.ones(D), 3 * np.ones(D), rng.uniform(0.05, 0.3, D))
+        oprop = prop
+    else:
+        samples = rng.normal(0.0, 0.8, size=(200, D))
+        prop = T.differential_evolution_proposal(samples, 0.2)
+        oprop = T.Proposal(4, np.concatenate([[0.2, 200], samples.ravel()]))
+    x0 = rng.uniform(-1.0, 1.0, size=(D, 300))
+    o = run_oracle(oracle, lik, pri, oprop, x0, 31, 3, 2, 7)
+    for lanes in (0, 1):
+        g = run_gpu(lik, pri, prop, x0, 31, 3, 2, 7, lanes=lanes)
+        assert_same(g, o)
+    with Context(seed=31) as ctx:
+        ctx.set_model(lik, pri, prop)
+        ctx.init(x0)
+        ctx.run(nbin=1, nskip=1, n_rec=1)
+        assert ctx.lanes() == lanes_auto
+
+
 def _nested_case(i):
     rng = np.random.default_rng(2000 + i)
     D = int(rng.choice([1, 2, 3, 4, 6, 8, 9, 12, 16, 20, 32]))
