@@ -60,7 +60,9 @@ enum {
    Any ndim >= 1 works for FLAT, DIAG_GAUSS, GAUSS_SHELL and GAUSS_MIX (FULLCOV_GAUSS: ndim <= 64):
    a dimension without compiled kernels runs on the next compiled width with zero-padded dims
    (zero likelihood terms, zero proposal steps, unbounded box); the padding never crosses this
-   boundary.  The DATA kinds take nd <= 4, the kD proposal the compiled widths only.
+   boundary.  The DATA kinds take nd <= 4.  The kD proposal runs at ndim 1-16 on every kind
+   and 17-32 on FLAT, DIAG_GAUSS and GAUSS_SHELL (the caller's tree; the device leaf boxes get
+   [0, 0] in the pad dims); wider is refused with MCG_EINVAL.
 */
 enum {
   MCG_LIK_FLAT = 0,
@@ -146,7 +148,8 @@ int mcg_set_likelihood(mcg_ctx* ctx, int32_t kind, int32_t ndim, const double* p
 int mcg_set_prior(mcg_ctx* ctx, int32_t kind, const double* params, size_t n);
 int mcg_set_proposal(mcg_ctx* ctx, int32_t kind, const double* params, size_t n);
 /* Interpolate_pdf.make pts low high (interpolate_pdf.ml:111-112): kD tree built on the host
-   with Kd_tree.tree_of_objects semantics (kd_tree.ml:155-175), flattened into HBM. */
+   with Kd_tree.tree_of_objects semantics (kd_tree.ml:155-175), flattened into HBM (at the model's
+   padded width when ndim has no kD kernel of its own: see "Any ndim" above). */
 int mcg_set_kd_proposal(mcg_ctx* ctx, const double* pts /*[M][D] row-major*/, int64_t M,
                         const double* low, const double* high);
 /* Mcmc.differential_evolution_proposal ?mode_hopping_frac to_float from_float samples

@@ -60,6 +60,15 @@ def combos():
                 # two dims per lane (D = 2P, mcg_mh_kernel.h Layout W = 2)
                 if (D % (4 * P) == 0 and P < 8) or D == 2 * P:
                     out.append((lik, "KD", D, P))
+    # kD at the padding widths (round 6: an ndim without a kernel of its own runs zero-padded):
+    # 12 on every kind but full covariance (whose 9-15 pad to 16), 24 / 32 split over lanes on
+    # the separable kinds (at most 16 dims a lane)
+    for lik in ("FLAT", "DIAG", "SHELL", "GMIX"):
+        out.append((lik, "KD", 12, 1))
+    for lik in ("FLAT", "DIAG", "SHELL"):
+        out.append((lik, "KD", 24, 2))
+        out.append((lik, "KD", 32, 2))
+        out.append((lik, "KD", 32, 4))
     # the multimodal target of test/nested_test.ml:41-64 (one lane per chain)
     for D in PAD:
         out.append(("GMIX", "GAUSS", D, 1))

@@ -91,7 +91,7 @@ struct Builder {
 }  // namespace
 
 int kd_build(mcg_ctx* ctx, const double* pts, int64_t M, int D, const double* low,
-             const double* high, KdState* dst) {
+             const double* high, KdState* dst, int Dpad) {
   Builder b{pts, D, M, {}, {}, {}, {}};
   std::vector<int64_t> idx((size_t)M);
   std::iota(idx.begin(), idx.end(), 0);
@@ -129,9 +129,29 @@ int kd_build(mcg_ctx* ctx, const double* pts, int64_t M, int D, const double* lo
   };
   if ((rc = up(k.d_nodes, k.nodes.data(), k.nodes.size() * sizeof(KdNode)))) return rc;
   if ((rc = up(k.d_logq, k.logq.data(), k.logq.size() * 8))) return rc;
-  if ((rc = up(k.d_box, k.box.data(), k.box.size() * 8))) return rc;
+  if (Dpad > D) {
+    // the MH kernel of width Dpad (zero-padded model): leaf boxes and the root
+    // box as [lo, hi] = [0, 0] in the pad dims, so a draw puts 0 there (the pad invariant) and
+    // the descent's root test holds for it; log q stays the D-dim density of the caller's tree.
+    // (A pad dim's draw is never strictly inside its box, so these kernels take the descent for
+    // every proposal: the same leaf, a slower step.)
+    std::vector<double> box((size_t)k.nleaves * 2 * Dpad, 0.0), root(2 * (size_t)Dpad, 0.0);
+    for (int64_t l = 0; l < k.nleaves; ++l)
+      for (int d = 0; d < D; ++d) {
+        box[(size_t)l * 2 * Dpad + d] = k.box[(size_t)l * 2 * D + d];
+        box[(size_t)l * 2 * Dpad + Dpad + d] = k.box[(size_t)l * 2 * D + D + d];
+      }
+    for (int d = 0; d < D; ++d) {
+      root[d] = k.root[d];
+      root[Dpad + d] = k.root[D + d];
+    }
+    if ((rc = up(k.d_box, box.data(), box.size() * 8))) return rc;
+    if ((rc = up(k.d_root, root.data(), root.size() * 8))) return rc;
+  } else {
+    if ((rc = up(k.d_box, k.box.data(), k.box.size() * 8))) return rc;
+    if ((rc = up(k.d_root, k.root.data(), k.root.size() * 8))) return rc;
+  }
   if ((rc = up(k.d_pts, k.pts.data(), k.pts.size() * 8))) return rc;
-  if ((rc = up(k.d_root, k.root.data(), k.root.size() * 8))) return rc;
   if ((rc = up(k.d_pt_leaf, k.pt_leaf.data(), k.pt_leaf.size() * 4))) return rc;
   k.built = true;
   return MCG_OK;

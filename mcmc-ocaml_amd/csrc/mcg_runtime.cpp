@@ -658,9 +658,16 @@ int mcg_set_kd_proposal(mcg_ctx* ctx, const double* pts, int64_t M, const double
   int D = ctx->D;
   if (D < 1) return set_error(ctx, MCG_ESTATE, "set the likelihood (ndim) first");
   if (M < 1) return set_error(ctx, MCG_EINVAL, "Interpolate_pdf.make: no points");
-  if (ctx->Dk != D)
-    return set_error(ctx, MCG_EINVAL, "KD_INTERP: ndim %d has no compiled kD kernel (widths 1-8, 16)", D);
-  int rc = kd_build(ctx, pts, M, D, low, high);
+  // an ndim without a kD kernel of its own runs zero-padded at the model's width Dk (kd_build
+  // pads the device boxes); the kD kernels are compiled at widths 1-8, 12 and 16 on every
+  // likelihood kind, and 24 / 32 on the lane-split ones
+  const int Dk = ctx->Dk;
+  bool have = false;
+  for (int P : {1, 2, 4, 8}) have = have || find_mh_kernel(Dk, P, ctx->lik_kind, MCG_PROP_KD_INTERP) != nullptr;
+  if (!have)
+    return set_error(ctx, MCG_EINVAL, "KD_INTERP: no compiled kD kernel for ndim %d (width %d) likelihood=%d",
+                     D, Dk, ctx->lik_kind);
+  int rc = kd_build(ctx, pts, M, D, low, high, nullptr, Dk);
   if (rc) return rc;
   double z = 0.0;
   return mcg_set_proposal(ctx, MCG_PROP_KD_INTERP, &z, 1);
@@ -844,6 +851,17 @@ int choose_lanes(mcg_ctx* ctx) {
     return 1;
   }
   if (fullcov_mfma) return 4;
+  if (kd_split && D > 16) {
+    // kD at the wide widths (24, 32): split so a lane holds at most 16 dims, more for occupancy
+    int best = 0;
+    const int64_t lanes_target = (int64_t)std::max(ctx->num_cus, 1) * 4 * 4 * 64;
+    for (int P : {1, 2, 4}) {
+      if (D > 16 * P || !splits(P)) continue;
+      if (best && ctx->N * best >= lanes_target) break;
+      best = P;
+    }
+    return best ? best : 1;
+  }
   if (wide_split) {
     for (int P : {1, 2, 4})
       if (D <= 16 * P && (P == 1 || splits(P))) return P;

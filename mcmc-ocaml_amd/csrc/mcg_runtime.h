@@ -195,7 +195,7 @@ void timing_begin(mcg_ctx* ctx, hipEvent_t* a, hipEvent_t* b);
 void timing_end(mcg_ctx* ctx, hipEvent_t a, hipEvent_t b, int kind);
 void timing_harvest(mcg_ctx* ctx);
 int kd_build(mcg_ctx* ctx, const double* pts, int64_t M, int D, const double* low, const double* high,
-             KdState* dst = nullptr);
+             KdState* dst = nullptr, int Dpad = 0);
 int pack_likelihood(mcg_ctx* ctx, int32_t kind, int D, const double* params, size_t n,
                     std::vector<double>& dev, int32_t* is_cauchy, int64_t* data_n);
 int pack_prior(mcg_ctx* ctx, int32_t kind, int D, const double* params, size_t n, std::vector<double>& dev);

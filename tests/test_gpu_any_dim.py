@@ -122,19 +122,62 @@ def test_nested_padded_widths_bit_exact(oracle, T, D, k):
 
 
 def test_unpaddable_combinations_fail_loudly(T):
-    """A kD proposal at a width with no kD kernel, or ndim past the widest kernel, is refused
-    with a message (MCG_EINVAL), not run wrong."""
+    """A kD proposal whose padded width has no kD kernel (round 6: kD pads to 12 / 16 on every
+    kind, 24 / 32 on the lane-split ones), or ndim past the widest kernel, is refused with a
+    message (MCG_EINVAL), not run wrong."""
     from mcmc_amd import Context
     from mcmc_amd._lib import InvalidArgument
     ctx = Context(seed=1)
-    D = 11
-    pts = np.random.default_rng(0).normal(size=(64, D))
-    with pytest.raises(InvalidArgument, match="kD"):
-        ctx.set_model(T.diag_gauss(np.zeros(D), np.ones(D)), T.flat_prior(),
-                      T.KdInterp(pts, -5 * np.ones(D), 5 * np.ones(D)))
+    for D, lik in ((40, T.diag_gauss(np.zeros(40), np.ones(40))),
+                   (20, T.gauss_mix(np.zeros((2, 20)), np.ones((2, 20))))):
+        pts = np.random.default_rng(0).normal(size=(64, D))
+        with pytest.raises(InvalidArgument, match="kD"):
+            ctx.set_model(lik, T.flat_prior(), T.KdInterp(pts, -5 * np.ones(D), 5 * np.ones(D)))
     D = 65
     ctx.set_model(T.diag_gauss(np.zeros(D), np.ones(D)), T.flat_prior(), T.gauss(0.1))
     with pytest.raises(InvalidArgument, match="no compiled"):
         ctx.init(np.zeros((D, 8)))
         ctx.run(nbin=1, n_rec=0)
     ctx.close()
+
+
+@pytest.mark.parametrize("D,lik_kind", [(9, "diag"), (13, "shell"), (20, "diag"), (30, "shell"), (10, "mix"),
+                                        (11, "fullcov")])
+@pytest.mark.parametrize("lanes", [0, 1])
+def test_kd_proposal_padded_widths_bit_exact(oracle, T, D, lik_kind, lanes):
+    """Round 6: the kD interpolated proposal (interpolate_pdf.ml:101-142) at an ndim without a kD
+    kernel of its own runs zero-padded (widths 12, 16, 24, 32): the tree is the caller's D-dim
+    tree, the device leaf boxes get [0, 0] in the pad dims, so the draws of the real dims (dims
+    2c, 2c + 1 from call c), log q and every decision equal the oracle's at the real ndim.  (lanes
+    1 at widths 24 / 32 has no kernel: the split is kept.)"""
+    from mcmc_amd import Context
+    rng = np.random.default_rng(70 + D)
+    if lik_kind == "diag":
+        lik = diag_model(T, D)[0]
+    elif lik_kind == "shell":
+        lik = T.gauss_shell(rng.uniform(-0.3, 0.3, D), 1.5, 0.4)
+    elif lik_kind == "mix":
+        lik = T.gauss_mix(rng.uniform(-1, 1, (2, D)), rng.uniform(0.5, 1.5, (2, D)))
+    else:
+        A = rng.normal(size=(D, D))
+        lik = T.fullcov_gauss(rng.uniform(-1, 1, D), A @ A.T / D + np.eye(D))
+    lo, hi = -3 * np.ones(D), 3 * np.ones(D)
+    pts = np.clip(rng.normal(0.0, 1.0, size=(400, D)), -2.9, 2.9)
+    kdp = T.KdInterp(pts, lo, hi)
+    okd = oracle.KdTree(pts, lo, hi)
+    pri = T.box(-4 * np.ones(D), 4 * np.ones(D))
+    x0 = rng.uniform(-1.5, 1.5, size=(D, 200))
+    g = run_gpu(lik, pri, kdp, x0, 19, nbin=4, nskip=2, n_rec=9, lanes=lanes if D <= 16 else 0)
+    m = oracle.Model(D, lik.kind, lik.params, pri.kind, pri.params, 3, [0.0], okd)
+    ll0 = np.array([m.loglik(x0[:, i]) for i in range(x0.shape[1])])
+    lp0 = np.array([m.logprior(x0[:, i]) for i in range(x0.shape[1])])
+    o = oracle.mh_run(m, 19, x0, ll0, lp0, nbin=4, nskip=2, n_rec=9, nthreads=8)
+    o["ll0"], o["lp0"] = ll0, lp0
+    o["tiles"] = oracle.tile_stats(D, x0.shape[1], 9, o)
+    assert_same(g, o)
+    if D > 16:
+        with Context(seed=19) as ctx:
+            ctx.set_model(lik, pri, kdp)
+            ctx.init(x0)
+            ctx.run(nbin=1, nskip=1, n_rec=1)
+            assert ctx.lanes() >= D // 16
