@@ -280,7 +280,7 @@ def c2(args):
 def c4(args):
     """Interpolate_pdf kD-tree independence proposal, D=8 N(0,1) target, M=32,768 exact draws,
     32,768 chains."""
-    D, N, M, S, K = 8, 32768, 32768, 1000, args.launches // 10
+    D, N, M, S, K = 8, args.c4_chains, 32768, 1000, args.launches // 10
     rng = np.random.default_rng(4)
     pts = rng.normal(size=(M, D))
     lo, hi = -10 * np.ones(D), 10 * np.ones(D)
@@ -369,6 +369,7 @@ def main():
                     help="C4/C5: timed sweeps / 100 (C4: launches of 1,000 sweeps, C5: of 500 -- at or under\n                    the runtime's own launch length min(4096, 2^26/N))")
     ap.add_argument("--reps", type=int, default=5, help="C3: timed nested runs after a warm-up run (median reported)")
     ap.add_argument("--c5-chains", type=int, default=131072)
+    ap.add_argument("--c4-chains", type=int, default=32768, help="C4 chains (BASELINE configs[3]: 32,768)")
     args = ap.parse_args()
     def c3k8(a):
         """C3 with 8,192 retirements a generation (two walker waves per draw-table workgroup)."""
