@@ -15,6 +15,7 @@
 #include "mcg_device.h"
 #include "mcg_math.h"
 #include "mcg.h"
+#include <utility>
 
 namespace mcg {
 
@@ -37,6 +38,22 @@ struct Layout {
     return q < W && (P > 1 || (W * i + q) < D);
   }
 };
+
+// f(integral_constant<int, 0>) .. f(integral_constant<int, N - 1>), in order (compile-time slots)
+template <int N, class F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl<N>(f, std::make_integer_sequence<int, N>{});
+}
+
+// steps of kD draw prefetch on P > 1 lanes (mh_kernel's KDA)
+#ifndef MCG_KD_AHEAD
+#define MCG_KD_AHEAD 4
+#endif
+constexpr int kKdAhead = MCG_KD_AHEAD;
 
 // the width of a chain's lane blocks: two dims per lane where the kD proposal runs on D = 2P lanes
 template <int D, int P, int PROP>
@@ -132,16 +149,23 @@ __device__ __forceinline__ uint64_t compress_ballot(uint64_t m) {
 template <int D>
 __device__ __forceinline__ int kd_find_leaf(const KdNode* __restrict__ nodes,
                                             const double* __restrict__ root, const double* v) {
+  // (branch-free: every root bound load in flight together)
   bool inside = true;
 #pragma unroll
-  for (int d = 0; d < D; ++d) inside = inside && (v[d] >= root[d]) && (v[d] <= root[D + d]);
+  for (int d = 0; d < D; ++d) inside = inside & (v[d] >= root[d]) & (v[d] <= root[D + d]);
   int node = 0;
   for (int guard = 0; guard < 4096; ++guard) {
     KdNode nd = nodes[node];
     if (nd.dim < 0) return -1 - nd.dim;
+    // the split coordinate by a select chain kept opaque: folded back into v[nd.dim], it put v
+    // on the scratch stack, and the scratch stores pending at the caller's join forced vmcnt(0)
+    // (loads and stores pending together) on the MH step's main path
     double c = v[0];
 #pragma unroll
-    for (int d = 1; d < D; ++d) c = (nd.dim == d) ? v[d] : c;
+    for (int d = 1; d < D; ++d) {
+      c = (nd.dim == d) ? v[d] : c;
+      asm volatile("" : "+v"(c));
+    }
     bool left = inside && (c <= nd.split);
     node = left ? node + 1 : nd.right;
   }
@@ -684,10 +708,16 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP, UNI>::kBlock), (MhSh
   // leaf, its box, a uniform point in it), so they are loaded ahead: KDA = 1, the leaf of step
   // t + 2 and the box and log q of step t + 1 while step t computes; KDA = 2 (the step loop
   // unrolled by two, one register slot per step parity), the leaf of step t + 4 and the box of
-  // step t + 2.  The same values as loading them in the step.
+  // step t + 2; P > 1 with at most 4 dims a lane (registers to spare) KDA = 4 (kKdAhead), the
+  // leaf of step t + 8 and the box of step t + 4 -- the loads of 8 steps in flight per lane,
+  // where 4 left 38 % of C4's wave-cycles waiting on them (round 5 PMC).  The same values as
+  // loading them in the step.  (kKdAhead = 8, in groups of 4, measured 6 % slower at C4.)
   // (P > 1: lane `sub` holds the box bounds of its own dims, local slot j at kd_lo[j], kd_hi[j])
   constexpr int KDN = PROP == MCG_PROP_KD_INTERP ? L::NL : 1;
-  constexpr int KDA = PROP == MCG_PROP_KD_INTERP ? 2 : 1;
+  constexpr int KDA = PROP == MCG_PROP_KD_INTERP ? (P > 1 && L::NL * kKdAhead <= 16 ? kKdAhead : P > 1 && L::NL <= 4 ? 4 : 2) : 1;
+  // kd_group's steps per group: half the slots where there are 8 (a group's boxes were issued a
+  // whole group earlier), else all of them
+  constexpr int KDG = KDA >= 8 ? KDA / 2 : KDA;
   int kd_leaf_n[KDA];
   double kd_lo[KDA][KDN], kd_hi[KDA][KDN];
   double kd_lqp[KDA];
@@ -738,26 +768,32 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP, UNI>::kBlock), (MhSh
       }
   };
   if constexpr (PROP == MCG_PROP_KD_INTERP) {
+    // every prologue load (state, constants, accumulators) completes here, before the prefetches
+    // go out: a constant whose load was still pending at the step loop's entry made the wait
+    // counts inside the loop lose track of the prefetches, and the first step of every unrolled
+    // group waited for all of them (vmcnt(0))
+    __builtin_amdgcn_s_waitcnt(0);
     if (a.nsteps > 0) {
-      kd_load_box(kd_pick_leaf(a.step_base), std::integral_constant<int, 0>{});
-      if constexpr (KDA == 2) {
-        kd_load_box(kd_pick_leaf(a.step_base + 1), std::integral_constant<int, 1>{});
-        kd_leaf_n[0] = kd_pick_leaf(a.step_base + 2);
-        kd_leaf_n[1] = kd_pick_leaf(a.step_base + 3);
-      } else {
-        kd_leaf_n[0] = kd_pick_leaf(a.step_base + 1);
-      }
+      // issued in the loop's own order (per slot: box, log q, the leaf KDA steps later), so the
+      // wait counts at the loop entry agree with those of the loop's back edge
+      int leaf0[KDA];
+#pragma unroll
+      for (int s = 0; s < KDA; ++s) leaf0[s] = kd_pick_leaf(a.step_base + s);
+      static_for<KDA>([&](auto s_c) __attribute__((always_inline)) {
+        constexpr int sl = decltype(s_c)::value;
+        kd_load_box(leaf0[sl], s_c);
+        kd_leaf_n[sl] = kd_pick_leaf(a.step_base + KDA + sl);
+      });
     }
   }
   // log u of step t (mcmc.ml:49).  P > 1: staggered accept uniforms -- at the first step of each
   // group of P steps, lane `sub` of the chain draws log u for step t + sub; step t + q reads it
   // from lane q (one DPP broadcast, or a shuffle at P = 8)
-  auto accept_lu = [&](int64_t t, uint64_t T) __attribute__((always_inline)) -> double {
+  auto accept_lu = [&](const int q, uint64_t T) __attribute__((always_inline)) -> double {
     if constexpr (P == 1) {
       const u32x4 wa = rng(gid, (uint32_t)T, CALL_ACCEPT, TAG_MH, (uint32_t)(T >> 32));
       return plog(u53(wa.x, wa.y), s_lt);
     } else {
-      const int q = (int)(t & (P - 1));
       if (q == 0) {
         const uint64_t Tj = T + (uint64_t)sub;
         const u32x4 wa = rng(gid, (uint32_t)Tj, CALL_ACCEPT, TAG_MH, (uint32_t)(Tj >> 32));
@@ -773,10 +809,124 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP, UNI>::kBlock), (MhSh
       }
     }
   };
+  // kKdReg: eval_lik / eval_prior of the lane's dims on the register constants (the same
+  // operations as eval_lik / eval_prior)
+  auto kd_reg_lik = [&](const double* yv) __attribute__((always_inline)) -> double {
+    if constexpr (!kKdReg || LIK == MCG_LIK_FLAT) {
+      return 0.0;
+    } else {
+      double S;
+      if constexpr (kW == 2) {
+        double e[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+          e[k] = LIK == MCG_LIK_DIAG_GAUSS ? fma(yv[k], rc_i[k], -rc_m[k]) : yv[k] - rc_m[k];
+        S = reduce_canon_w2<P>(e[0], e[1], sub);
+      } else {
+        double A[L::NA];
+#pragma unroll
+        for (int j = 0; j < L::NA; ++j) A[j] = 0.0;
+#pragma unroll
+        for (int i = 0; i < L::NCL; ++i)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            if (!L::valid(sub, i, k)) continue;
+            const double e = LIK == MCG_LIK_DIAG_GAUSS ? fma(yv[4 * i + k], rc_i[4 * i + k], -rc_m[4 * i + k])
+                                                       : yv[4 * i + k] - rc_m[4 * i + k];
+            A[i % L::NA] = fma(e, e, A[i % L::NA]);
+          }
+        S = reduce_canon<P>(A);
+      }
+      if constexpr (LIK == MCG_LIK_DIAG_GAUSS) {
+        return rc_c - 0.5 * S;
+      } else {
+        const double rr = psqrt(S);
+        const double qq = (rr - rc_r) * rc_iw;
+        return rc_c - 0.5 * qq * qq;
+      }
+    }
+  };
+  auto kd_reg_gauss_prior = [&](const double* yv) __attribute__((always_inline)) -> double {
+    typedef const __attribute__((address_space(4))) double kconst;
+    kconst* kpri = (kconst*)a.pri;
+    asm volatile("" : "+s"(kpri));
+    return eval_gauss_prior<D, P, kconst*, kW>(yv, sub, a, kpri);
+  };
+  auto kd_reg_box_prior = [&](const double* yv) __attribute__((always_inline)) -> double {
+    int inb = 1;
+#pragma unroll
+    for (int i = 0; i < L::NCL; ++i)
+#pragma unroll
+      for (int k = 0; k < kW; ++k) {
+        if (!L::valid(sub, i, k)) continue;
+        const double v = yv[kW * i + k];
+        if constexpr (kKdReg) inb &= (int)(v >= rc_lo[kW * i + k]) & (int)(v <= rc_hi[kW * i + k]);
+      }
+    inb = and_lanes<P>(inb);
+    return inb ? rc_lp : -__builtin_inf();
+  };
+  auto kd_reg_prior = [&](const double* yv) __attribute__((always_inline)) -> double {
+    if (a.prior_kind == MCG_PRIOR_FLAT) return 0.0;
+    if (a.prior_kind == MCG_PRIOR_DIAG_GAUSS) return kd_reg_gauss_prior(yv);
+    return kd_reg_box_prior(yv);
+  };
+  // the accept of step t (mcmc.ml:42-56) from its proposal's terms, then the kD prefetch into
+  // the step's slot, the bitmap row and the record
+  auto mh_accept = [&](int64_t t, uint64_t T, const int tq, auto par_c, const double* yv, double lly, double lpy,
+                       double lqy, double lf, double lb, double lu) __attribute__((always_inline)) {
+    constexpr int par = decltype(par_c)::value;
+    const double post_y = lly + lpy;
+    const double post_x = ll + lp;
+    const double ratio = ((post_y - post_x) + lb) - lf;
+    const bool acc = lu < ratio;
+    if (acc) {
+#pragma unroll
+      for (int j = 0; j < L::NL; ++j) x[j] = yv[j];
+      ll = lly;
+      lp = lpy;
+      lq = lqy;
+      ++na;
+    }
+    if constexpr (PROP == MCG_PROP_KD_INTERP) {
+      // the box and log q of step t + KDA into this step's slot (its leaf arrived KDA steps
+      // ago), and the leaf of step t + 2 KDA.  Issued after the accept, where the slot's old
+      // log q (this step's lqy) is dead: issued before it, old and new log q were live together,
+      // and the register allocator rotated the slots with copies at the loop latch that waited
+      // for the fresh loads, i.e. for every prefetch in flight
+      kd_load_box(kd_leaf_n[par], std::integral_constant<int, par>{});
+      if constexpr (P == 1) {
+        kd_leaf_n[par] = kd_pick_leaf(T + 2 * KDA);
+      } else {
+        if (tq == 0) pick_own = kd_pick(T + 2 * KDA + (uint64_t)sub);
+        kd_leaf_n[par] = a.kd_pt_leaf[bcast_u32(pick_own, tq)];
+      }
+    }
+    if (a.flags & RUNF_RECORD_ACCEPT) {
+      const uint64_t m = compress_ballot<P>((uint64_t)__ballot(acc && active));
+      const int64_t wave = tid >> 6;
+      if (lane == 0 && wave * (64 / P) < N) {
+        uint8_t* row = a.bits + (a.t0 + t) * a.bits_row_bytes;
+        const int64_t byte = wave * (8 / P);
+        if constexpr (P == 1) *(uint64_t*)(row + byte) = m;
+        else if constexpr (P == 2) *(uint32_t*)(row + byte) = (uint32_t)m;
+        else if constexpr (P == 4) *(uint16_t*)(row + byte) = (uint16_t)m;
+        else row[byte] = (uint8_t)m;
+      }
+    }
+    const int64_t tt1 = a.t0 + t + 1;
+    if (tt1 == next_rec && r < a.rec_end) {
+      record(r);
+      ++r;
+      next_rec += a.nskip;
+    }
+  };
   // one MH step (mcmc.ml:37-56); par: the step's parity, a compile-time slot of the kD prefetch
   auto mh_step = [&](int64_t t, auto par_c) __attribute__((always_inline)) {
     constexpr int par = decltype(par_c)::value;
     const uint64_t T = a.step_base + (uint64_t)t;
+    // t mod P, the step's place in its group of P (staggered draws); a compile-time constant
+    // where the unrolled slots cover whole groups
+    const int tq = (KDA > 1 && KDA % P == 0) ? par % P : (int)(t & (P - 1));
     const uint32_t tlo = (uint32_t)T, thi = (uint32_t)(T >> 32);
     double lf = 0.0, lb = 0.0, lqy = 0.0;
     // Re-read the (tiny, cache-resident) model constants every step: opaque pointers stop the
@@ -982,18 +1132,11 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP, UNI>::kBlock), (MhSh
                   if (L::valid(o, i, k)) yf[L::dim(o, i, k)] = __shfl(y[kW * i + k], (lane & ~(P - 1)) | o, 64);
             lqy = a.kd_logq[kd_find_leaf<D>(a.kd_nodes, a.kd_root, yf)];
           }
+          // consumed here, so the load completes inside this rare branch (left pending at the
+          // join, the wait counts after it lost track of the prefetches in flight)
+          asm volatile("" : "+v"(lqy));
         }
-        // the next step's box and log q go out now (its leaf arrived during this step), and
-        // the leaf of the step after it: their latency hides behind this step's likelihood,
-        // accept and records and the next step's uniforms
-        kd_load_box(kd_leaf_n[par], std::integral_constant<int, par>{});
-        if constexpr (P == 1) {
-          kd_leaf_n[par] = kd_pick_leaf(T + 2 * KDA);
-        } else {
-          const int qk = (int)(t & (P - 1));
-          if (qk == 0) pick_own = kd_pick(T + 2 * KDA + (uint64_t)sub);
-          kd_leaf_n[par] = a.kd_pt_leaf[bcast_u32(pick_own, qk)];
-        }
+        // (the box and log q of step t + KDA go out after this step's accept: kd_prefetch)
         lf = lqy;   // log_jump_prob start proposed = log q(proposed)
         lb = lq;    // log_jump_prob proposed start = log q(start)
       }
@@ -1093,59 +1236,8 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP, UNI>::kBlock), (MhSh
       }
       if constexpr (kKdReg) {
         // eval_lik / eval_prior of the lane's dims on the register constants (the same operations)
-        if constexpr (LIK == MCG_LIK_FLAT) {
-          lly = 0.0;
-        } else {
-          double S;
-          if constexpr (kW == 2) {
-            double e[2];
-#pragma unroll
-            for (int k = 0; k < 2; ++k)
-              e[k] = LIK == MCG_LIK_DIAG_GAUSS ? fma(y[k], rc_i[k], -rc_m[k]) : y[k] - rc_m[k];
-            S = reduce_canon_w2<P>(e[0], e[1], sub);
-          } else {
-            double A[L::NA];
-#pragma unroll
-            for (int j = 0; j < L::NA; ++j) A[j] = 0.0;
-#pragma unroll
-            for (int i = 0; i < L::NCL; ++i)
-#pragma unroll
-              for (int k = 0; k < 4; ++k) {
-                if (!L::valid(sub, i, k)) continue;
-                const double e = LIK == MCG_LIK_DIAG_GAUSS ? fma(y[4 * i + k], rc_i[4 * i + k], -rc_m[4 * i + k])
-                                                           : y[4 * i + k] - rc_m[4 * i + k];
-                A[i % L::NA] = fma(e, e, A[i % L::NA]);
-              }
-            S = reduce_canon<P>(A);
-          }
-          if constexpr (LIK == MCG_LIK_DIAG_GAUSS) {
-            lly = rc_c - 0.5 * S;
-          } else {
-            const double rr = psqrt(S);
-            const double qq = (rr - rc_r) * rc_iw;
-            lly = rc_c - 0.5 * qq * qq;
-          }
-        }
-        if (a.prior_kind == MCG_PRIOR_FLAT) {
-          lpy = 0.0;
-        } else if (a.prior_kind == MCG_PRIOR_DIAG_GAUSS) {
-          typedef const __attribute__((address_space(4))) double kconst;
-          kconst* kpri = (kconst*)a.pri;
-          asm volatile("" : "+s"(kpri));
-          lpy = eval_gauss_prior<D, P, kconst*, kW>(y, sub, a, kpri);
-        } else {
-          int inb = 1;
-#pragma unroll
-          for (int i = 0; i < L::NCL; ++i)
-#pragma unroll
-            for (int k = 0; k < kW; ++k) {
-              if (!L::valid(sub, i, k)) continue;
-              const double v = y[kW * i + k];
-              inb &= (int)(v >= rc_lo[kW * i + k]) & (int)(v <= rc_hi[kW * i + k]);
-            }
-          inb = and_lanes<P>(inb);
-          lpy = inb ? rc_lp : -__builtin_inf();
-        }
+        lly = kd_reg_lik(y);
+        lpy = kd_reg_prior(y);
       } else {
         // likelihood / prior constants through scalar loads (the scalar cache and lgkmcnt, not
         // a per-step vmcnt wait behind the proposal's loads)
@@ -1158,45 +1250,91 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP, UNI>::kBlock), (MhSh
       }
     }
     // ---- Hastings ratio and accept test (mcmc.ml:42-56) ----
-    const double post_y = lly + lpy;
-    const double post_x = ll + lp;
-    const double lu = accept_lu(t, T);
-    const double ratio = ((post_y - post_x) + lb) - lf;
-    const bool acc = lu < ratio;
-    if (acc) {
-#pragma unroll
-      for (int j = 0; j < L::NL; ++j) x[j] = y[j];
-      ll = lly;
-      lp = lpy;
-      lq = lqy;
-      ++na;
-    }
-    if (a.flags & RUNF_RECORD_ACCEPT) {
-      const uint64_t m = compress_ballot<P>((uint64_t)__ballot(acc && active));
-      const int64_t wave = tid >> 6;
-      if (lane == 0 && wave * (64 / P) < N) {
-        uint8_t* row = a.bits + (a.t0 + t) * a.bits_row_bytes;
-        const int64_t byte = wave * (8 / P);
-        if constexpr (P == 1) *(uint64_t*)(row + byte) = m;
-        else if constexpr (P == 2) *(uint32_t*)(row + byte) = (uint32_t)m;
-        else if constexpr (P == 4) *(uint16_t*)(row + byte) = (uint16_t)m;
-        else row[byte] = (uint8_t)m;
-      }
-    }
-    const int64_t tt1 = a.t0 + t + 1;
-    if (tt1 == next_rec && r < a.rec_end) {
-      record(r);
-      ++r;
-      next_rec += a.nskip;
-    }
+    const double lu = accept_lu(tq, T);
+    mh_accept(t, T, tq, par_c, y, lly, lpy, lqy, lf, lb, lu);
   };
-  if constexpr (KDA == 2) {
-    int64_t t = 0;
-    for (; t + 1 < a.nsteps; t += 2) {
-      mh_step(t, std::integral_constant<int, 0>{});
-      mh_step(t + 1, std::integral_constant<int, 1>{});
+  // kD proposal on P > 1 lanes, KDA steps at a time (round 6).  The independence proposal's draw,
+  // its log q and the proposal's likelihood and prior do not depend on the chain state, so the
+  // KDA steps' proposals are evaluated together (branch-free across the steps, the rare face
+  // descents and the prior kind hoisted out: one basic block the scheduler interleaves), then
+  // the KDA accepts run in order.  The same operations as mh_step, step for step.
+  constexpr bool kKdGroup = kKdReg && KDA >= 4 && KDG % P == 0;
+  // group of KDG steps t0 .. t0 + KDG - 1 on prefetch slots B .. B + KDG - 1
+  auto kd_group = [&](int64_t t0, auto b_c) __attribute__((always_inline)) {
+    constexpr int B = decltype(b_c)::value;
+    constexpr int G = KDG;
+    double yg[G][L::NL];
+    double lqg[G], llg[G], lpg[G], lug[G];
+    int stg[G];
+    static_for<G>([&](auto s_c) __attribute__((always_inline)) {
+      constexpr int sl = decltype(s_c)::value;
+      kd_uniforms(a.step_base + (uint64_t)(t0 + sl));
+      bool strict = true;
+#pragma unroll
+      for (int j = 0; j < L::NL; ++j) {
+        yg[sl][j] = 0.0;
+        if (!L::valid(sub, j >> 2, j & 3)) continue;
+        yg[sl][j] = kd_lo[B + sl][j] + (kd_hi[B + sl][j] - kd_lo[B + sl][j]) * kd_u[j];
+        strict = strict && (yg[sl][j] > kd_lo[B + sl][j]) && (yg[sl][j] < kd_hi[B + sl][j]);
+      }
+      stg[sl] = and_lanes<P>(strict ? 1 : 0);
+      lqg[sl] = kd_lqp[B + sl];
+    });
+    static_for<G>([&](auto s_c) __attribute__((always_inline)) {
+      constexpr int sl = decltype(s_c)::value;
+      if (!stg[sl]) {
+        double yf[D];
+#pragma unroll
+        for (int o = 0; o < P; ++o)
+#pragma unroll
+          for (int i = 0; i < L::NCL; ++i)
+#pragma unroll
+            for (int k = 0; k < kW; ++k)
+              if (L::valid(o, i, k)) yf[L::dim(o, i, k)] = __shfl(yg[sl][kW * i + k], (lane & ~(P - 1)) | o, 64);
+        double v = a.kd_logq[kd_find_leaf<D>(a.kd_nodes, a.kd_root, yf)];
+        asm volatile("" : "+v"(v));                     // completes inside the rare branch
+        lqg[sl] = v;
+      }
+    });
+#pragma unroll
+    for (int sl = 0; sl < G; ++sl) llg[sl] = kd_reg_lik(yg[sl]);
+    if (a.prior_kind == MCG_PRIOR_FLAT) {
+#pragma unroll
+      for (int sl = 0; sl < G; ++sl) lpg[sl] = 0.0;
+    } else if (a.prior_kind == MCG_PRIOR_DIAG_GAUSS) {
+#pragma unroll
+      for (int sl = 0; sl < G; ++sl) lpg[sl] = kd_reg_gauss_prior(yg[sl]);
+    } else {
+#pragma unroll
+      for (int sl = 0; sl < G; ++sl) lpg[sl] = kd_reg_box_prior(yg[sl]);
     }
-    if (t < a.nsteps) mh_step(t, std::integral_constant<int, 0>{});
+#pragma unroll
+    for (int sl = 0; sl < G; ++sl) lug[sl] = accept_lu(sl % P, a.step_base + (uint64_t)(t0 + sl));
+    static_for<G>([&](auto s_c) __attribute__((always_inline)) {
+      constexpr int sl = decltype(s_c)::value;
+      // log_jump_prob start proposed = log q(proposed); proposed start = log q(start), the
+      // state after step t0 + sl - 1
+      mh_accept(t0 + sl, a.step_base + (uint64_t)(t0 + sl), sl % P, std::integral_constant<int, B + sl>{}, yg[sl],
+                llg[sl], lpg[sl], lqg[sl], lqg[sl], lq, lug[sl]);
+    });
+  };
+  if constexpr (KDA > 1) {
+    // step t uses prefetch slot t mod KDA: the loop unrolled by KDA, then the last nsteps mod KDA
+    // steps on slots 0, 1, ...
+    int64_t t = 0;
+    if constexpr (kKdGroup) {
+      for (; t + KDA - 1 < a.nsteps; t += KDA)
+        static_for<KDA / KDG>([&](auto g_c) __attribute__((always_inline)) {
+          kd_group(t + decltype(g_c)::value * KDG, std::integral_constant<int, decltype(g_c)::value * KDG>{});
+        });
+    } else {
+      for (; t + KDA - 1 < a.nsteps; t += KDA)
+        static_for<KDA>([&](auto s_c) __attribute__((always_inline)) { mh_step(t + decltype(s_c)::value, s_c); });
+    }
+    const int64_t t_end = t;
+    static_for<KDA - 1>([&](auto s_c) __attribute__((always_inline)) {
+      if (t_end + decltype(s_c)::value < a.nsteps) mh_step(t_end + decltype(s_c)::value, s_c);
+    });
   } else {
     for (int64_t t = 0; t < a.nsteps; ++t) mh_step(t, std::integral_constant<int, 0>{});
   }
