@@ -467,3 +467,40 @@ def test_sharded_kd_interp_equals_single_context(T):
     a = run_gpu(lik, pri, kdp, x0[:, :256], 29, nbin=5, nskip=1, n_rec=30, chain_offset=0)
     b = run_gpu(lik, pri, kdp, x0[:, 256:], 29, nbin=5, nskip=1, n_rec=30, chain_offset=256)
     _assert_shards_equal_full(full, [a, b])
+
+
+@pytest.mark.parametrize("lanes,lik_kind,prior_kind,nbin,nskip,spl", [
+    (4, "diag", "box", 3, 1, 0),          # the C4 shape: groups of 4 steps and a 3-step tail
+    (4, "shell", "open", 5, 3, 7),        # launches of 7 steps: every group offset, tails in each
+    (2, "diag", "flat", 6, 2, 0),         # four dims a lane (P = 2: two group steps per stagger)
+    (2, "flat", "box", 1, 1, 5),
+    (4, "diag", "gauss", 2, 5, 9),
+])
+def test_kd_grouped_step_bit_exact(oracle, T, lanes, lik_kind, prior_kind, nbin, nskip, spl):
+    """Round 6: the kD proposal on P > 1 lanes evaluates four steps' proposals together, then
+    accepts them in order (mh_kernel kd_group).  Step counts that leave tails, launches split at
+    every offset (steps_per_launch), records every 1 / 2 / 3 / 5 steps, each likelihood and prior
+    kind of the register path: records, bitmap, state, counters and tiles equal the oracle's."""
+    D = 8
+    rng = np.random.default_rng(90 + lanes + nbin)
+    pts = rng.normal(size=(1500, D))
+    lo, hi = -4.0 * np.ones(D), 4.0 * np.ones(D)
+    kd, okd = T.KdInterp(pts, lo, hi), oracle.KdTree(pts, lo, hi)
+    if lik_kind == "diag":
+        lik = T.diag_gauss(rng.uniform(-0.5, 0.5, D), rng.uniform(0.7, 1.5, D))
+    elif lik_kind == "shell":
+        lik = T.gauss_shell(np.zeros(D), 1.5, 0.5)
+    else:
+        lik = T.flat(D)
+    if prior_kind == "box":
+        pri = T.box(-3.5 * np.ones(D), 3.5 * np.ones(D))
+    elif prior_kind == "open":
+        pri = T.box(-3.0 * np.ones(D), 3.2 * np.ones(D), open_=True)
+    elif prior_kind == "gauss":
+        pri = T.gauss_prior(np.zeros(D), 2.0 * np.ones(D))
+    else:
+        pri = T.flat_prior()
+    x0 = rng.uniform(-1.0, 1.0, size=(D, 320))
+    g = run_gpu(lik, pri, kd, x0, 5, nbin=nbin, nskip=nskip, n_rec=23, lanes=lanes, spl=spl)
+    o = run_oracle(oracle, lik, pri, kd, x0, 5, nbin, nskip, 23, kd=okd)
+    assert_same(g, o)
