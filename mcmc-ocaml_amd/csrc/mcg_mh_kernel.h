@@ -54,6 +54,11 @@ __device__ __forceinline__ void static_for(F&& f) {
 #define MCG_KD_AHEAD 4
 #endif
 constexpr int kKdAhead = MCG_KD_AHEAD;
+// non-kD steps on P > 1 lanes unrolled by P (MCG_STEP_UNROLL=1)
+#ifndef MCG_STEP_UNROLL
+#define MCG_STEP_UNROLL 0
+#endif
+constexpr bool kStepUnroll = MCG_STEP_UNROLL != 0;
 
 // the width of a chain's lane blocks: two dims per lane where the kD proposal runs on D = 2P lanes
 template <int D, int P, int PROP>
@@ -921,12 +926,13 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP, UNI>::kBlock), (MhSh
     }
   };
   // one MH step (mcmc.ml:37-56); par: the step's parity, a compile-time slot of the kD prefetch
-  auto mh_step = [&](int64_t t, auto par_c) __attribute__((always_inline)) {
+  auto mh_step = [&](int64_t t, auto par_c, auto q_c) __attribute__((always_inline)) {
     constexpr int par = decltype(par_c)::value;
+    constexpr int kq = decltype(q_c)::value;           // t mod P when the caller knows it, else -1
     const uint64_t T = a.step_base + (uint64_t)t;
     // t mod P, the step's place in its group of P (staggered draws); a compile-time constant
     // where the unrolled slots cover whole groups
-    const int tq = (KDA > 1 && KDA % P == 0) ? par % P : (int)(t & (P - 1));
+    const int tq = kq >= 0 ? kq : (KDA > 1 && KDA % P == 0) ? par % P : (int)(t & (P - 1));
     const uint32_t tlo = (uint32_t)T, thi = (uint32_t)(T >> 32);
     double lf = 0.0, lb = 0.0, lqy = 0.0;
     // Re-read the (tiny, cache-resident) model constants every step: opaque pointers stop the
@@ -1329,14 +1335,27 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP, UNI>::kBlock), (MhSh
         });
     } else {
       for (; t + KDA - 1 < a.nsteps; t += KDA)
-        static_for<KDA>([&](auto s_c) __attribute__((always_inline)) { mh_step(t + decltype(s_c)::value, s_c); });
+        static_for<KDA>([&](auto s_c) __attribute__((always_inline)) {
+          mh_step(t + decltype(s_c)::value, s_c, std::integral_constant<int, -1>{});
+        });
     }
     const int64_t t_end = t;
     static_for<KDA - 1>([&](auto s_c) __attribute__((always_inline)) {
-      if (t_end + decltype(s_c)::value < a.nsteps) mh_step(t_end + decltype(s_c)::value, s_c);
+      if (t_end + decltype(s_c)::value < a.nsteps)
+        mh_step(t_end + decltype(s_c)::value, s_c, std::integral_constant<int, -1>{});
     });
+  } else if constexpr (kStepUnroll && P > 1) {
+    // the loop unrolled by P: each step's place in its group of P (staggered accept uniforms) is
+    // a compile-time constant
+    int64_t t = 0;
+    for (; t + P - 1 < a.nsteps; t += P)
+      static_for<P>([&](auto s_c) __attribute__((always_inline)) {
+        mh_step(t + decltype(s_c)::value, std::integral_constant<int, 0>{}, s_c);
+      });
+    for (; t < a.nsteps; ++t) mh_step(t, std::integral_constant<int, 0>{}, std::integral_constant<int, -1>{});
   } else {
-    for (int64_t t = 0; t < a.nsteps; ++t) mh_step(t, std::integral_constant<int, 0>{});
+    for (int64_t t = 0; t < a.nsteps; ++t)
+      mh_step(t, std::integral_constant<int, 0>{}, std::integral_constant<int, -1>{});
   }
 
   if (!active) return;
