@@ -878,7 +878,8 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP, UNI>::kBlock), (MhSh
   // the accept of step t (mcmc.ml:42-56) from its proposal's terms, then the kD prefetch into
   // the step's slot, the bitmap row and the record
   auto mh_accept = [&](int64_t t, uint64_t T, const int tq, auto par_c, const double* yv, double lly, double lpy,
-                       double lqy, double lf, double lb, double lu) __attribute__((always_inline)) {
+                       double lqy, double lf, double lb, double lu, auto rec_c,
+                       auto pick_c) __attribute__((always_inline)) {
     constexpr int par = decltype(par_c)::value;
     const double post_y = lly + lpy;
     const double post_x = ll + lp;
@@ -902,7 +903,10 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP, UNI>::kBlock), (MhSh
       if constexpr (P == 1) {
         kd_leaf_n[par] = kd_pick_leaf(T + 2 * KDA);
       } else {
-        if (tq == 0) pick_own = kd_pick(T + 2 * KDA + (uint64_t)sub);
+        // (pick_c: the caller drew this group's picks ahead, kd_group)
+        if constexpr (!decltype(pick_c)::value) {
+          if (tq == 0) pick_own = kd_pick(T + 2 * KDA + (uint64_t)sub);
+        }
         kd_leaf_n[par] = a.kd_pt_leaf[bcast_u32(pick_own, tq)];
       }
     }
@@ -918,11 +922,13 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP, UNI>::kBlock), (MhSh
         else row[byte] = (uint8_t)m;
       }
     }
-    const int64_t tt1 = a.t0 + t + 1;
-    if (tt1 == next_rec && r < a.rec_end) {
-      record(r);
-      ++r;
-      next_rec += a.nskip;
+    if constexpr (decltype(rec_c)::value) {
+      const int64_t tt1 = a.t0 + t + 1;
+      if (tt1 == next_rec && r < a.rec_end) {
+        record(r);
+        ++r;
+        next_rec += a.nskip;
+      }
     }
   };
   // one MH step (mcmc.ml:37-56); par: the step's parity, a compile-time slot of the kD prefetch
@@ -1257,7 +1263,7 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP, UNI>::kBlock), (MhSh
     }
     // ---- Hastings ratio and accept test (mcmc.ml:42-56) ----
     const double lu = accept_lu(tq, T);
-    mh_accept(t, T, tq, par_c, y, lly, lpy, lqy, lf, lb, lu);
+    mh_accept(t, T, tq, par_c, y, lly, lpy, lqy, lf, lb, lu, std::true_type{}, std::false_type{});
   };
   // kD proposal on P > 1 lanes, KDA steps at a time (round 6).  The independence proposal's draw,
   // its log q and the proposal's likelihood and prior do not depend on the chain state, so the
@@ -1286,6 +1292,11 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP, UNI>::kBlock), (MhSh
       stg[sl] = and_lanes<P>(strict ? 1 : 0);
       lqg[sl] = kd_lqp[B + sl];
     });
+    // the picks of steps t0 + 2 KDA .. (staggered: lane sub draws step t0 + 2 KDA + q P + sub for
+    // the q-th group of P steps), drawn here beside the other draws instead of inside the accepts
+    uint32_t pickg[G / P > 0 ? G / P : 1];
+#pragma unroll
+    for (int q = 0; q < G / P; ++q) pickg[q] = kd_pick(a.step_base + (uint64_t)(t0 + 2 * KDA + q * P + sub));
     static_for<G>([&](auto s_c) __attribute__((always_inline)) {
       constexpr int sl = decltype(s_c)::value;
       if (!stg[sl]) {
@@ -1316,13 +1327,64 @@ __global__ void __launch_bounds__((MhShape<D, P, LIK, PROP, UNI>::kBlock), (MhSh
     }
 #pragma unroll
     for (int sl = 0; sl < G; ++sl) lug[sl] = accept_lu(sl % P, a.step_base + (uint64_t)(t0 + sl));
-    static_for<G>([&](auto s_c) __attribute__((always_inline)) {
-      constexpr int sl = decltype(s_c)::value;
-      // log_jump_prob start proposed = log q(proposed); proposed start = log q(start), the
-      // state after step t0 + sl - 1
-      mh_accept(t0 + sl, a.step_base + (uint64_t)(t0 + sl), sl % P, std::integral_constant<int, B + sl>{}, yg[sl],
-                llg[sl], lpg[sl], lqg[sl], lqg[sl], lq, lug[sl]);
-    });
+    // every step of the group records, and only into the moments and harmonic-mean partials (the
+    // C4 shape): the G accepts run back to back, then the G records from the states they left --
+    // the same updates in the same order as record() after each step, without a branch between
+    // the accepts
+    const bool rec_all = accum && (a.flags & (RUNF_RECORD_X | RUNF_RECORD_LLP)) == 0 && a.nskip == 1 &&
+                         next_rec == a.t0 + t0 + 1 && r + G <= a.rec_end;
+    if (rec_all) {
+      double xs[G][L::NL], lls[G];
+      static_for<G>([&](auto s_c) __attribute__((always_inline)) {
+        constexpr int sl = decltype(s_c)::value;
+        // log_jump_prob start proposed = log q(proposed); proposed start = log q(start), the
+        // state after step t0 + sl - 1
+        if constexpr (sl % P == 0) pick_own = pickg[sl / P];
+        mh_accept(t0 + sl, a.step_base + (uint64_t)(t0 + sl), sl % P, std::integral_constant<int, B + sl>{},
+                  yg[sl], llg[sl], lpg[sl], lqg[sl], lqg[sl], lq, lug[sl], std::false_type{}, std::true_type{});
+#pragma unroll
+        for (int j = 0; j < L::NL; ++j) xs[sl][j] = x[j];
+        lls[sl] = ll;
+      });
+#pragma unroll
+      for (int sl = 0; sl < G; ++sl) {
+        const double inv = inv_pf;                     // 1/(R+1), host IEEE division
+        inv_pf = welford_weight(a, r + sl + 1 - a.next_r0);
+#pragma unroll
+        for (int i = 0; i < L::NCL; ++i)
+#pragma unroll
+          for (int k = 0; k < kW; ++k) {
+            if (!L::valid(sub, i, k)) continue;
+            if constexpr (!ACfg::kLds && !ACfg::kReg) { if (!active) continue; }
+            double& mu = acc_mean(i, k);
+            double& m2 = acc_m2(i, k);
+            const double xv = xs[sl][kW * i + k];
+            const double delta = xv - mu;
+            const double mnew = fma(delta, inv, mu);
+            m2 = fma(delta, xv - mnew, m2);
+            mu = mnew;
+          }
+      }
+#pragma unroll
+      for (int sl = 0; sl < G; ++sl) {
+        const int64_t R = r + sl;
+        const int jr = (int)(R & (P - 1));
+        if (sub == jr) {
+          hm_pv = -lls[sl];
+          hm_pok = true;
+        }
+        if (jr == P - 1) hm_flush(R - (P - 1));
+      }
+      r += G;
+      next_rec += G;
+    } else {
+      static_for<G>([&](auto s_c) __attribute__((always_inline)) {
+        constexpr int sl = decltype(s_c)::value;
+        if constexpr (sl % P == 0) pick_own = pickg[sl / P];
+        mh_accept(t0 + sl, a.step_base + (uint64_t)(t0 + sl), sl % P, std::integral_constant<int, B + sl>{},
+                  yg[sl], llg[sl], lpg[sl], lqg[sl], lqg[sl], lq, lug[sl], std::true_type{}, std::true_type{});
+      });
+    }
   };
   if constexpr (KDA > 1) {
     // step t uses prefetch slot t mod KDA: the loop unrolled by KDA, then the last nsteps mod KDA
