@@ -504,3 +504,53 @@ def test_kd_grouped_step_bit_exact(oracle, T, lanes, lik_kind, prior_kind, nbin,
     g = run_gpu(lik, pri, kd, x0, 5, nbin=nbin, nskip=nskip, n_rec=23, lanes=lanes, spl=spl)
     o = run_oracle(oracle, lik, pri, kd, x0, 5, nbin, nskip, 23, kd=okd)
     assert_same(g, o)
+
+
+@pytest.mark.parametrize("lanes,prior_kind,nbin,spl,appends", [
+    (4, "box", 0, 0, 2),       # the C4 shape: record 0 is the start state, so records run one off
+    (4, "gauss", 3, 7, 1),     # burn-in, then groups at every offset in launches of 7 steps
+    (2, "box", 2, 0, 3),       # four dims a lane
+])
+def test_kd_grouped_records_bit_exact(oracle, T, lanes, prior_kind, nbin, spl, appends):
+    """Round 6: when every step of a kD group records only into the moments and harmonic-mean
+    partials (no recorded rows -- the C4 bench's shape), the group runs its accepts first, then
+    its records.  Moments / harmonic-mean tiles, accept bitmap, state and counters equal the
+    oracle's over appended runs (record indices offset against the groups)."""
+    from mcmc_amd import Context
+    D, N = 8, 320
+    rng = np.random.default_rng(7 + lanes + nbin)
+    pts = rng.normal(size=(1200, D))
+    lo, hi = -4.0 * np.ones(D), 4.0 * np.ones(D)
+    kd, okd = T.KdInterp(pts, lo, hi), oracle.KdTree(pts, lo, hi)
+    lik = T.diag_gauss(rng.uniform(-0.5, 0.5, D), rng.uniform(0.7, 1.5, D))
+    pri = T.box(-3.5 * np.ones(D), 3.5 * np.ones(D)) if prior_kind == "box" else \
+        T.gauss_prior(np.zeros(D), 2.0 * np.ones(D))
+    x0 = rng.uniform(-1.0, 1.0, size=(D, N))
+    n_rec = 21
+    ctx = Context(seed=9, lanes_per_chain=lanes, steps_per_launch=spl)
+    ctx.set_model(lik, pri, kd)
+    ctx.init(x0)
+    ctx.run(nbin=nbin, nskip=1, n_rec=n_rec, record_x=False, record_llp=False, record_accept=True,
+            accumulate=True)
+    bits = [ctx.records(x=False, llp=False, accept=True)[3]]
+    for _ in range(appends - 1):
+        ctx.run(nbin=0, nskip=1, n_rec=n_rec, record_x=False, record_llp=False, record_accept=True,
+                accumulate=True, append=True)
+        bits.append(ctx.records(x=False, llp=False, accept=True)[3])
+    x, ll, lp = ctx.state()
+    acc, rej = ctx.counters()
+    tiles = ctx.tile_stats()
+    ctx.close()
+    # the oracle: one run of the same total steps (appended runs continue the record count)
+    m = oracle.Model(D, lik.kind, lik.params, pri.kind, pri.params, 3, [0.0], okd)
+    ll0 = np.array([m.loglik(x0[:, i]) for i in range(N)])
+    lp0 = np.array([m.logprior(x0[:, i]) for i in range(N)])
+    total = n_rec * appends
+    o = oracle.mh_run(m, 9, x0, ll0, lp0, nbin=nbin, nskip=1, n_rec=total, record_x=False, record_llp=False,
+                      nthreads=8)
+    np.testing.assert_array_equal(x, o["x"])
+    np.testing.assert_array_equal(ll, o["ll"])
+    np.testing.assert_array_equal(lp, o["lp"])
+    assert acc == int(o["nacc"].sum())
+    np.testing.assert_array_equal(np.concatenate(bits, axis=0), o["bits"])
+    np.testing.assert_array_equal(tiles, oracle.tile_stats(D, N, total, o))
